@@ -1,0 +1,218 @@
+"""Benchmark: samples/s through the K=15 D-LADMM forward (m=256, n=512) on MI355X.
+
+Workload (BASELINE.json configs[1]/north_star): the reference's V4 model
+(main_syn_l1l1_scalar.py:34-131) at m=256, n=512, K=15, B=65,536 columns per GPU, synthetic inputs
+with the gen_syn_data.py distribution generated on device, reference-init parameters.  One "step"
+= one complete forward with every layer's Z, E, L and T written (the reference's return lists),
+the per-layer L1L1 objective of the training loop fused in, and (N > 1) one RCCL all-reduce of
+the [K, 2] objective sums.  Batch is sharded across ranks (weak scaling: B per GPU fixed).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
+
+Prints ONE JSON line (rank 0).  Roofline of the dominant kernel (the fused K-layer kernel):
+algorithmic FLOP per launch (4K+2)*m*n*B over its average duration measured here with
+HIP events recorded on the launch stream around the kernel itself; peak = 157.3 TF/s fp32 MFMA.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "samples/sec through d=15 D-LADMM forward (m=256,n=512); %HBM-roofline"
+PEAK_F32_MFMA = 157.3e12   # MI355X_MICROARCH.md: fp32 matrix 157.3 TF/s (spec; 155 measured)
+PEAK_HBM = 8.0e12          # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=65536, help="columns per GPU")
+    ap.add_argument("--m", type=int, default=256)
+    ap.add_argument("--n", type=int, default=512)
+    ap.add_argument("--layers", type=int, default=15)
+    ap.add_argument("--alpha", type=float, default=0.001)
+    ap.add_argument("--lean", action="store_true", help="write only the last layer (not default)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=8192, help="columns of the CPU sample")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def synth(m, n, B, seed, dev):
+    """gen_syn_data.py:14-47 distribution on device: A column-normalised N(0,1) (same on every
+    rank), Z*, E* Bernoulli(0.1)*N(0,1), X = A Z* + E*; Z0 = U(0,1)/n, E0 = L0 = 0."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(1126)
+    A = torch.randn(m, n, generator=g, device=dev)
+    A = A / A.pow(2).sum(0, keepdim=True).sqrt()
+    g.manual_seed(1126 + 7919 * (seed + 1))
+    zs = (torch.rand(n, B, generator=g, device=dev) < 0.1) * torch.randn(n, B, generator=g,
+                                                                        device=dev)
+    es = (torch.rand(m, B, generator=g, device=dev) < 0.1) * torch.randn(m, B, generator=g,
+                                                                        device=dev)
+    X = (A @ zs + es).contiguous()
+    Z0 = torch.rand(n, B, generator=g, device=dev) / n
+    E0 = torch.zeros(m, B, device=dev)
+    L0 = torch.zeros(m, B, device=dev)
+    del zs, es
+    return A, X, Z0, E0, L0
+
+
+def cpu_baseline(m, n, K, B):
+    """The oracle (CPU restatement of the reference forward, numpy fp32 + BLAS) on a bounded
+    sample of the same workload: B columns, median of 3 forwards after 1 warmup."""
+    from oracle import dladmm_oracle as oracle
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import problems
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max((d.get("num_threads", 1) for d in threadpool_info()
+                     if d.get("user_api") == "blas"), default=1)
+    except Exception:  # pragma: no cover
+        cores = os.cpu_count()
+    inp = problems.make_inputs(m, n, B, 1126)
+    sd = problems.make_state_dict("v4", m, n, B, K, inp["A"], 1126)
+    args = ("v4", inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd, K)
+    oracle.forward(*args)
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        oracle.forward(*args)
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    return {"value": B / t, "unit": "samples/s", "cores": int(cores), "kind": "port",
+            "sample": f"oracle/dladmm_oracle.py V4 forward, m={m} n={n} K={K}, B={B} columns, "
+                      f"fp32 numpy+BLAS, median of 3 after 1 warmup ({t*1e3:.0f} ms/forward)"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")  # RCCL on ROCm
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+    dl = importlib.import_module("d-ladmm_amd")
+
+    m, n, K, B = a.m, a.n, a.layers, a.batch
+    A, X, Z0, E0, L0 = synth(m, n, B, rank, dev)
+    net = dl.DLADMMNetScalar(m=m, n=0, d=n, batch_size=B, A=A, Z0=Z0, E0=E0, L0=L0, layers=K)
+    net.requires_grad_(False)
+    keep_all = not a.lean
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.steps)]
+    for e in ev:
+        e.record()  # torch creates the hipEvent lazily; make the handles exist
+    torch.cuda.synchronize()
+
+    def step(evpair=None):
+        r = net.run(X, keep_all=keep_all, loss_kind=dl._lib.LOSS_L1L1, kernel_events=evpair)
+        sums = r.loss_sums
+        if world > 1:
+            dist.all_reduce(sums)  # one RCCL all-reduce of the [K, 2] objective sums over xGMI
+        return r, sums
+
+    with torch.no_grad():
+        for _ in range(a.warmup):
+            r, sums = step()
+            del r
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            r, sums = step((ev[2 * i], ev[2 * i + 1]))
+            del r
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kern_ms = [ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(a.steps)]
+    kern_avg = float(np.mean(kern_ms)) * 1e-3
+    if world > 1:
+        tt = torch.tensor([elapsed, kern_avg], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, kern_avg = float(tt[0]), float(tt[1])
+    obj = ((a.alpha * sums[:, 0] + sums[:, 1]) / (B * world)).cpu().numpy()
+
+    if rank == 0:
+        total = B * world * a.steps
+        value = total / elapsed
+        flop = (4 * K + 2) * m * n * B                      # per launch (one rank's shard)
+        achieved = flop / kern_avg
+        # algorithmic HBM bytes per sample (SURVEY 8d, V4 API-parity): inputs X,Z0,E0,L0 +
+        # outputs Z,E,L (K layers) + T (K+1); weights (K+1)*m*n*4 per launch
+        bytes_io = 4 * ((m + n + 2 * m) + K * (n + 2 * m) + (K + 1) * m) if keep_all else \
+            4 * ((m + n + 2 * m) + (n + 3 * m))
+        bytes_launch = bytes_io * B + (K + 1) * m * n * 4
+        traffic = None
+        if os.path.exists(a.traffic_json):
+            try:
+                tj = json.load(open(a.traffic_json))
+                if tj.get("workload") == f"v4 m={m} n={n} K={K} B={B} keep_all={int(keep_all)}":
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        res = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (gen_syn_data.py distribution generated on device; reference-init "
+                    "V4 parameters, random W = 0.4(A^T + 1e-3 N))",
+            "config": {
+                "workload": f"DLADMMNet_scalar (V4) forward m={m} n={n} K={K} B={B}/GPU, all "
+                            f"layers' Z/E/L/T written{'' if keep_all else ' (lean: last only)'} + "
+                            "fused per-layer L1L1 objective",
+                "variant": "v4", "m": m, "n": n, "layers": K, "batch_per_gpu": B,
+                "global_batch": B * world, "keep_all": keep_all,
+                "parallelism": f"batch-shard dp{world} (one RCCL all-reduce of [K,2] sums)",
+            },
+            "roofline": {
+                "bound": "mfma",
+                "achieved": achieved / 1e12,
+                "peak": PEAK_F32_MFMA / 1e12,
+                "unit": "TFLOP/s",
+                "frac": achieved / PEAK_F32_MFMA,
+                "traffic": traffic,
+                "kernel": "dladmm::fused_kernel<256,512,VVAR,SCALAR>",
+                "kernel_ms": kern_avg * 1e3,
+                "flop_per_launch": flop,
+                "algorithmic_bytes_per_launch": bytes_launch,
+                "hbm_frac_algorithmic": bytes_launch / kern_avg / PEAK_HBM,
+            },
+            "objective_last_layer": float(obj[-1]),
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(m, n, K, a.cpu_batch)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,101 @@
+"""ctypes binding of the C ABI in include/dladmm.h (libdladmm_hip.so, built in-tree).
+
+No torch types cross this boundary: the descriptor carries raw device pointers, sizes and leading
+dimensions; the stream is a hipStream_t passed as an integer.  The library is loaded lazily and
+loading failures raise -- there is no fallback path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libdladmm_hip.so")
+
+ABI_VERSION = 1
+MAX_LAYERS = 64
+NSCALAR = 8
+
+# enum dladmm_variant
+V1_LENA, V2_LTHETA, V3_FULL, V4_SCALAR, V5_TIED, V6_LASSO = 1, 2, 3, 4, 5, 6
+# enum dladmm_loss_kind
+LOSS_NONE, LOSS_L1L1, LOSS_LASSO = 0, 1, 2
+# enum dladmm_param_slot
+P_BETA1, P_BETA2, P_BETA3, P_SS2, P_SS2B, P_THETA_E, P_THETA_Z, P_S1 = range(8)
+
+# every symbol include/dladmm.h declares (checked by tests/test_capi.py)
+EXPORTED = ("dladmm_abi_version", "dladmm_fwd_workspace_bytes", "dladmm_fwd_path",
+            "dladmm_fwd_f32", "dladmm_error_string")
+
+_fp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+
+
+class FwdDesc(ctypes.Structure):
+    """Mirror of `struct dladmm_fwd_desc` (include/dladmm.h)."""
+    _fields_ = [
+        ("abi_version", _i32), ("variant", _i32), ("m", _i32), ("n", _i32),
+        ("batch", _i32), ("layers", _i32), ("keep_all", _i32), ("loss_kind", _i32),
+        ("X", _fp), ("ld_x", _i64),
+        ("A", _fp), ("ld_a", _i64),
+        ("Z0", _fp), ("ld_z0", _i64),
+        ("E0", _fp), ("ld_e0", _i64),
+        ("L0", _fp), ("ld_l0", _i64),
+        ("W", ctypes.POINTER(_fp)), ("ld_w", _i64),
+        ("scalar_params", _fp),
+        ("row_params", _fp), ("row_stride", _i64),
+        ("beta1_elem", ctypes.POINTER(_fp)),
+        ("beta2_elem", ctypes.POINTER(_fp)),
+        ("ld_beta", _i64),
+        ("Z", _fp), ("E", _fp), ("L", _fp), ("T", _fp),
+        ("ld_out", _i64),
+        ("loss_sums", _fp),
+        ("workspace", _fp), ("workspace_bytes", ctypes.c_size_t),
+        ("ev_kernel_start", _fp), ("ev_kernel_stop", _fp),
+    ]
+
+
+_LIB = None
+
+
+def lib():
+    """Load libdladmm_hip.so (after torch, so it binds torch's HIP runtime by SONAME)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"dladmm: HIP library not built ({LIB_PATH} missing); run "
+            "`python -c 'import __graft_entry__ as g; g.build()'` or `make -C d-ladmm_amd`")
+    import torch  # noqa: F401  -- makes torch's libamdhip64 the process-wide HIP runtime
+    L = ctypes.CDLL(LIB_PATH)
+    L.dladmm_abi_version.restype = ctypes.c_int
+    L.dladmm_abi_version.argtypes = []
+    L.dladmm_fwd_workspace_bytes.restype = ctypes.c_size_t
+    L.dladmm_fwd_workspace_bytes.argtypes = [ctypes.POINTER(FwdDesc)]
+    L.dladmm_fwd_path.restype = ctypes.c_int
+    L.dladmm_fwd_path.argtypes = [ctypes.POINTER(FwdDesc)]
+    L.dladmm_fwd_f32.restype = ctypes.c_int
+    L.dladmm_fwd_f32.argtypes = [ctypes.POINTER(FwdDesc), ctypes.c_void_p]
+    L.dladmm_error_string.restype = ctypes.c_char_p
+    L.dladmm_error_string.argtypes = [ctypes.c_int]
+    if L.dladmm_abi_version() != ABI_VERSION:
+        raise RuntimeError("dladmm: library ABI version mismatch; rebuild")
+    _LIB = L
+    return L
+
+
+def check(code: int):
+    if code != 0:
+        msg = lib().dladmm_error_string(code).decode()
+        if code < 0:
+            raise ValueError(f"{msg} (code {code})")
+        raise RuntimeError(f"dladmm HIP error: {msg} (code {code})")
+
+
+def ptr_array(ptrs):
+    arr = (_fp * max(len(ptrs), 1))()
+    for i, p in enumerate(ptrs):
+        arr[i] = p
+    return arr

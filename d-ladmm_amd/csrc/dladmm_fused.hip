@@ -1,0 +1,717 @@
+// dladmm_fused.hip -- MI355X (gfx950 / CDNA4) fused K-layer D-LADMM forward.
+//
+// Replaces the Python loop of DLADMMNet.forward (main_lena.py:57-98,
+// main_syn_l1l1_scalar.py:80-127, main_syn_lasso_scalar.py:65-114 and the other variants
+// listed in include/dladmm.h) with ONE persistent-state kernel per forward.
+//
+// Design (DESIGN.md has the full derivation):
+//  * one workgroup = 4 waves = a tile of 64 batch columns; wave w owns columns 16w..16w+15;
+//  * the whole per-column state -- Z (n), E, L, X and T/Var (m each) -- stays in registers for
+//    all K layers, laid out exactly like the C/D fragment of v_mfma_f32_16x16x4_f32:
+//    lane l holds column (l & 15) and feature rows 16*b + 4*(l >> 4) + r, r = 0..3;
+//  * with that layout the accumulator of one GEMM IS the B operand of the next: U = W_k*Var
+//    lands in Z's layout, P = A*Z lands in E/L/T's layout, and every shrink / AXPY of the
+//    reference is lane-local -- no LDS transpose, no HBM round trip for the state;
+//  * W_k and A are pre-packed (pack_frags_kernel) into "fragment order" (1 KiB per 16x16
+//    fragment = exactly what one wave's lanes need for 4 MFMAs), streamed from L2/MALL by
+//    global_load_lds_dwordx4 into a double-buffered LDS ring shared by the 4 waves;
+//  * epilogues are deferred by one block so each block's HBM stores overlap the next block's
+//    MFMAs instead of being drained by the next ring barrier.
+// Elementwise arithmetic keeps the reference's evaluation order and is compiled with
+// -ffp-contract=off so every mul/add rounds like the separate torch ops do.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dladmm.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace dladmm {
+
+enum { EM_V1 = 0, EM_VVAR = 1, EM_LASSO = 2 };   // E-step form
+enum { PK_SCALAR = 0, PK_ROW = 1, PK_ELEM = 2 };  // parameter broadcast class
+
+constexpr int kWaves = 4;
+constexpr int kTileCols = 16 * kWaves;  // batch columns per workgroup
+constexpr int kFrag = 256;              // floats per packed 16x16 fragment (1 KiB)
+
+struct FusedArgs {
+  int m, n, B, K;
+  int keep_all, loss_kind, nwaves;
+  int pad0;
+  const float* X;  int64_t ldx;
+  const float* Z0; int64_t ldz0;
+  const float* E0; int64_t lde0;
+  const float* L0; int64_t ldl0;
+  const float* Ap;   // packed A   [MB][NB] fragments
+  const float* Wp;   // packed W_k [K][NB][MB] fragments
+  const float* scal; // [K][8]
+  const float* rowp; int64_t rstride;  // [K][8][rstride]
+  int64_t ldb;
+  const float* b1e[DLADMM_MAX_LAYERS];
+  const float* b2e[DLADMM_MAX_LAYERS];
+  float* Zo; float* Eo; float* Lo; float* To; int64_t ldo;
+  float* lossp;      // [K][2][nwaves]
+};
+
+// literal relu(x - th) - relu(-1.0*x - th) (main_lena.py:52-53); NaN propagates like torch relu
+__device__ __forceinline__ float relu_(float v) { return (v <= 0.0f) ? 0.0f : v; }
+__device__ __forceinline__ float shrink(float x, float th) {
+  return relu_(x - th) - relu_(-x - th);
+}
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void glds16(const float* gsrc, f32x4* ldst) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)gsrc,
+                                   (void __attribute__((address_space(3)))*)ldst, 16, 0, 0);
+}
+
+// All waves: own LDS-DMA + LDS reads complete, then workgroup barrier.  One opaque statement,
+// so the compiler can neither hoist ring reads above it nor sink earlier ones below it.
+__device__ __forceinline__ void ring_barrier() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Pin a value to the accumulation register file (AGPR).  The MFMA operands Z and Var live
+// there for the whole forward (MFMA srcA/srcB may be AGPRs on gfx950), leaving the 256 arch
+// VGPRs for E, L, fragments and epilogue temporaries.
+__device__ __forceinline__ void pin_agpr(float& x) { asm volatile("" : "+a"(x)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int MP, int NP, int EMODE, int PKIND>
+struct Fused {
+  static constexpr int MB = MP / 16;
+  static constexpr int NB = NP / 16;
+  static constexpr int GF = MB * NB;                // fragments per GEMM
+  static constexpr int CF = GF < 16 ? GF : 16;      // fragments per ring chunk
+  static constexpr int NCH = GF / CF;               // chunks per GEMM
+  static constexpr int TAB = 6 * MP + NP;           // per-row param table (floats)
+  static constexpr int RING_F4 = 2 * CF * 64;
+  static constexpr int TAB_F4 = (PKIND == PK_ROW) ? (3 * TAB) / 4 : 0;  // 3 layer buffers
+  static_assert(MP % 16 == 0 && NP % 16 == 0, "padded dims must be multiples of 16");
+  static_assert(GF % CF == 0, "chunking");
+  static_assert(TAB % 4 == 0, "table alignment");
+};
+
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+constexpr uint32_t kOOB = 0x80000000u;  // lane offset that is out of range for every buffer
+
+// raw buffer resource; accesses at byte offsets >= bytes are dropped (stores) / read 0 (loads)
+__device__ __forceinline__ rsrc_t mkrsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float bload(rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ void bstore(rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)off, 0, 0);
+}
+typedef const __attribute__((address_space(4))) float* cfloat_p;  // scalar-loaded
+
+// Byte offset walker over the rows 16b + 4g + r of a [rows][ld] matrix, one block at a time.
+// The running offset is made opaque after every step so the compiler cannot precompute (and
+// keep live) one offset register per row of the unrolled layer body.
+struct Walk {
+  uint32_t cur, ld4;
+  __device__ __forceinline__ uint32_t at(int r) const { return cur + (uint32_t)r * ld4; }
+  __device__ __forceinline__ void next() {
+    cur += 16u * ld4;
+    asm volatile("" : "+v"(cur));
+  }
+};
+
+template <int MP, int NP, int EMODE, int PKIND>
+__global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
+  using F = Fused<MP, NP, EMODE, PKIND>;
+  constexpr int MB = F::MB, NB = F::NB, CF = F::CF, NCH = F::NCH, TAB = F::TAB;
+  __shared__ f32x4 smem[F::RING_F4 + F::TAB_F4];
+  f32x4* ring = smem;
+  float* tab = reinterpret_cast<float*>(smem + F::RING_F4);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t col = (int64_t)blockIdx.x * kTileCols + w * 16 + j;
+  const bool cv = col < a.B;
+  const int m = a.m, n = a.n, K = a.K;
+  const bool lossz = a.loss_kind != 0;
+  const bool lasso = a.loss_kind == DLADMM_LOSS_LASSO;
+
+  // per-lane byte offset of (row 4g, column col) in a [rows][ld] fp32 matrix; kOOB for padding
+  auto lane_off = [&](int64_t ld) -> uint32_t {
+    return cv ? (uint32_t)((col + (int64_t)(4 * g) * ld) * 4) : kOOB;
+  };
+
+  float Zr[NB][4], Er[MB][4], Lr[MB][4], Vr[MB][4];
+  float pb[3][4];  // prefetched per-element betas (PK_ELEM) for the pending G2 block
+  float px[4];     // prefetched X rows of the pending G2 block (X is re-read, not resident)
+  float regsum = 0.f, fitsum = 0.f;
+
+  // ---------------------------------------------------------------- ring (LDS-DMA) stream
+  int cur = 0;  // slot of the chunk being consumed
+  auto issue = [&](const float* src, int slot) {
+    // opaque uniform base: stops the compiler from precomputing (and keeping live) the
+    // 64-bit per-lane address of every chunk of the stream; the load becomes
+    // global_load_lds_dwordx4 voff, s[base] with a loop-invariant 32-bit lane offset
+    uint64_t sb = (uint64_t)src;
+    asm volatile("" : "+s"(sb));
+    const float* base = (const float*)sb;
+    f32x4* dst = ring + slot * (CF * 64);
+#pragma unroll
+    for (int i = 0; i < (CF + 3) / 4; ++i) {
+      const int f = i * 4 + w;
+      if (f < CF) glds16(base + f * kFrag + lane * 4, dst + f * 64);
+    }
+  };
+  auto acquire = [&](const float* next_src) {
+    ring_barrier();
+    if (next_src) issue(next_src, cur ^ 1);
+  };
+  auto frag = [&](int fc) -> f32x4 { return ring[cur * (CF * 64) + fc * 64 + lane]; };
+
+  // ---------------------------------------------------------------- parameters
+  auto row_tab_load = [&](int k, int buf) {  // per-row params of layer k -> tab[buf]
+    if constexpr (PKIND == PK_ROW) {
+      float* t = tab + buf * TAB;
+      const float* src = a.rowp + (int64_t)k * 8 * a.rstride;
+      for (int i = tid; i < TAB; i += 256) {
+        const int slot = i < 6 * MP ? i / MP : 6;
+        const int row = i < 6 * MP ? i % MP : i - 6 * MP;
+        const int lim = slot == 6 ? n : m;
+        t[i] = row < lim ? src[(int64_t)slot * a.rstride + row] : 0.0f;
+      }
+    }
+  };
+  // uniform per-layer scalars (s_load).  k = -1 (prologue) reads layer 0; b1n = beta1 of the
+  // layer whose Var the G2 epilogue of layer k produces (k+1, clamped).
+  struct LayerP { float b1, b2, b3, ss2, ss2b, the, thz, s1, b1n; };
+  auto layer_params = [&](int k) -> LayerP {
+    LayerP p{};
+    if constexpr (PKIND != PK_ROW) {
+      const int kk = k < 0 ? 0 : k;
+      const int kn = k < 0 ? 0 : (k + 1 < K ? k + 1 : k);
+      cfloat_p sp = (cfloat_p)a.scal + kk * DLADMM_NSCALAR;
+      p.b1 = sp[DLADMM_P_BETA1];
+      p.b2 = sp[DLADMM_P_BETA2];
+      p.b3 = sp[DLADMM_P_BETA3];
+      p.ss2 = sp[DLADMM_P_SS2];
+      p.ss2b = sp[DLADMM_P_SS2B];
+      p.the = sp[DLADMM_P_THETA_E];
+      p.thz = sp[DLADMM_P_THETA_Z];
+      p.s1 = sp[DLADMM_P_S1];
+      p.b1n = ((cfloat_p)a.scal)[kn * DLADMM_NSCALAR + DLADMM_P_BETA1];
+    }
+    return p;
+  };
+  // value of param `slot` for (layer k, block b, reg r)
+  auto prm = [&](const LayerP& P, int k, int slot, int b, int r) -> float {
+    if constexpr (PKIND == PK_ROW) {
+      const int off = (slot == DLADMM_P_THETA_Z) ? 6 * MP : slot * MP;
+      return tab[(k % 3) * TAB + off + 16 * b + 4 * g + r];
+    } else {
+      switch (slot) {
+        case DLADMM_P_BETA1: return P.b1;
+        case DLADMM_P_BETA2: return P.b2;
+        case DLADMM_P_BETA3: return P.b3;
+        case DLADMM_P_SS2: return P.ss2;
+        case DLADMM_P_SS2B: return P.ss2b;
+        case DLADMM_P_THETA_E: return P.the;
+        case DLADMM_P_THETA_Z: return P.thz;
+        default: return P.s1;
+      }
+    }
+  };
+
+  // ---------------------------------------------------------------- initial state
+  {
+    const rsrc_t rz = mkrsrc(a.Z0, (uint32_t)(n * a.ldz0 * 4));
+    const rsrc_t re = mkrsrc(a.E0, (uint32_t)(m * a.lde0 * 4));
+    const rsrc_t rl = mkrsrc(a.L0, (uint32_t)(m * a.ldl0 * 4));
+    const uint32_t oz = lane_off(a.ldz0), oe = lane_off(a.lde0),
+                   ol = lane_off(a.ldl0);
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        Zr[b][r] = bload(rz, oz + (uint32_t)((16 * b + r) * a.ldz0 * 4));
+        pin_agpr(Zr[b][r]);
+      }
+#pragma unroll
+    for (int b = 0; b < MB; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        Er[b][r] = bload(re, oe + (uint32_t)((16 * b + r) * a.lde0 * 4));
+        Lr[b][r] = bload(rl, ol + (uint32_t)((16 * b + r) * a.ldl0 * 4));
+        Vr[b][r] = 0.0f;
+        pin_agpr(Vr[b][r]);
+      }
+  }
+  row_tab_load(0, 0);
+  issue(a.Ap, 0);
+
+  const uint32_t oo = lane_off(a.ldo);                    // output lane offset
+  const uint32_t ox = lane_off(a.ldx);                    // X lane offset
+  const rsrc_t rx = mkrsrc(a.X, (uint32_t)(m * a.ldx * 4));
+  const uint32_t ob = lane_off(a.ldb);                    // per-element beta lane offset
+  const uint32_t zbytes = (uint32_t)(n * a.ldo * 4), mbytes = (uint32_t)(m * a.ldo * 4);
+
+  // ---------------------------------------------------------------- per-layer epilogues
+  Walk zw{oo, (uint32_t)(a.ldo * 4)}, mw{oo, (uint32_t)(a.ldo * 4)};
+  Walk xw{ox, (uint32_t)(a.ldx * 4)}, bw{ob, (uint32_t)(a.ldb * 4)};
+  // G1 block b of layer k: Z = S(Z - s1*(W_k Var), theta_z)    main_lena.py:86 / tied :114
+  auto epi1 = [&](const LayerP& P, rsrc_t rzo, int k, int b, f32x4 c0, f32x4 c1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float u = c0[r] + c1[r];
+      if constexpr (PKIND == PK_SCALAR) u = P.s1 * u;  // V5 ss1[k]; exactly 1.0 otherwise
+      const float z = shrink(Zr[b][r] - u, prm(P, k, DLADMM_P_THETA_Z, b, r));
+      Zr[b][r] = z;
+      pin_agpr(Zr[b][r]);
+      bstore(rzo, zw.at(r), z);
+      regsum += cv ? fabsf(z) : 0.0f;
+    }
+    zw.next();
+  };
+  // G2 block b of layer k.  Branch-free over k: for the prologue (k = -1, pro = true) the
+  // E/L updates are discarded and T0 = A Z0 + E0 - X (main_lena.py:70) falls out of the same
+  // expression; its E/L stores go to 0-record buffers.
+  struct OutR { rsrc_t e, l, t; };
+  auto epi2 = [&](const LayerP& P, const OutR& O, int k, int b, f32x4 c0, f32x4 c1) {
+    const bool pro = k < 0;
+    const int kp = pro ? 0 : k;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float Pv = c0[r] + c1[r];
+      const float x = px[r];
+      const uint32_t off = mw.at(r);
+      const float l0 = Lr[b][r];
+      float e;
+      if constexpr (EMODE == EM_V1) {
+        // E = S(X - A Z - b2*L, theta_e)                      main_lena.py:87
+        const float b2 = (PKIND == PK_ELEM) ? pb[1][r] : prm(P, kp, DLADMM_P_BETA2, b, r);
+        e = shrink((x - Pv) - b2 * l0, prm(P, kp, DLADMM_P_THETA_E, b, r));
+      } else if constexpr (EMODE == EM_VVAR) {
+        // VVar = L + b2*(A Z + E - X); E = S(E - ss2*VVar)    main_syn_l1l1_scalar.py:114-115
+        const float vv = l0 + prm(P, kp, DLADMM_P_BETA2, b, r) * ((Pv + Er[b][r]) - x);
+        e = shrink(Er[b][r] - prm(P, kp, DLADMM_P_SS2, b, r) * vv,
+                   prm(P, kp, DLADMM_P_THETA_E, b, r));
+      } else {
+        // E = ss2_1*(X - A Z) - ss2_2*L                       main_syn_lasso_scalar.py:102-103
+        e = prm(P, kp, DLADMM_P_SS2, b, r) * (x - Pv) - prm(P, kp, DLADMM_P_SS2B, b, r) * l0;
+      }
+      e = pro ? Er[b][r] : e;
+      const float t = (Pv + e) - x;                            // main_lena.py:70 / :88
+      const float b3 = (PKIND == PK_ELEM) ? pb[0][r] : prm(P, kp, DLADMM_P_BETA3, b, r);
+      const float l = pro ? l0 : l0 + b3 * t;                  // main_lena.py:89 / scalar :118
+      Er[b][r] = e;
+      Lr[b][r] = l;
+      bstore(O.e, off, e);
+      bstore(O.l, off, l);
+      bstore(O.t, off, t);
+      const float res = x - Pv;
+      fitsum += cv ? (lasso ? res * res : fabsf(res)) : 0.0f;
+      // Var of the next layer: L + b1*T  (main_lena.py:85); unused after the last layer
+      float b1n;
+      if constexpr (PKIND == PK_ELEM) b1n = pb[2][r];
+      else if constexpr (PKIND == PK_ROW) b1n = prm(P, k + 1, DLADMM_P_BETA1, b, r);
+      else b1n = P.b1n;
+      Vr[b][r] = l + b1n * t;
+      pin_agpr(Vr[b][r]);
+    }
+    mw.next();
+  };
+  // per-wave partial objective of layer k (k < 0: just reset the prologue's sums)
+  auto flush_loss = [&](int k) {
+    if (lossz && k >= 0) {
+      const float rs = wave_sum(regsum), fs = wave_sum(fitsum);
+      if (lane == 0) {
+        const int gw = blockIdx.x * kWaves + w;
+        a.lossp[(int64_t)(2 * k + 0) * a.nwaves + gw] = rs;
+        a.lossp[(int64_t)(2 * k + 1) * a.nwaves + gw] = lasso ? 0.5f * fs : fs;
+      }
+    }
+    regsum = 0.f;
+    fitsum = 0.f;
+  };
+  auto prefetch_elem = [&](int k, int b) {  // X / betas the G2 epilogue of (k, b) will need
+#pragma unroll
+    for (int r = 0; r < 4; ++r) px[r] = bload(rx, xw.at(r));
+    xw.next();
+    if constexpr (PKIND == PK_ELEM) {
+      const uint32_t eb = (uint32_t)(m * a.ldb * 4);
+      const rsrc_t r1 = mkrsrc(k >= 0 ? a.b1e[k] : nullptr, k >= 0 ? eb : 0u);
+      const rsrc_t r2 = mkrsrc(k >= 0 ? a.b2e[k] : nullptr, k >= 0 ? eb : 0u);
+      const rsrc_t rn = mkrsrc(k + 1 < K ? a.b1e[k + 1] : nullptr, k + 1 < K ? eb : 0u);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t off = bw.at(r);
+        pb[0][r] = bload(r1, off);
+        pb[1][r] = bload(r2, off);
+        pb[2][r] = bload(rn, off);
+      }
+      bw.next();
+    }
+  };
+
+  // ---------------------------------------------------------------- the K-layer loop
+  // Phase order: G2(-1) [P0 = A Z0], then per layer G1(k) [W_k Var], G2(k) [A Z_k].
+  // Each block's epilogue is deferred to the start of the next block (after its ring barrier),
+  // the last block's epilogue to the start of the next phase.
+  const int64_t wl = (int64_t)F::GF * kFrag;  // floats per packed W_k
+  f32x4 q0 = {0.f, 0.f, 0.f, 0.f}, q1 = {0.f, 0.f, 0.f, 0.f};
+  for (int k = -1; k < K; ++k) {
+    const bool st = a.keep_all || k == K - 1;
+    const int ko = a.keep_all ? k : 0;
+    const LayerP P = layer_params(k);
+    const LayerP Pp = layer_params(k - 1);
+    // outputs of layer k (Z, E, L) and T[k+1]; num_records 0 = not stored
+    const rsrc_t rzo = mkrsrc(a.Zo + (int64_t)ko * n * a.ldo, st && k >= 0 ? zbytes : 0u);
+    const OutR O{mkrsrc(a.Eo + (int64_t)ko * m * a.ldo, st && k >= 0 ? mbytes : 0u),
+                 mkrsrc(a.Lo + (int64_t)ko * m * a.ldo, st && k >= 0 ? mbytes : 0u),
+                 mkrsrc(a.To ? a.To + (int64_t)(a.keep_all ? k + 1 : 0) * m * a.ldo : nullptr,
+                        (a.To && st) ? mbytes : 0u)};
+    // outputs of layer k-1 (its last G2 block's epilogue runs inside this layer's G1)
+    const bool stp = a.keep_all || k - 1 == K - 1;
+    const int kop = a.keep_all ? k - 1 : 0;
+    const OutR Op{mkrsrc(a.Eo + (int64_t)kop * m * a.ldo, stp && k - 1 >= 0 ? mbytes : 0u),
+                  mkrsrc(a.Lo + (int64_t)kop * m * a.ldo, stp && k - 1 >= 0 ? mbytes : 0u),
+                  mkrsrc(a.To ? a.To + (int64_t)(a.keep_all ? k : 0) * m * a.ldo : nullptr,
+                         (a.To && stp) ? mbytes : 0u)};
+    const float* wk = a.Wp + (int64_t)(k < 0 ? 0 : k) * wl;
+
+    // ---- G1(k): U[b] = sum_jb Wp_k[b][jb] * Var[jb]
+    if (k >= 0) {
+      zw.cur = oo;
+      // layer k+1's row table -> buffer (k+1)%3.  Its previous content (layer k-2) was last
+      // read in G1(k-1)'s deferred epilogue, several ring barriers ago; its readers (G2(k)
+      // epilogues, layer k+1) all come after G1(k)'s first barrier.
+      if (k + 1 < K) row_tab_load(k + 1, (k + 1) % 3);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int jb = 0; jb < MB; ++jb) {
+          const int fi = b * MB + jb;
+          if (fi % CF == 0) {
+            const int ch = fi / CF;
+            acquire(ch + 1 < NCH ? wk + (int64_t)(ch + 1) * CF * kFrag : a.Ap);
+          }
+          if (jb == 0) {
+            if (b == 0) {
+              epi2(Pp, Op, k - 1, MB - 1, q0, q1);
+              flush_loss(k - 1);
+            } else {
+              epi1(P, rzo, k, b - 1, q0, q1);
+            }
+          }
+          const f32x4 wv = frag(fi % CF);
+          c0 = mfma4(wv.x, Vr[jb][0], c0);
+          c1 = mfma4(wv.y, Vr[jb][1], c1);
+          c0 = mfma4(wv.z, Vr[jb][2], c0);
+          c1 = mfma4(wv.w, Vr[jb][3], c1);
+          if (fi % CF == CF - 1) cur ^= 1;
+        }
+        q0 = c0;
+        q1 = c1;
+      }
+    }
+    // ---- G2(k): P[b] = sum_kb Ap[b][kb] * Z[kb]
+    const float* next_base = (k + 1 < K) ? a.Wp + (int64_t)(k + 1) * wl : nullptr;
+    mw.cur = oo;
+    xw.cur = ox;
+    bw.cur = ob;
+#pragma unroll
+    for (int b = 0; b < MB; ++b) {
+      f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < NB; ++kb) {
+        const int fi = b * NB + kb;
+        if (fi % CF == 0) {
+          const int ch = fi / CF;
+          acquire(ch + 1 < NCH ? a.Ap + (int64_t)(ch + 1) * CF * kFrag : next_base);
+        }
+        if (kb == 0) {
+          if (b == 0) {
+            if (k >= 0) epi1(P, rzo, k, NB - 1, q0, q1);
+          } else {
+            epi2(P, O, k, b - 1, q0, q1);
+          }
+          prefetch_elem(k, b);
+        }
+        const f32x4 wv = frag(fi % CF);
+        c0 = mfma4(wv.x, Zr[kb][0], c0);
+        c1 = mfma4(wv.y, Zr[kb][1], c1);
+        c0 = mfma4(wv.z, Zr[kb][2], c0);
+        c1 = mfma4(wv.w, Zr[kb][3], c1);
+        if (fi % CF == CF - 1) cur ^= 1;
+      }
+      q0 = c0;
+      q1 = c1;
+    }
+  }
+  {
+    const LayerP P = layer_params(K - 1);
+    const int ko = a.keep_all ? K - 1 : 0;
+    const OutR O{mkrsrc(a.Eo + (int64_t)ko * m * a.ldo, mbytes),
+                 mkrsrc(a.Lo + (int64_t)ko * m * a.ldo, mbytes),
+                 mkrsrc(a.To ? a.To + (int64_t)(a.keep_all ? K : 0) * m * a.ldo : nullptr,
+                        a.To ? mbytes : 0u)};
+    epi2(P, O, K - 1, MB - 1, q0, q1);
+    flush_loss(K - 1);
+  }
+}
+
+// ------------------------------------------------------------------------ weight packing
+struct PackArgs {
+  const float* src[DLADMM_MAX_LAYERS + 1];
+  int R, C, RB, CB;
+  int64_t ld;
+  float* dst;
+};
+
+// dst[t][ib][jb][lane][q] = src_t[16 ib + (lane & 15)][16 jb + 4 (lane >> 4) + q], 0 outside
+__global__ __launch_bounds__(256) void pack_frags_kernel(const PackArgs p) {
+  const int t = blockIdx.y;
+  const int64_t fr = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (fr >= (int64_t)p.RB * p.CB) return;
+  const int lane = threadIdx.x & 63;
+  const int ib = (int)(fr / p.CB), jb = (int)(fr % p.CB);
+  const int row = 16 * ib + (lane & 15);
+  const int c0 = 16 * jb + 4 * (lane >> 4);
+  const float* s = p.src[t];
+  f32x4 v;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    v[q] = (row < p.R && c0 + q < p.C) ? s[(int64_t)row * p.ld + c0 + q] : 0.0f;
+  reinterpret_cast<f32x4*>(p.dst)[((int64_t)t * p.RB * p.CB + fr) * 64 + lane] = v;
+}
+
+// ------------------------------------------------------------------------ loss reduction
+// sums[i] = sum_w part[i][w] in fp64, fixed order (bitwise reproducible)
+__global__ __launch_bounds__(256) void loss_reduce_kernel(const float* part, int nw, double* sums) {
+  __shared__ double red[256];
+  const int i = blockIdx.x;
+  double s = 0.0;
+  for (int wv = threadIdx.x; wv < nw; wv += 256) s += (double)part[(int64_t)i * nw + wv];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) sums[i] = red[0];
+}
+
+}  // namespace dladmm
+
+// ======================================================================== host side / C ABI
+namespace dladmm {
+
+struct Shape { int MP, NP; };
+// Register-resident instantiations (state = NP/4 + MP VGPRs per lane; <= 384 at 256 x 512).
+// A problem runs on the smallest instantiation that covers it; zero padding is exact
+// (padded rows of A/W are 0, so padded state rows stay 0 -- see DESIGN.md).
+constexpr Shape kShapes[] = {{16, 32}, {64, 256}, {256, 512}};
+constexpr int kNumShapes = sizeof(kShapes) / sizeof(kShapes[0]);
+
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+inline int pick_shape(int m, int n) {
+  for (int i = 0; i < kNumShapes; ++i)
+    if (m <= kShapes[i].MP && n <= kShapes[i].NP) return i;
+  return -1;
+}
+
+struct Plan {
+  int shape, MP, NP, tiles, nwaves;
+  size_t off_ap, off_wp, off_loss, total;
+};
+
+inline int validate(const dladmm_fwd_desc* d) {
+  if (!d) return DLADMM_E_NULL;
+  if (d->abi_version != DLADMM_ABI_VERSION) return DLADMM_E_ABI_VERSION;
+  if (d->variant < DLADMM_V1_LENA || d->variant > DLADMM_V6_LASSO) return DLADMM_E_VARIANT;
+  if (d->m < 1 || d->n < 1 || d->batch < 1) return DLADMM_E_SHAPE;
+  if (d->layers < 1 || d->layers > DLADMM_MAX_LAYERS) return DLADMM_E_LAYERS;
+  if (d->loss_kind < 0 || d->loss_kind > 2) return DLADMM_E_UNSUPPORTED;
+  if (!d->X || !d->A || !d->Z0 || !d->E0 || !d->L0 || !d->W || !d->Z || !d->E || !d->L)
+    return DLADMM_E_NULL;
+  for (int k = 0; k < d->layers; ++k)
+    if (!d->W[k]) return DLADMM_E_NULL;
+  if (d->loss_kind && !d->loss_sums) return DLADMM_E_NULL;
+  const int v = d->variant;
+  if (v == DLADMM_V2_LTHETA || v == DLADMM_V3_FULL) {
+    if (!d->row_params) return DLADMM_E_NULL;
+    if (d->row_stride < d->m || d->row_stride < d->n) return DLADMM_E_SHAPE;
+  } else if (!d->scalar_params) {
+    return DLADMM_E_NULL;
+  }
+  if (v == DLADMM_V1_LENA) {
+    if (!d->beta1_elem || !d->beta2_elem) return DLADMM_E_NULL;
+    for (int k = 0; k < d->layers; ++k)
+      if (!d->beta1_elem[k] || !d->beta2_elem[k]) return DLADMM_E_NULL;
+    if (d->ld_beta < d->batch) return DLADMM_E_SHAPE;
+  }
+  const int64_t B = d->batch;
+  if (d->ld_x < B || d->ld_z0 < B || d->ld_e0 < B || d->ld_l0 < B || d->ld_out < B)
+    return DLADMM_E_SHAPE;
+  if (d->ld_a < d->n || d->ld_w < d->m) return DLADMM_E_SHAPE;
+  // the kernel addresses every per-column matrix with 32-bit buffer offsets (< 2^31 bytes)
+  const int64_t lim = (int64_t)1 << 31;
+  const int64_t mx = d->m > d->n ? d->m : d->n;
+  if (mx * d->ld_x * 4 >= lim || mx * d->ld_z0 * 4 >= lim || mx * d->ld_e0 * 4 >= lim ||
+      mx * d->ld_l0 * 4 >= lim || mx * d->ld_out * 4 >= lim ||
+      (v == DLADMM_V1_LENA && mx * d->ld_beta * 4 >= lim))
+    return DLADMM_E_SHAPE;
+  return 0;
+}
+
+inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
+  const int s = pick_shape(d->m, d->n);
+  if (s < 0) return DLADMM_E_UNSUPPORTED;
+  p->shape = s;
+  p->MP = kShapes[s].MP;
+  p->NP = kShapes[s].NP;
+  p->tiles = (d->batch + kTileCols - 1) / kTileCols;
+  p->nwaves = p->tiles * kWaves;
+  const size_t frag_bytes = (size_t)p->MP * p->NP * sizeof(float);
+  p->off_ap = 0;
+  p->off_wp = align256(frag_bytes);
+  p->off_loss = p->off_wp + align256(frag_bytes * d->layers);
+  p->total = p->off_loss + align256((size_t)2 * d->layers * p->nwaves * sizeof(float));
+  return 0;
+}
+
+template <int MP, int NP, int EM, int PK>
+hipError_t launch_fused(const FusedArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((fused_kernel<MP, NP, EM, PK>), dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int MP, int NP>
+hipError_t dispatch_variant(int variant, const FusedArgs& a, int grid, hipStream_t s) {
+  switch (variant) {
+    case DLADMM_V1_LENA: return launch_fused<MP, NP, EM_V1, PK_ELEM>(a, grid, s);
+    case DLADMM_V2_LTHETA: return launch_fused<MP, NP, EM_V1, PK_ROW>(a, grid, s);
+    case DLADMM_V3_FULL: return launch_fused<MP, NP, EM_VVAR, PK_ROW>(a, grid, s);
+    case DLADMM_V4_SCALAR:
+    case DLADMM_V5_TIED: return launch_fused<MP, NP, EM_VVAR, PK_SCALAR>(a, grid, s);
+    case DLADMM_V6_LASSO: return launch_fused<MP, NP, EM_LASSO, PK_SCALAR>(a, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t dispatch_shape(int shape, int variant, const FusedArgs& a, int grid, hipStream_t s) {
+  switch (shape) {
+    case 0: return dispatch_variant<16, 32>(variant, a, grid, s);
+    case 1: return dispatch_variant<64, 256>(variant, a, grid, s);
+    case 2: return dispatch_variant<256, 512>(variant, a, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace dladmm
+
+extern "C" {
+
+int dladmm_abi_version(void) { return DLADMM_ABI_VERSION; }
+
+size_t dladmm_fwd_workspace_bytes(const dladmm_fwd_desc* d) {
+  using namespace dladmm;
+  if (validate(d)) return 0;
+  Plan p;
+  if (make_plan(d, &p)) return 0;
+  return p.total;
+}
+
+int dladmm_fwd_path(const dladmm_fwd_desc* d) {
+  using namespace dladmm;
+  if (int e = validate(d)) return e;
+  return pick_shape(d->m, d->n) >= 0 ? 1 : DLADMM_E_UNSUPPORTED;
+}
+
+int dladmm_fwd_f32(const dladmm_fwd_desc* d, void* stream) {
+  using namespace dladmm;
+  if (int e = validate(d)) return e;
+  Plan p;
+  if (int e = make_plan(d, &p)) return e;
+  if (!d->workspace || d->workspace_bytes < p.total) return DLADMM_E_WORKSPACE;
+  if (((uintptr_t)d->workspace) & 255) return DLADMM_E_ALIGN;
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)d->workspace;
+  float* Ap = (float*)(ws + p.off_ap);
+  float* Wp = (float*)(ws + p.off_wp);
+  float* lossp = (float*)(ws + p.off_loss);
+  const int MB = p.MP / 16, NB = p.NP / 16;
+
+  // 1. pack A and every W_k into MFMA fragment order (zero-padded to MP x NP)
+  PackArgs pa{};
+  pa.src[0] = d->A;
+  pa.R = d->m; pa.C = d->n; pa.RB = MB; pa.CB = NB; pa.ld = d->ld_a; pa.dst = Ap;
+  hipLaunchKernelGGL(pack_frags_kernel, dim3((MB * NB + 3) / 4, 1), dim3(256), 0, s, pa);
+  PackArgs pw{};
+  for (int k = 0; k < d->layers; ++k) pw.src[k] = d->W[k];
+  pw.R = d->n; pw.C = d->m; pw.RB = NB; pw.CB = MB; pw.ld = d->ld_w; pw.dst = Wp;
+  hipLaunchKernelGGL(pack_frags_kernel, dim3((MB * NB + 3) / 4, d->layers), dim3(256), 0, s, pw);
+  if (hipError_t e = hipGetLastError()) return (int)e;
+
+  // 2. the fused K-layer forward
+  FusedArgs a{};
+  a.m = d->m; a.n = d->n; a.B = d->batch; a.K = d->layers;
+  a.keep_all = d->keep_all ? 1 : 0; a.loss_kind = d->loss_kind; a.nwaves = p.nwaves;
+  a.X = d->X; a.ldx = d->ld_x;
+  a.Z0 = d->Z0; a.ldz0 = d->ld_z0;
+  a.E0 = d->E0; a.lde0 = d->ld_e0;
+  a.L0 = d->L0; a.ldl0 = d->ld_l0;
+  a.Ap = Ap; a.Wp = Wp;
+  a.scal = d->scalar_params;
+  a.rowp = d->row_params; a.rstride = d->row_stride;
+  a.ldb = d->ld_beta;
+  if (d->variant == DLADMM_V1_LENA)
+    for (int k = 0; k < d->layers; ++k) { a.b1e[k] = d->beta1_elem[k]; a.b2e[k] = d->beta2_elem[k]; }
+  a.Zo = d->Z; a.Eo = d->E; a.Lo = d->L; a.To = d->T; a.ldo = d->ld_out;
+  a.lossp = lossp;
+  if (d->ev_kernel_start) {
+    if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_start, s)) return (int)e;
+  }
+  if (hipError_t e = dispatch_shape(p.shape, d->variant, a, p.tiles, s)) return (int)e;
+  if (d->ev_kernel_stop) {
+    if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_stop, s)) return (int)e;
+  }
+
+  // 3. per-layer loss sums, fixed-order fp64 reduction of the per-wave partials
+  if (d->loss_kind) {
+    hipLaunchKernelGGL(loss_reduce_kernel, dim3(2 * d->layers), dim3(256), 0, s,
+                       (const float*)lossp, p.nwaves, d->loss_sums);
+    if (hipError_t e = hipGetLastError()) return (int)e;
+  }
+  return 0;
+}
+
+const char* dladmm_error_string(int code) {
+  switch (code) {
+    case 0: return "success";
+    case DLADMM_E_ABI_VERSION: return "dladmm: descriptor abi_version mismatch";
+    case DLADMM_E_VARIANT: return "dladmm: unknown variant";
+    case DLADMM_E_SHAPE: return "dladmm: invalid shape or leading dimension";
+    case DLADMM_E_LAYERS: return "dladmm: layers must be in [1, DLADMM_MAX_LAYERS]";
+    case DLADMM_E_NULL: return "dladmm: required pointer is NULL";
+    case DLADMM_E_WORKSPACE: return "dladmm: workspace missing or too small";
+    case DLADMM_E_UNSUPPORTED: return "dladmm: unsupported configuration";
+    case DLADMM_E_ALIGN: return "dladmm: workspace must be 256-byte aligned";
+  }
+  if (code > 0) return hipGetErrorString((hipError_t)code);
+  return "dladmm: unknown error";
+}
+
+}  // extern "C"

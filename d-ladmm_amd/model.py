@@ -1,0 +1,311 @@
+"""Drop-in `DLADMMNet` modules: reference constructor, parameter names/shapes and return lists,
+with the K-layer loop replaced by one fused HIP call (ops.dladmm_forward).
+
+One class per reference variant (the reference copy-pastes a different `class DLADMMNet` into
+each script):
+
+  DLADMMNet            V1  main_lena.py:16-102            beta (m, batch_size), thetas fixed
+  DLADMMNetLTheta      V2  main_syn_l1l1_ltheta.py:16-95  beta (m,1), thetas (d,1)/(m,1)
+  DLADMMNetFull        V3  main_syn_l1l1_full.py:16-96    per-row beta1/2/3, ss2, thetas
+  DLADMMNetScalar      V4  main_syn_l1l1_scalar.py:34-131 all (1,1); returns (Z, E, L, T)
+  DLADMMNetScalarTied  V5  main_syn_l1l1_scalar_tied.py:34-104 one shared fc + ss1[k]
+  DLADMMNetLasso       V6  main_syn_lasso_scalar.py:17-118 linear LASSO E-step
+
+Constructor signature `(m, n, d, batch_size, A, Z0, E0, L0, layers)`, `state_dict` keys and
+shapes, `name()` and the forward return arity all follow the reference, so a reference
+checkpoint (e.g. DLADMMNet.pth.tar, 45 keys for V1 at layers=15) loads with
+`load_state_dict(..., strict=True)` unchanged.  `forward` is inference-only: with autograd
+recording and parameters that require grad it raises (backward is future work).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .ops import dladmm_forward
+
+
+def _dev(t: torch.Tensor) -> torch.Tensor:
+    """The reference calls .cuda() on A, Z0, E0, L0 (main_lena.py:23-26); on ROCm torch.cuda is
+    the HIP device.  Without a device (CPU-only hosts) the tensors stay put so the module can
+    still be built and (de)serialised; forward then raises."""
+    return t.cuda() if torch.cuda.is_available() else t
+
+
+class _DLADMMBase(nn.Module):
+    VARIANT = 0
+    RETURNS_T = False
+    WSCALE = 1.0     # fc init scale: main_lena.py:49 (1.0) / main_syn_l1l1_scalar.py:72 (0.4)
+    NAME = "DLADMMNet"
+
+    def __init__(self, m, n, d, batch_size, A, Z0, E0, L0, layers):
+        super().__init__()
+        self.m = m
+        self.n = n
+        self.d = d
+        self.batch_size = batch_size
+        self.A = _dev(A)
+        self.Z0 = _dev(Z0)
+        self.E0 = _dev(E0)
+        self.L0 = _dev(L0)
+        self.layers = layers
+        self._register_params()
+        self._init_fc()
+        # the reference follows construction with model.cuda() (main_lena.py:191); do it here
+        self.to(self.A.device)
+
+    # --- construction -----------------------------------------------------------------
+    def _plist(self, name, shape, value):
+        pl = nn.ParameterList()
+        for _ in range(self.layers):
+            pl.append(nn.Parameter(value * torch.ones(*shape, dtype=torch.float32)))
+        setattr(self, name, pl)
+
+    def _register_params(self):  # pragma: no cover - per variant
+        raise NotImplementedError
+
+    def _init_fc(self):
+        # main_lena.py:45-49 / main_syn_l1l1_scalar.py:67-72: every Linear's weight is replaced by
+        # s * (A^T + 1e-3 * N(0, 1)), on A's device
+        for mod in self.modules():
+            if isinstance(mod, nn.Linear):
+                w = self.A.t() + (1e-3) * torch.randn_like(self.A.t())
+                if self.WSCALE != 1.0:
+                    w = w * self.WSCALE
+                # A.t() + noise inherits A.t()'s column-major strides; store it row-major (same
+                # values, same state_dict) so the weight packer reads rows
+                mod.weight = nn.Parameter(w.contiguous())
+
+    def name(self):
+        return self.NAME
+
+    # --- fused forward ----------------------------------------------------------------
+    def _weights(self) -> List[torch.Tensor]:
+        return [self.fc[k].weight for k in range(self.layers)]
+
+    def _tables(self, dev) -> dict:  # pragma: no cover - per variant
+        raise NotImplementedError
+
+    def _check_grad(self):
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise RuntimeError(
+                "dladmm: the fused HIP forward is inference-only (no backward yet); call it "
+                "under torch.no_grad() / torch.inference_mode() or set requires_grad_(False)")
+
+    def run(self, x: torch.Tensor, keep_all: bool = True, loss_kind: int = 0,
+            kernel_events=None):
+        """Fused forward returning the raw ops.ForwardResult (stacked [K, rows, B] outputs)."""
+        self._check_grad()
+        with torch.no_grad():
+            dev = self.A.device
+            return dladmm_forward(
+                self.VARIANT, x, self.A, [w.detach() for w in self._weights()],
+                self.Z0, self.E0, self.L0, keep_all=keep_all, want_T=self.RETURNS_T,
+                loss_kind=loss_kind, kernel_events=kernel_events, **self._tables(dev))
+
+    def forward(self, x):
+        r = self.run(x)
+        K = self.layers
+        Z = [r.Z[k] for k in range(K)]
+        E = [r.E[k] for k in range(K)]
+        L = [r.L[k] for k in range(K)]
+        if self.RETURNS_T:
+            return Z, E, L, [r.T[k] for k in range(K + 1)]
+        return Z, E, L
+
+    def layer_objectives(self, x, alpha: float, kind: str = "l1l1", kernel_events=None):
+        """Forward + the per-layer objective of the reference training loop, fused in-kernel:
+        l1l1  alpha*sum(|Z_k|,0).mean() + sum(|X - A Z_k|,0).mean()   main_syn_l1l1_scalar.py:290-294
+        lasso alpha*sum(|Z_k|,0).mean() + 0.5*sum((X-A Z_k)^2,0).mean() main_syn_lasso_scalar.py:276-281
+        Returns (ForwardResult, fp64 tensor [K])."""
+        lk = {"l1l1": _lib.LOSS_L1L1, "lasso": _lib.LOSS_LASSO}[kind]
+        r = self.run(x, loss_kind=lk, kernel_events=kernel_events)
+        obj = (alpha * r.loss_sums[:, 0] + r.loss_sums[:, 1]) / x.shape[1]
+        return r, obj
+
+
+def _stack_scalar(pl) -> torch.Tensor:
+    return torch.cat([p.detach().reshape(1) for p in pl])
+
+
+def _scalar_table(K, dev, **cols) -> torch.Tensor:
+    """(K, 8) fp32 table of per-layer scalars; missing slots 0 (unused by the variant)."""
+    slots = {"b1": _lib.P_BETA1, "b2": _lib.P_BETA2, "b3": _lib.P_BETA3, "ss2": _lib.P_SS2,
+             "ss2b": _lib.P_SS2B, "the": _lib.P_THETA_E, "thz": _lib.P_THETA_Z, "s1": _lib.P_S1}
+    t = torch.zeros((K, _lib.NSCALAR), dtype=torch.float32, device=dev)
+    for k, v in cols.items():
+        t[:, slots[k]] = v.to(device=dev, dtype=torch.float32) if torch.is_tensor(v) else v
+    return t
+
+
+def _row_table(K, R, dev, m, n, **cols) -> torch.Tensor:
+    """(K, 8, R) fp32 table of per-row params (R = max(m, n)); theta_z holds n rows, the rest m."""
+    slots = {"b1": _lib.P_BETA1, "b2": _lib.P_BETA2, "b3": _lib.P_BETA3, "ss2": _lib.P_SS2,
+             "ss2b": _lib.P_SS2B, "the": _lib.P_THETA_E, "thz": _lib.P_THETA_Z}
+    t = torch.zeros((K, _lib.NSCALAR, R), dtype=torch.float32, device=dev)
+    for k, pl in cols.items():
+        rows = n if k == "thz" else m
+        t[:, slots[k], :rows] = torch.stack([p.detach().reshape(-1) for p in pl]).to(dev)
+    return t
+
+
+class DLADMMNet(_DLADMMBase):
+    """V1, main_lena.py:16-102 (also main_syn_l1l1.py, main_syn_gt.py)."""
+    VARIANT = _lib.V1_LENA
+
+    def _register_params(self):
+        # main_lena.py:30-41: beta1/beta2 (m, batch_size) per layer; thresholds are plain tensors
+        self.beta1 = nn.ParameterList()
+        self.beta2 = nn.ParameterList()
+        self.fc = nn.ModuleList()
+        for _ in range(self.layers):
+            self.beta1.append(nn.Parameter(torch.ones(self.m, self.batch_size, dtype=torch.float32)))
+            self.beta2.append(nn.Parameter(torch.ones(self.m, self.batch_size, dtype=torch.float32)))
+            self.fc.append(nn.Linear(self.m, self.d, bias=False))
+        self.active_para = _dev(torch.tensor(0.025, dtype=torch.float32))
+        self.active_para1 = _dev(torch.tensor(0.06, dtype=torch.float32))
+
+    def _tables(self, dev):
+        K = self.layers
+        return dict(
+            scalar_params=_scalar_table(K, dev, thz=self.active_para.detach().float(),
+                                        the=self.active_para1.detach().float(), s1=1.0),
+            beta1_elem=[b.detach() for b in self.beta1],
+            beta2_elem=[b.detach() for b in self.beta2])
+
+
+class DLADMMNetLTheta(_DLADMMBase):
+    """V2, main_syn_l1l1_ltheta.py:16-95 (also _bkp, _rw, -dgap, main_syn_gt_ltheta.py)."""
+    VARIANT = _lib.V2_LTHETA
+
+    def _register_params(self):
+        # main_syn_l1l1_ltheta.py:30-43
+        self._plist("beta1", (self.m, 1), 1.0)
+        self._plist("beta2", (self.m, 1), 1.0)
+        self._plist("active_para", (self.d, 1), 0.025)
+        self._plist("active_para1", (self.m, 1), 0.06)
+        self.fc = nn.ModuleList([nn.Linear(self.m, self.d, bias=False) for _ in range(self.layers)])
+
+    def _tables(self, dev):
+        K, R = self.layers, max(self.m, self.d)
+        return dict(row_params=_row_table(K, R, dev, self.m, self.d, b1=self.beta1, b2=self.beta2,
+                                          b3=self.beta1, the=self.active_para1,
+                                          thz=self.active_para))
+
+
+class DLADMMNetFull(_DLADMMBase):
+    """V3, main_syn_l1l1_full.py:16-96 (also main_syn_l1l1-sl2_full.py)."""
+    VARIANT = _lib.V3_FULL
+    WSCALE = 0.4
+
+    def _register_params(self):
+        # main_syn_l1l1_full.py:29-44
+        for nm in ("beta1", "beta2", "beta3", "ss2"):
+            self._plist(nm, (self.m, 1), 1.0)
+        self._plist("active_para", (self.d, 1), 0.2)
+        self._plist("active_para1", (self.m, 1), 0.8)
+        self.fc = nn.ModuleList([nn.Linear(self.m, self.d, bias=False) for _ in range(self.layers)])
+
+    def _tables(self, dev):
+        K, R = self.layers, max(self.m, self.d)
+        return dict(row_params=_row_table(K, R, dev, self.m, self.d, b1=self.beta1, b2=self.beta2,
+                                          b3=self.beta3, ss2=self.ss2, the=self.active_para1,
+                                          thz=self.active_para))
+
+
+class DLADMMNetScalar(_DLADMMBase):
+    """V4, main_syn_l1l1_scalar.py:34-131 (also -sl2_scalar, _scalar_z0)."""
+    VARIANT = _lib.V4_SCALAR
+    RETURNS_T = True
+    WSCALE = 0.4
+    NAME = "DLADMMNet_scalar"
+
+    def __init__(self, m, n, d, batch_size, A, Z0, E0, L0, layers):
+        super().__init__(m, n, d, batch_size, A, Z0, E0, L0, layers)
+        # main_syn_l1l1_scalar.py:41-48 attributes used by the (un-learned) KM iteration
+        self.At = self.A.t()
+        A_np = A.detach().cpu().numpy()
+        self.A_np = A_np
+        self.L = _dev((np.linalg.norm(np.matmul(A_np.T, A_np), ord=2) * torch.ones(1, 1)).float())
+
+    def _register_params(self):
+        # main_syn_l1l1_scalar.py:50-65
+        for nm in ("beta1", "beta2", "beta3", "ss2"):
+            self._plist(nm, (1, 1), 1.0)
+        self._plist("active_para", (1, 1), 0.2)
+        self._plist("active_para1", (1, 1), 0.8)
+        self.fc = nn.ModuleList([nn.Linear(self.m, self.d, bias=False) for _ in range(self.layers)])
+
+    def _tables(self, dev):
+        K = self.layers
+        return dict(scalar_params=_scalar_table(
+            K, dev, b1=_stack_scalar(self.beta1), b2=_stack_scalar(self.beta2),
+            b3=_stack_scalar(self.beta3), ss2=_stack_scalar(self.ss2),
+            the=_stack_scalar(self.active_para1), thz=_stack_scalar(self.active_para), s1=1.0))
+
+
+class DLADMMNetScalarTied(DLADMMNetScalar):
+    """V5, main_syn_l1l1_scalar_tied.py:34-104: one shared fc scaled by ss1[k]."""
+    VARIANT = _lib.V5_TIED
+    NAME = "DLADMMNet_scalar_tied"
+
+    def _register_params(self):
+        # main_syn_l1l1_scalar_tied.py:50-66 (registration order = state_dict order)
+        for nm in ("beta1", "beta2", "beta3", "ss1", "ss2"):
+            self._plist(nm, (1, 1), 1.0)
+        self._plist("active_para", (1, 1), 1e-4)
+        self._plist("active_para1", (1, 1), 1e-2)
+        self.fc = nn.Linear(self.m, self.d, bias=False)
+
+    def _weights(self):
+        return [self.fc.weight] * self.layers
+
+    def _tables(self, dev):
+        K = self.layers
+        return dict(scalar_params=_scalar_table(
+            K, dev, b1=_stack_scalar(self.beta1), b2=_stack_scalar(self.beta2),
+            b3=_stack_scalar(self.beta3), ss2=_stack_scalar(self.ss2),
+            the=_stack_scalar(self.active_para1), thz=_stack_scalar(self.active_para),
+            s1=_stack_scalar(self.ss1)))
+
+
+class DLADMMNetLasso(DLADMMNetScalar):
+    """V6, main_syn_lasso_scalar.py:17-118: E = ss2_1*(X - A Z) - ss2_2*L."""
+    VARIANT = _lib.V6_LASSO
+    NAME = "DLADMMNet"
+
+    def _register_params(self):
+        # main_syn_lasso_scalar.py:33-50
+        self._plist("beta1", (1, 1), 1.0)
+        self._plist("beta3", (1, 1), 1.0)
+        self._plist("ss2_1", (1, 1), 0.5)
+        self._plist("ss2_2", (1, 1), 0.5)
+        self._plist("active_para", (1, 1), 0.2)
+        self.fc = nn.ModuleList([nn.Linear(self.m, self.d, bias=False) for _ in range(self.layers)])
+
+    def _tables(self, dev):
+        K = self.layers
+        return dict(scalar_params=_scalar_table(
+            K, dev, b1=_stack_scalar(self.beta1), b3=_stack_scalar(self.beta3),
+            ss2=_stack_scalar(self.ss2_1), ss2b=_stack_scalar(self.ss2_2),
+            thz=_stack_scalar(self.active_para), s1=1.0))
+
+
+VARIANTS = {
+    "v1": DLADMMNet, "v2": DLADMMNetLTheta, "v3": DLADMMNetFull,
+    "v4": DLADMMNetScalar, "v5": DLADMMNetScalarTied, "v6": DLADMMNetLasso,
+}
+
+
+def load_checkpoint(model: nn.Module, path: str, strict: bool = True):
+    """`torch.load(model_file); model.load_state_dict(...)` as test_lena_lskm.py:284-285 does,
+    accepting a raw state_dict or a {'state_dict': ...} wrapper (the .pth.tar convention).
+    Uses weights_only=True: a checkpoint cannot execute code."""
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    if isinstance(sd, dict) and "state_dict" in sd and isinstance(sd["state_dict"], dict):
+        sd = sd["state_dict"]
+    return model.load_state_dict(sd, strict=strict)

@@ -1,0 +1,162 @@
+"""The fused K-layer forward as one device call (torch is only the memory/stream plumbing).
+
+`dladmm_forward` packs the per-layer parameters into the tables the C ABI expects, allocates the
+outputs and the workspace with torch on the current device, and enqueues
+`dladmm_fwd_f32` (include/dladmm.h) on torch's current HIP stream.  There is no CPU fallback:
+CPU tensors or a missing library raise.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import _lib
+
+
+@dataclass
+class ForwardResult:
+    Z: torch.Tensor          # [K | 1, n, B]
+    E: torch.Tensor          # [K | 1, m, B]
+    L: torch.Tensor          # [K | 1, m, B]
+    T: Optional[torch.Tensor]  # [K+1 | 1, m, B] or None
+    loss_sums: Optional[torch.Tensor]  # [K, 2] fp64: (sum|Z_k|, fit_k)
+
+
+def _f32_dev(t: torch.Tensor, name: str) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"dladmm: {name} must be a tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(f"dladmm: {name} is on {t.device}; the fused forward runs on a HIP "
+                           "device only (no CPU fallback)")
+    if t.dtype != torch.float32:
+        raise TypeError(f"dladmm: {name} must be float32, got {t.dtype}")
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"dladmm: {name} must be a 2-D row-major matrix (batch contiguous)")
+    return t
+
+
+def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[torch.Tensor],
+                   Z0: torch.Tensor, E0: torch.Tensor, L0: torch.Tensor, *,
+                   scalar_params: Optional[torch.Tensor] = None,
+                   row_params: Optional[torch.Tensor] = None,
+                   beta1_elem: Sequence[torch.Tensor] = (),
+                   beta2_elem: Sequence[torch.Tensor] = (),
+                   keep_all: bool = True, want_T: bool = True, loss_kind: int = 0,
+                   out: Optional[ForwardResult] = None,
+                   kernel_events: Optional[tuple] = None) -> ForwardResult:
+    """Run the whole K-layer forward of `variant` (dladmm_variant) on X's device.
+
+    X: (m, B); A: (m, n); W: K tensors (n, m) (fc[k].weight; V5 passes the shared one K times);
+    Z0: (n, B); E0, L0: (m, B).  scalar_params: (K, 8) device fp32 (V1, V4-V6);
+    row_params: (K, 8, max(m, n)) (V2, V3); beta{1,2}_elem: K tensors (m, B) (V1).
+    Returns views-ready stacked outputs and, if loss_kind, the per-layer (sum|Z|, fit) sums.
+    """
+    L = _lib.lib()
+    X = _f32_dev(X, "X")
+    A = _f32_dev(A, "A")
+    Z0, E0, L0 = _f32_dev(Z0, "Z0"), _f32_dev(E0, "E0"), _f32_dev(L0, "L0")
+    m, B = X.shape
+    n = A.shape[1]
+    K = len(W)
+    if A.shape[0] != m:
+        raise RuntimeError(f"dladmm: A is {tuple(A.shape)} but X has {m} rows")
+    if tuple(Z0.shape) != (n, B) or tuple(E0.shape) != (m, B) or tuple(L0.shape) != (m, B):
+        raise RuntimeError(
+            "dladmm: Z0/E0/L0 shapes do not broadcast with X: "
+            f"Z0 {tuple(Z0.shape)}, E0 {tuple(E0.shape)}, L0 {tuple(L0.shape)}, X {tuple(X.shape)}")
+    if not 1 <= K <= _lib.MAX_LAYERS:
+        raise ValueError(f"dladmm: layers must be in [1, {_lib.MAX_LAYERS}], got {K}")
+    Ws = [_f32_dev(w if w.dim() == 2 and w.stride(1) == 1 else w.contiguous(), f"W[{k}]")
+          for k, w in enumerate(W)]
+    ldw = Ws[0].stride(0)
+    for k, w in enumerate(Ws):
+        if tuple(w.shape) != (n, m) or w.stride(0) != ldw:
+            raise RuntimeError(f"dladmm: fc[{k}].weight must be ({n}, {m}) with a common stride")
+    dev = X.device
+
+    Kout = K if keep_all else 1
+    if out is None:
+        Zo = torch.empty((Kout, n, B), device=dev, dtype=torch.float32)
+        Eo = torch.empty((Kout, m, B), device=dev, dtype=torch.float32)
+        Lo = torch.empty((Kout, m, B), device=dev, dtype=torch.float32)
+        To = (torch.empty((Kout + 1 if keep_all else 1, m, B), device=dev, dtype=torch.float32)
+              if want_T else None)
+        ls = torch.empty((K, 2), device=dev, dtype=torch.float64) if loss_kind else None
+        out = ForwardResult(Zo, Eo, Lo, To, ls)
+
+    d = _lib.FwdDesc()
+    d.abi_version = _lib.ABI_VERSION
+    d.variant, d.m, d.n, d.batch, d.layers = variant, m, n, B, K
+    d.keep_all, d.loss_kind = int(bool(keep_all)), int(loss_kind)
+    d.X, d.ld_x = X.data_ptr(), X.stride(0)
+    d.A, d.ld_a = A.data_ptr(), A.stride(0)
+    d.Z0, d.ld_z0 = Z0.data_ptr(), Z0.stride(0)
+    d.E0, d.ld_e0 = E0.data_ptr(), E0.stride(0)
+    d.L0, d.ld_l0 = L0.data_ptr(), L0.stride(0)
+    warr = _lib.ptr_array([w.data_ptr() for w in Ws])
+    d.W, d.ld_w = ctypes.cast(warr, ctypes.POINTER(ctypes.c_void_p)), ldw
+    keep = [warr]
+    if scalar_params is not None:
+        sp = scalar_params
+        if sp.device != dev or sp.dtype != torch.float32 or tuple(sp.shape) != (K, _lib.NSCALAR) \
+                or not sp.is_contiguous():
+            raise ValueError("dladmm: scalar_params must be a contiguous (K, 8) fp32 device tensor")
+        d.scalar_params = sp.data_ptr()
+    if row_params is not None:
+        rp = row_params
+        if rp.device != dev or rp.dtype != torch.float32 or rp.dim() != 3 or \
+                rp.shape[0] != K or rp.shape[1] != _lib.NSCALAR or not rp.is_contiguous():
+            raise ValueError("dladmm: row_params must be a contiguous (K, 8, R) fp32 device tensor")
+        d.row_params, d.row_stride = rp.data_ptr(), rp.shape[2]
+    if len(beta1_elem):
+        b1 = [_f32_dev(b, f"beta1[{k}]") for k, b in enumerate(beta1_elem)]
+        b2 = [_f32_dev(b, f"beta2[{k}]") for k, b in enumerate(beta2_elem)]
+        ldb = b1[0].stride(0)
+        for b in b1 + b2:
+            if tuple(b.shape) != (m, B) or b.stride(0) != ldb:
+                raise RuntimeError(
+                    f"dladmm: per-sample beta of shape {tuple(b.shape)} does not broadcast with "
+                    f"X {tuple(X.shape)} (main_lena.py:35-36 betas are (m, batch_size))")
+        a1 = _lib.ptr_array([b.data_ptr() for b in b1])
+        a2 = _lib.ptr_array([b.data_ptr() for b in b2])
+        keep += [a1, a2]
+        d.beta1_elem = ctypes.cast(a1, ctypes.POINTER(ctypes.c_void_p))
+        d.beta2_elem = ctypes.cast(a2, ctypes.POINTER(ctypes.c_void_p))
+        d.ld_beta = ldb
+    d.Z, d.E, d.L = out.Z.data_ptr(), out.E.data_ptr(), out.L.data_ptr()
+    d.T = out.T.data_ptr() if out.T is not None else None
+    d.ld_out = B
+    d.loss_sums = out.loss_sums.data_ptr() if out.loss_sums is not None else None
+    if kernel_events is not None:  # (torch.cuda.Event, torch.cuda.Event) around the fused kernel
+        d.ev_kernel_start = kernel_events[0].cuda_event
+        d.ev_kernel_stop = kernel_events[1].cuda_event
+
+    wsb = L.dladmm_fwd_workspace_bytes(ctypes.byref(d))
+    if wsb == 0:
+        path = L.dladmm_fwd_path(ctypes.byref(d))
+        _lib.check(path if path < 0 else -7)
+    ws = _workspace(dev, wsb)
+    d.workspace, d.workspace_bytes = ws.data_ptr(), wsb
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _lib.check(L.dladmm_fwd_f32(ctypes.byref(d), ctypes.c_void_p(stream)))
+    del keep
+    return out
+
+
+_WS = {}
+
+
+def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
+    """Per-device cached workspace (grown on demand; torch's allocator keeps it 256-B aligned).
+
+    Reuse is stream-ordered: every call enqueues on the current stream of `dev`.
+    """
+    key = (dev.type, dev.index)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1), device=dev, dtype=torch.uint8)
+        _WS[key] = buf
+    return buf

@@ -1,0 +1,156 @@
+/*
+ * dladmm.h -- C ABI of the MI355X-native fused D-LADMM forward (libdladmm_hip.so).
+ *
+ * The reference (xhchrn/D-LADMM) has no FFI: its interface for this path is the Python
+ * nn.Module `DLADMMNet` whose forward() runs the K-layer Z/E/lambda update loop
+ * (main_lena.py:57-98, main_syn_l1l1_scalar.py:80-127, main_syn_lasso_scalar.py:65-114, ...).
+ * This header is the boundary underneath the drop-in Python module (d-ladmm_amd/model.py):
+ * the whole K-layer loop of one forward() is ONE call of dladmm_fwd_f32().
+ *
+ * Conventions
+ *  - Every matrix is fp32, row-major "features x batch" exactly like the reference tensors
+ *    (X, E, L, T: m x B; Z: n x B; A: m x n; fc[k].weight = W_k: n x m), batch contiguous.
+ *    Row strides (leading dims, in elements) are explicit so batch shards can be views.
+ *  - All pointers are DEVICE pointers except the pointer tables inside the descriptor
+ *    (W, beta1_elem, beta2_elem), which are host arrays of `layers` device pointers.
+ *  - The library never allocates: the caller provides outputs and a workspace of
+ *    dladmm_fwd_workspace_bytes() bytes (device memory, 256-byte aligned).
+ *  - The call is asynchronous on `stream` (a hipStream_t passed as void*); nothing syncs.
+ *  - Return value: 0 on success, a negative DLADMM_E_* code for an invalid descriptor, or a
+ *    positive hipError_t from the HIP runtime.  dladmm_error_string() maps either to text.
+ */
+#ifndef DLADMM_H_
+#define DLADMM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DLADMM_ABI_VERSION 1
+#define DLADMM_MAX_LAYERS 64
+
+/* Reference variants (class DLADMMNet of the named reference script). */
+enum dladmm_variant {
+  DLADMM_V1_LENA = 1,   /* main_lena.py:16-102          beta (m,B) per sample, fixed thetas   */
+  DLADMM_V2_LTHETA = 2, /* main_syn_l1l1_ltheta.py:16-95 beta (m,1), learned (d,1)/(m,1) thetas */
+  DLADMM_V3_FULL = 3,   /* main_syn_l1l1_full.py:16-96   per-row beta1/2/3, ss2, thetas         */
+  DLADMM_V4_SCALAR = 4, /* main_syn_l1l1_scalar.py:34-131 all params (1,1)                     */
+  DLADMM_V5_TIED = 5,   /* main_syn_l1l1_scalar_tied.py:34-104 shared fc, per-layer ss1       */
+  DLADMM_V6_LASSO = 6   /* main_syn_lasso_scalar.py:17-118 linear E-step                      */
+};
+
+/* Per-layer objective reduced inside the kernel (the reference training loop's loss[k]). */
+enum dladmm_loss_kind {
+  DLADMM_LOSS_NONE = 0,
+  DLADMM_LOSS_L1L1 = 1, /* sum|Z_k| and sum|X - A Z_k|        main_syn_l1l1_scalar.py:290-294   */
+  DLADMM_LOSS_LASSO = 2 /* sum|Z_k| and 0.5*sum (X - A Z_k)^2  main_syn_lasso_scalar.py:276-281 */
+};
+
+/* Error codes (negative). */
+#define DLADMM_E_ABI_VERSION (-1)
+#define DLADMM_E_VARIANT (-2)
+#define DLADMM_E_SHAPE (-3)
+#define DLADMM_E_LAYERS (-4)
+#define DLADMM_E_NULL (-5)
+#define DLADMM_E_WORKSPACE (-6)
+#define DLADMM_E_UNSUPPORTED (-7)
+#define DLADMM_E_ALIGN (-8)
+
+/*
+ * Scalar parameter slots, per layer: scalar_params[k * DLADMM_NSCALAR + slot].
+ * For the per-row variants (V2, V3) the same slots live in row_params (see below); for V1 the
+ * betas are per-element tensors and only the two fixed thresholds are read from here.
+ *   beta1  main_lena.py:35            b1 in  Var = L + b1*T                      (all)
+ *   beta2  main_lena.py:36            b2 in  E-step                                (V1-V5)
+ *   beta3  main_syn_l1l1_scalar.py:61 b3 in  L = L + b3*T   (V1/V2 pass beta1)    (all)
+ *   ss2    main_syn_l1l1_scalar.py:62 E = S(E - ss2*VVar)   / LASSO ss2_1          (V3-V6)
+ *   ss2b   main_syn_lasso_scalar.py:47 LASSO ss2_2                                 (V6)
+ *   theta_z / theta_e  active_para / active_para1 (V1: 0.025 / 0.06 fixed)         (all)
+ *   s1     main_syn_l1l1_scalar_tied.py:34 ss1 (1.0 for untied variants)            (V5)
+ */
+enum dladmm_param_slot {
+  DLADMM_P_BETA1 = 0,
+  DLADMM_P_BETA2 = 1,
+  DLADMM_P_BETA3 = 2,
+  DLADMM_P_SS2 = 3,
+  DLADMM_P_SS2B = 4,
+  DLADMM_P_THETA_E = 5,
+  DLADMM_P_THETA_Z = 6,
+  DLADMM_P_S1 = 7,
+  DLADMM_NSCALAR = 8
+};
+
+typedef struct dladmm_fwd_desc {
+  int32_t abi_version; /* = DLADMM_ABI_VERSION */
+  int32_t variant;     /* enum dladmm_variant */
+  int32_t m;           /* rows of A (reference ctor arg m)        */
+  int32_t n;           /* columns of A (reference ctor arg d)     */
+  int32_t batch;       /* columns of X processed by this call     */
+  int32_t layers;      /* K (reference ctor arg layers), <= DLADMM_MAX_LAYERS */
+  int32_t keep_all;    /* 1: write Z/E/L for every layer and T[0..K] (reference return lists);
+                          0: write only layer K-1 (Z,E,L) and T[K]                              */
+  int32_t loss_kind;   /* enum dladmm_loss_kind */
+
+  /* inputs (device) */
+  const float* X;  int64_t ld_x;   /* m x batch */
+  const float* A;  int64_t ld_a;   /* m x n     */
+  const float* Z0; int64_t ld_z0;  /* n x batch */
+  const float* E0; int64_t ld_e0;  /* m x batch */
+  const float* L0; int64_t ld_l0;  /* m x batch */
+
+  /* weights: host array of `layers` device pointers to fc[k].weight (n x m, row stride ld_w).
+     V5 (tied) passes the same pointer `layers` times. */
+  const float* const* W; int64_t ld_w;
+
+  /* parameters (device), see dladmm_param_slot:
+       V4/V5/V6: scalar_params  [layers][DLADMM_NSCALAR]
+       V2/V3:    row_params     [layers][DLADMM_NSCALAR][rows] with rows = max(m, n); the
+                 theta_z slot holds n values, every other slot m values; s1 unused
+       V1:       scalar_params (theta_z/theta_e only) + beta1_elem/beta2_elem: host arrays of
+                 `layers` device pointers to the (m x batch) per-sample betas, row stride ld_beta */
+  const float* scalar_params;
+  const float* row_params; int64_t row_stride; /* elements between slots of one layer */
+  const float* const* beta1_elem;
+  const float* const* beta2_elem;
+  int64_t ld_beta;
+
+  /* outputs (device).  keep_all: Z [K][n][ld_out], E/L [K][m][ld_out], T [K+1][m][ld_out];
+     else one layer each.  T may be NULL (V1-V3 do not return it). */
+  float* Z; float* E; float* L; float* T;
+  int64_t ld_out;
+
+  /* per-layer loss sums (device, fp64): loss_sums[k*2+0] = sum|Z_k|,
+     loss_sums[k*2+1] = sum|X-AZ_k| (L1L1) or 0.5*sum(X-AZ_k)^2 (LASSO).  NULL if loss_kind=0. */
+  double* loss_sums;
+
+  void* workspace; size_t workspace_bytes;
+
+  /* optional profiling: hipEvent_t handles recorded on `stream` immediately before / after the
+     fused K-layer kernel (NULL = not recorded) */
+  void* ev_kernel_start;
+  void* ev_kernel_stop;
+} dladmm_fwd_desc;
+
+/* ABI version the library was built with. */
+int dladmm_abi_version(void);
+
+/* Workspace the call needs for this descriptor (0 on an invalid descriptor). */
+size_t dladmm_fwd_workspace_bytes(const dladmm_fwd_desc* d);
+
+/* Which kernel path this descriptor takes: 1 = fused persistent K-layer kernel,
+   2 = per-layer kernel pair (large shapes), <0 = DLADMM_E_* error. */
+int dladmm_fwd_path(const dladmm_fwd_desc* d);
+
+/* Enqueue the whole K-layer forward on `stream` (hipStream_t). */
+int dladmm_fwd_f32(const dladmm_fwd_desc* d, void* stream);
+
+/* Text for a return code of this library (DLADMM_E_* or hipError_t). */
+const char* dladmm_error_string(int code);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DLADMM_H_ */

@@ -1,0 +1,63 @@
+"""Shared test setup.
+
+Markers: `gpu` = needs a HIP device (run on the MI355X box with `pytest -m gpu`); everything else
+runs on CPU.  The oracle (oracle/dladmm_oracle.py) is imported here only as the checker.
+"""
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+for p in (ROOT, GOLDEN):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a HIP (MI355X) device")
+
+
+def has_gpu():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        return False
+
+
+def pytest_collection_modifyitems(config, items):
+    if has_gpu():
+        return
+    skip = pytest.mark.skip(reason="no HIP device in this container")
+    for it in items:
+        if "gpu" in it.keywords:
+            it.add_marker(skip)
+
+
+@pytest.fixture(scope="session")
+def dl():
+    """The product package (directory name is not an identifier)."""
+    return importlib.import_module("d-ladmm_amd")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle import dladmm_oracle
+    return dladmm_oracle
+
+
+@pytest.fixture(scope="session")
+def problems():
+    import problems as P
+    return P
+
+
+def load_golden(name):
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    meta = json.loads(str(g["meta"]))
+    return g, meta

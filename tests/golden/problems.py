@@ -1,0 +1,169 @@
+"""Deterministic synthetic D-LADMM problems and parameter sets (test data generator).
+
+This is *data generation*, shared by the golden-fixture generator (make_golden.py, run in the
+build container against the reference) and by the tests (which regenerate the same arrays from the
+same seeds and check them against the sha256 recorded in each fixture).
+
+Input distribution follows the reference's synthetic generator
+/root/reference/gen_syn_data.py:14-47:
+  A ~ N(0,1)^{m x n} with unit-norm columns            (gen_syn_data.py:14-16)
+  Z* = Bern(p) * N(mu, sigma)  (n x B)                  (gen_syn_data.py:25-32)
+  E* = Bern(p) * N(mu, sigma)  (m x B)                  (gen_syn_data.py:36-43)
+  X  = A Z* + E*                                        (gen_syn_data.py:46)
+and the reference's initial iterates
+  Z0 = U(0,1)/d, E0 = L0 = 0                            (main_lena.py:181-183)
+
+Parameter sets follow each variant's constructor (reference init) -- see VARIANT_SPECS -- and can
+optionally be perturbed so that per-row / per-element broadcasting is actually exercised.
+The weight init `W_k = s * (A^T + 1e-3 * N(0,1))` is main_lena.py:49 (s = 1) and
+main_syn_l1l1_scalar.py:72 (s = 0.4); we draw the noise from numpy instead of the (unseeded)
+torch RNG so the fixtures are reproducible.
+"""
+from __future__ import annotations
+
+import hashlib
+from collections import OrderedDict
+
+import numpy as np
+
+# name -> (shape kind, reference init value).  Shape kinds: 'mB' (m x batch), 'm1' (m x 1),
+# 'n1' (d x 1), '11' (1 x 1).  Order = registration order = state_dict order.
+VARIANT_SPECS = {
+    # V1 main_lena.py:30-41 (per-sample beta, fixed thresholds 0.025 / 0.06 are NOT params)
+    "v1": dict(params=[("beta1", "mB", 1.0), ("beta2", "mB", 1.0)],
+               fc="per_layer", wscale=1.0, ret_t=False),
+    # V2 main_syn_l1l1_ltheta.py:30-43
+    "v2": dict(params=[("beta1", "m1", 1.0), ("beta2", "m1", 1.0),
+                       ("active_para", "n1", 0.025), ("active_para1", "m1", 0.06)],
+               fc="per_layer", wscale=1.0, ret_t=False),
+    # V3 main_syn_l1l1_full.py:29-44
+    "v3": dict(params=[("beta1", "m1", 1.0), ("beta2", "m1", 1.0), ("beta3", "m1", 1.0),
+                       ("ss2", "m1", 1.0), ("active_para", "n1", 0.2), ("active_para1", "m1", 0.8)],
+               fc="per_layer", wscale=0.4, ret_t=False),
+    # V4 main_syn_l1l1_scalar.py:50-72
+    "v4": dict(params=[("beta1", "11", 1.0), ("beta2", "11", 1.0), ("beta3", "11", 1.0),
+                       ("ss2", "11", 1.0), ("active_para", "11", 0.2), ("active_para1", "11", 0.8)],
+               fc="per_layer", wscale=0.4, ret_t=True),
+    # V5 main_syn_l1l1_scalar_tied.py:50-72 (one shared fc, per-layer ss1)
+    "v5": dict(params=[("beta1", "11", 1.0), ("beta2", "11", 1.0), ("beta3", "11", 1.0),
+                       ("ss1", "11", 1.0), ("ss2", "11", 1.0), ("active_para", "11", 1e-4),
+                       ("active_para1", "11", 1e-2)],
+               fc="tied", wscale=0.4, ret_t=True),
+    # V6 main_syn_lasso_scalar.py:33-57
+    "v6": dict(params=[("beta1", "11", 1.0), ("beta3", "11", 1.0), ("ss2_1", "11", 0.5),
+                       ("ss2_2", "11", 0.5), ("active_para", "11", 0.2)],
+               fc="per_layer", wscale=0.4, ret_t=True),
+}
+
+# Reference source file each variant's class is taken from (fixture generation only).
+VARIANT_SOURCES = {
+    "v1": "main_lena.py",
+    "v2": "main_syn_l1l1_ltheta.py",
+    "v3": "main_syn_l1l1_full.py",
+    "v4": "main_syn_l1l1_scalar.py",
+    "v5": "main_syn_l1l1_scalar_tied.py",
+    "v6": "main_syn_lasso_scalar.py",
+}
+
+
+def _shape(kind: str, m: int, n: int, B: int):
+    return {"mB": (m, B), "m1": (m, 1), "n1": (n, 1), "11": (1, 1)}[kind]
+
+
+def make_inputs(m: int, n: int, B: int, seed: int, p: float = 0.1, sigma: float = 1.0):
+    """gen_syn_data.py:14-47 distribution, fp32, plus Z0/E0/L0 of main_lena.py:181-183."""
+    rng = np.random.default_rng(seed)
+    A = rng.standard_normal((m, n))
+    A = A / np.sqrt(np.sum(A ** 2.0, axis=0, keepdims=True))
+    zs = rng.binomial(1, p, size=(n, B)) * rng.normal(0.0, sigma, size=(n, B))
+    es = rng.binomial(1, p, size=(m, B)) * rng.normal(0.0, sigma, size=(m, B))
+    X = A @ zs + es
+    Z0 = rng.random((n, B)) / n
+    A = A.astype(np.float32)
+    return dict(
+        A=A,
+        X=X.astype(np.float32),
+        Z0=Z0.astype(np.float32),
+        E0=np.zeros((m, B), np.float32),
+        L0=np.zeros((m, B), np.float32),
+        Zstar=zs.astype(np.float32),
+        Estar=es.astype(np.float32),
+    )
+
+
+def make_state_dict(variant: str, m: int, n: int, B: int, K: int, A: np.ndarray, seed: int,
+                    perturb: float = 0.0, wscale: float | None = None,
+                    negtheta: bool = False) -> "OrderedDict[str, np.ndarray]":
+    """state_dict (reference key names and shapes) at the reference init, optionally perturbed.
+
+    perturb > 0 multiplies every entry of every non-weight param by (1 + perturb * U(-1, 1)).
+    negtheta flips the thresholds of every other layer negative (exercises the literal two-relu
+    shrink, main_lena.py:52-53, for theta < 0).
+    """
+    spec = VARIANT_SPECS[variant]
+    rng = np.random.default_rng(seed + 7919)
+    s = spec["wscale"] if wscale is None else wscale
+    sd: "OrderedDict[str, np.ndarray]" = OrderedDict()
+    for name, kind, val in spec["params"]:
+        for k in range(K):
+            shp = _shape(kind, m, n, B)
+            v = np.full(shp, val, np.float64)
+            if perturb > 0:
+                v = v * (1.0 + perturb * rng.uniform(-1.0, 1.0, size=shp))
+            if negtheta and name.startswith("active_para") and k % 2 == 1:
+                v = -0.25 * np.abs(v)
+            sd[f"{name}.{k}"] = v.astype(np.float32)
+    At = A.T.astype(np.float64)
+    if spec["fc"] == "per_layer":
+        for k in range(K):
+            w = (At + 1e-3 * rng.standard_normal(At.shape)) * s
+            sd[f"fc.{k}.weight"] = w.astype(np.float32)
+    else:
+        w = (At + 1e-3 * rng.standard_normal(At.shape)) * s
+        sd["fc.weight"] = w.astype(np.float32)
+    return sd
+
+
+def sha256(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+# The fixture catalogue: name -> problem definition.  Kept here so the tests can regenerate the
+# inputs of any fixture from its recorded definition.
+FIXTURES = {
+    # small shapes: every variant, reference init and perturbed
+    "v1_small_init": dict(variant="v1", m=16, n=32, B=8, K=3, seed=1126),
+    "v1_small_pert": dict(variant="v1", m=16, n=32, B=8, K=3, seed=1127, perturb=0.2, wscale=0.4),
+    "v2_small_pert": dict(variant="v2", m=16, n=32, B=8, K=3, seed=1128, perturb=0.2, wscale=0.4),
+    "v3_small_pert": dict(variant="v3", m=16, n=32, B=8, K=3, seed=1129, perturb=0.2),
+    "v4_small_init": dict(variant="v4", m=16, n=32, B=8, K=3, seed=1130),
+    "v4_small_pert": dict(variant="v4", m=16, n=32, B=8, K=3, seed=1131, perturb=0.2),
+    "v4_small_negtheta": dict(variant="v4", m=16, n=32, B=8, K=4, seed=1132, perturb=0.2,
+                              negtheta=True),
+    "v5_small_pert": dict(variant="v5", m=16, n=32, B=8, K=3, seed=1133, perturb=0.2),
+    "v6_small_pert": dict(variant="v6", m=16, n=32, B=8, K=3, seed=1134, perturb=0.2),
+    # ragged / non-multiple-of-16 shapes (reference synthetic scripts use m=250, d=500)
+    "v4_ragged": dict(variant="v4", m=250, n=500, B=7, K=4, seed=1135, perturb=0.1),
+    "v2_ragged": dict(variant="v2", m=30, n=70, B=5, K=3, seed=1136, perturb=0.2, wscale=0.4),
+    # BASELINE config 1: main_lena.py plumbing shape (A 64 x 256, depth 5, batch 20), V1 default init
+    "v1_lena_cfg1": dict(variant="v1", m=64, n=256, B=20, K=5, seed=1137),
+    # BASELINE config 2 shape (m=256, n=512, depth 15), few columns
+    "v4_med": dict(variant="v4", m=256, n=512, B=12, K=15, seed=1138),
+    "v4_med_pert": dict(variant="v4", m=256, n=512, B=12, K=15, seed=1139, perturb=0.1),
+    "v1_med_w04": dict(variant="v1", m=256, n=512, B=12, K=15, seed=1140, perturb=0.1, wscale=0.4),
+    "v1_med_init": dict(variant="v1", m=256, n=512, B=12, K=15, seed=1141),
+    "v6_med": dict(variant="v6", m=256, n=512, B=12, K=15, seed=1142),
+    "v3_med_pert": dict(variant="v3", m=256, n=512, B=12, K=15, seed=1143, perturb=0.1),
+    # BASELINE config 4 shape (LASSO m=512, n=2048, depth 40), few columns
+    "v6_cfg4": dict(variant="v6", m=512, n=2048, B=4, K=40, seed=1144),
+}
+
+
+def build_problem(defn: dict):
+    """Regenerate (inputs, state_dict) of a fixture definition."""
+    d = dict(defn)
+    inp = make_inputs(d["m"], d["n"], d["B"], d["seed"])
+    sd = make_state_dict(d["variant"], d["m"], d["n"], d["B"], d["K"], inp["A"], d["seed"],
+                         perturb=d.get("perturb", 0.0), wscale=d.get("wscale"),
+                         negtheta=d.get("negtheta", False))
+    return inp, sd

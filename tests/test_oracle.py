@@ -1,0 +1,54 @@
+"""The oracle (CPU restatement) is pinned against golden vectors produced by the reference
+classes themselves (tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+import problems as P
+
+
+@pytest.mark.parametrize("name", sorted(P.FIXTURES))
+def test_inputs_regenerate_bit_exact(name):
+    """The fixture's inputs/params are regenerated from its seed; their sha256 must match what
+    the reference was run on."""
+    g, meta = load_golden(name)
+    inp, sd = P.build_problem(meta["defn"])
+    for k, v in inp.items():
+        assert P.sha256(v) == meta["sha256"][k], k
+    for k, v in sd.items():
+        assert P.sha256(v) == meta["sha256"]["sd:" + k], k
+    assert list(sd.keys()) == meta["keys"], "state_dict key order differs from the reference"
+
+
+@pytest.mark.parametrize("name", sorted(P.FIXTURES))
+def test_oracle_matches_reference(name, oracle):
+    g, meta = load_golden(name)
+    d = meta["defn"]
+    inp, sd = P.build_problem(d)
+    out = oracle.forward(d["variant"], inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd,
+                         d["K"])
+    for nm in ("Z", "E", "L", "T"):
+        if nm not in g.files:
+            assert nm not in out
+            continue
+        ref = g[nm]
+        got = np.stack(out[nm])
+        assert got.shape == ref.shape
+        gap = g["gap_" + nm]
+        for k in range(ref.shape[0]):
+            # same fp32 op sequence; only BLAS summation order may differ from torch's
+            tol = max(1e-5, 3.0 * float(gap[k]))
+            assert oracle.nrel(got[k], ref[k]) <= tol, (nm, k)
+    obj = oracle.layer_objectives(out["Z"], inp["X"], inp["A"], meta["alpha"], "l1l1")
+    np.testing.assert_allclose(obj, g["loss_l1l1"], rtol=1e-5)
+    obj = oracle.layer_objectives(out["Z"], inp["X"], inp["A"], meta["alpha"], "lasso")
+    np.testing.assert_allclose(obj, g["loss_lasso"], rtol=1e-5)
+
+
+def test_literal_two_relu_shrink(oracle):
+    """main_lena.py:52-53 for theta < 0 gives 2x on |x| < -theta (not sign(x)max(|x|-theta,0))."""
+    x = np.array([-1.0, -0.125, 0.0, 0.125, 1.0], np.float32)
+    np.testing.assert_array_equal(oracle.self_active(x, np.float32(-0.25)),
+                                  np.array([-1.25, -0.25, 0.0, 0.25, 1.25], np.float32))
+    np.testing.assert_array_equal(oracle.self_active(x, np.float32(0.25)),
+                                  np.array([-0.75, 0.0, 0.0, 0.0, 0.75], np.float32))
