@@ -120,16 +120,17 @@ def main():
         e.record()  # torch creates the hipEvent lazily; make the handles exist
     torch.cuda.synchronize()
 
+    ddist = importlib.import_module("d-ladmm_amd.dist")
+
     def step(evpair=None):
         r = net.run(X, keep_all=keep_all, loss_kind=dl._lib.LOSS_L1L1, kernel_events=evpair)
-        sums = r.loss_sums
-        if world > 1:
-            dist.all_reduce(sums)  # one RCCL all-reduce of the [K, 2] objective sums over xGMI
-        return r, sums
+        # one RCCL all-reduce of the [K, 2] objective sums over xGMI (no-op at N = 1)
+        obj = ddist.global_objectives(r.loss_sums, a.alpha, B * world)
+        return r, obj
 
     with torch.no_grad():
         for _ in range(a.warmup):
-            r, sums = step()
+            r, obj = step()
             del r
         torch.cuda.synchronize()
         if world > 1:
@@ -137,7 +138,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(a.steps):
-            r, sums = step((ev[2 * i], ev[2 * i + 1]))
+            r, obj = step((ev[2 * i], ev[2 * i + 1]))
             del r
         torch.cuda.synchronize()
         if world > 1:
@@ -150,7 +151,7 @@ def main():
         tt = torch.tensor([elapsed, kern_avg], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, kern_avg = float(tt[0]), float(tt[1])
-    obj = ((a.alpha * sums[:, 0] + sums[:, 1]) / (B * world)).cpu().numpy()
+    obj = obj.cpu().numpy()
 
     if rank == 0:
         total = B * world * a.steps

@@ -1,0 +1,95 @@
+"""N > 1 host logic on CPU with gloo, world_size 2: batch sharding + the one collective.
+
+Each rank runs the oracle (checker) on its column shard, reduces its local objective sums and the
+ranks combine them with dist.global_objectives; the result must equal the full-batch objective,
+and the shards' outputs must tile the full-batch outputs exactly (columns are independent)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import importlib
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests", "golden"))
+    import problems
+    from oracle import dladmm_oracle as oracle
+    ddist = importlib.import_module("d-ladmm_amd.dist")
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m, n, B, K, alpha = 32, 64, 37, 4, 0.001
+    inp = problems.make_inputs(m, n, B, 77)
+    sd = problems.make_state_dict("v4", m, n, B, K, inp["A"], 77, perturb=0.1)
+    s0, s1 = ddist.shard_columns(B, rank, world)
+    cols = slice(s0, s1)
+    out = oracle.forward("v4", inp["X"][:, cols], inp["A"], inp["Z0"][:, cols],
+                         inp["E0"][:, cols], inp["L0"][:, cols], sd, K)
+    sums = torch.zeros(K, 2, dtype=torch.float64)
+    for k in range(K):
+        Zk = out["Z"][k].astype(np.float64)
+        r = inp["X"][:, cols].astype(np.float64) - inp["A"].astype(np.float64) @ Zk
+        sums[k, 0] = float(np.abs(Zk).sum())
+        sums[k, 1] = float(np.abs(r).sum())
+    obj = ddist.global_objectives(sums, alpha, B)
+    q.put((rank, (s0, s1), obj.numpy(), [z for z in out["Z"]]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_shard_and_reduce():
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tests", "golden"))
+    import problems
+    from oracle import dladmm_oracle as oracle
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    m, n, B, K, alpha = 32, 64, 37, 4, 0.001
+    inp = problems.make_inputs(m, n, B, 77)
+    sd = problems.make_state_dict("v4", m, n, B, K, inp["A"], 77, perturb=0.1)
+    full = oracle.forward("v4", inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd, K)
+    ref = oracle.layer_objectives(full["Z"], inp["X"], inp["A"], alpha, "l1l1")
+    assert res[0][1] == (0, 19) and res[1][1] == (19, 37)
+    for _, _, obj, _ in res:
+        np.testing.assert_allclose(obj, ref, rtol=1e-6)
+    for k in range(K):
+        tiled = np.concatenate([res[0][3][k], res[1][3][k]], axis=1)
+        assert oracle.nrel(tiled, full["Z"][k]) <= 1e-6
+
+
+def test_shard_columns_cover_exactly():
+    import importlib
+    ddist = importlib.import_module("d-ladmm_amd.dist")
+    for total in (1, 7, 64, 65536, 262144):
+        for world in (1, 2, 3, 8):
+            spans = [ddist.shard_columns(total, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            for (a0, a1), (b0, b1) in zip(spans, spans[1:]):
+                assert a1 == b0
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
