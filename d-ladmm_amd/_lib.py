@@ -10,7 +10,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libdladmm_hip.so")
+LIB_PATH = os.environ.get("DLADMM_LIB") or os.path.join(HERE, "lib", "libdladmm_hip.so")
 
 ABI_VERSION = 1
 MAX_LAYERS = 64

@@ -27,6 +27,8 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+#include <utility>
+
 namespace dladmm {
 
 enum { EM_V1 = 0, EM_VVAR = 1, EM_LASSO = 2 };   // E-step form
@@ -72,14 +74,35 @@ __device__ __forceinline__ void glds16(const float* gsrc, f32x4* ldst) {
 
 // All waves: own LDS-DMA + LDS reads complete, then workgroup barrier.  One opaque statement,
 // so the compiler can neither hoist ring reads above it nor sink earlier ones below it.
+#ifndef DLADMM_SYNC_MODE
+#define DLADMM_SYNC_MODE 0  // experiment knob: 1 = no vmcnt wait, 2 = no barrier (WRONG results)
+#endif
 __device__ __forceinline__ void ring_barrier() {
+#if DLADMM_SYNC_MODE == 0
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#elif DLADMM_SYNC_MODE == 1
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
 }
 
 // Pin a value to the accumulation register file (AGPR).  The MFMA operands Z and Var live
 // there for the whole forward (MFMA srcA/srcB may be AGPRs on gfx950), leaving the 256 arch
 // VGPRs for E, L, fragments and epilogue temporaries.
-__device__ __forceinline__ void pin_agpr(float& x) { asm volatile("" : "+a"(x)); }
+__device__ __forceinline__ void pin_agpr(float& x) { asm("" : "+a"(x)); }
+
+// Compile-time loop: fn(std::integral_constant<int, 0..N-1>) in order.  The unrolled GEMM
+// phases are written with it (not #pragma unroll) so every step's body is specialised in the
+// front end -- dead epilogue branches never reach the optimiser.
+template <typename Fn, int... Is>
+__device__ __forceinline__ void static_for_impl(Fn&& fn, std::integer_sequence<int, Is...>) {
+  (fn(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename Fn>
+__device__ __forceinline__ void static_for(Fn&& fn) {
+  static_for_impl(fn, std::make_integer_sequence<int, N>{});
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -92,11 +115,15 @@ struct Fused {
   static constexpr int MB = MP / 16;
   static constexpr int NB = NP / 16;
   static constexpr int GF = MB * NB;                // fragments per GEMM
-  static constexpr int CF = GF < 16 ? GF : 16;      // fragments per ring chunk
+#ifndef DLADMM_CHUNK
+#define DLADMM_CHUNK 16
+#endif
+  static constexpr int CF = GF < DLADMM_CHUNK ? GF : DLADMM_CHUNK;  // fragments per ring chunk
   static constexpr int NCH = GF / CF;               // chunks per GEMM
   static constexpr int TAB = 6 * MP + NP;           // per-row param table (floats)
   static constexpr int RING_F4 = 2 * CF * 64;
   static constexpr int TAB_F4 = (PKIND == PK_ROW) ? (3 * TAB) / 4 : 0;  // 3 layer buffers
+  static constexpr int X_F4 = kWaves * MB * 64;  // the tile's X, resident in LDS (fragment order)
   static_assert(MP % 16 == 0 && NP % 16 == 0, "padded dims must be multiples of 16");
   static_assert(GF % CF == 0, "chunking");
   static_assert(TAB % 4 == 0, "table alignment");
@@ -133,9 +160,12 @@ template <int MP, int NP, int EMODE, int PKIND>
 __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   using F = Fused<MP, NP, EMODE, PKIND>;
   constexpr int MB = F::MB, NB = F::NB, CF = F::CF, NCH = F::NCH, TAB = F::TAB;
-  __shared__ f32x4 smem[F::RING_F4 + F::TAB_F4];
+  constexpr int D = 2;         // fragments read ahead of the MFMAs that consume them
+  constexpr int NBUF = D + 1;  // fragment registers in rotation
+  __shared__ f32x4 smem[F::RING_F4 + F::X_F4 + F::TAB_F4];
   f32x4* ring = smem;
-  float* tab = reinterpret_cast<float*>(smem + F::RING_F4);
+  f32x4* xs = smem + F::RING_F4;  // xs[w][b][lane] = X rows 16b+4g+0..3 of this lane's column
+  float* tab = reinterpret_cast<float*>(smem + F::RING_F4 + F::X_F4);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -153,8 +183,7 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   };
 
   float Zr[NB][4], Er[MB][4], Lr[MB][4], Vr[MB][4];
-  float pb[3][4];  // prefetched per-element betas (PK_ELEM) for the pending G2 block
-  float px[4];     // prefetched X rows of the pending G2 block (X is re-read, not resident)
+  float pb[2][3][4];  // per-element betas (PK_ELEM) of the G2 blocks in flight, by block parity
   float regsum = 0.f, fitsum = 0.f;
 
   // ---------------------------------------------------------------- ring (LDS-DMA) stream
@@ -169,13 +198,19 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     f32x4* dst = ring + slot * (CF * 64);
 #pragma unroll
     for (int i = 0; i < (CF + 3) / 4; ++i) {
-      const int f = i * 4 + w;
-      if (f < CF) glds16(base + f * kFrag + lane * 4, dst + f * 64);
+      if constexpr (CF % 4 == 0) {
+        glds16(base + (i * 4 + w) * kFrag + lane * 4, dst + (i * 4 + w) * 64);
+      } else {
+        const int f = i * 4 + w;
+        if (f < CF) glds16(base + f * kFrag + lane * 4, dst + f * 64);
+      }
     }
   };
+  // ring barrier for the chunk about to be consumed, then prefetch the next chunk into the
+  // other slot (always a valid source: past the end of the stream it re-reads packed A)
   auto acquire = [&](const float* next_src) {
     ring_barrier();
-    if (next_src) issue(next_src, cur ^ 1);
+    issue(next_src, cur ^ 1);
   };
   auto frag = [&](int fc) -> f32x4 { return ring[cur * (CF * 64) + fc * 64 + lane]; };
 
@@ -238,7 +273,8 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     const rsrc_t re = mkrsrc(a.E0, (uint32_t)(m * a.lde0 * 4));
     const rsrc_t rl = mkrsrc(a.L0, (uint32_t)(m * a.ldl0 * 4));
     const uint32_t oz = lane_off(a.ldz0), oe = lane_off(a.lde0),
-                   ol = lane_off(a.ldl0);
+                   ol = lane_off(a.ldl0), ox = lane_off(a.ldx);
+    const rsrc_t rx = mkrsrc(a.X, (uint32_t)(m * a.ldx * 4));
 #pragma unroll
     for (int b = 0; b < NB; ++b)
 #pragma unroll
@@ -247,88 +283,90 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
         pin_agpr(Zr[b][r]);
       }
 #pragma unroll
-    for (int b = 0; b < MB; ++b)
+    for (int b = 0; b < MB; ++b) {
+      f32x4 xv;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
+        xv[r] = bload(rx, ox + (uint32_t)((16 * b + r) * a.ldx * 4));
         Er[b][r] = bload(re, oe + (uint32_t)((16 * b + r) * a.lde0 * 4));
         Lr[b][r] = bload(rl, ol + (uint32_t)((16 * b + r) * a.ldl0 * 4));
         Vr[b][r] = 0.0f;
         pin_agpr(Vr[b][r]);
       }
+      xs[(w * MB + b) * 64 + lane] = xv;  // read back only by this wave (no barrier needed)
+    }
   }
   row_tab_load(0, 0);
   issue(a.Ap, 0);
 
   const uint32_t oo = lane_off(a.ldo);                    // output lane offset
-  const uint32_t ox = lane_off(a.ldx);                    // X lane offset
-  const rsrc_t rx = mkrsrc(a.X, (uint32_t)(m * a.ldx * 4));
   const uint32_t ob = lane_off(a.ldb);                    // per-element beta lane offset
   const uint32_t zbytes = (uint32_t)(n * a.ldo * 4), mbytes = (uint32_t)(m * a.ldo * 4);
-
-  // ---------------------------------------------------------------- per-layer epilogues
   Walk zw{oo, (uint32_t)(a.ldo * 4)}, mw{oo, (uint32_t)(a.ldo * 4)};
-  Walk xw{ox, (uint32_t)(a.ldx * 4)}, bw{ob, (uint32_t)(a.ldb * 4)};
-  // G1 block b of layer k: Z = S(Z - s1*(W_k Var), theta_z)    main_lena.py:86 / tied :114
-  auto epi1 = [&](const LayerP& P, rsrc_t rzo, int k, int b, f32x4 c0, f32x4 c1) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float u = c0[r] + c1[r];
-      if constexpr (PKIND == PK_SCALAR) u = P.s1 * u;  // V5 ss1[k]; exactly 1.0 otherwise
-      const float z = shrink(Zr[b][r] - u, prm(P, k, DLADMM_P_THETA_Z, b, r));
-      Zr[b][r] = z;
-      pin_agpr(Zr[b][r]);
-      bstore(rzo, zw.at(r), z);
-      regsum += cv ? fabsf(z) : 0.0f;
-    }
-    zw.next();
+  Walk bw{ob, (uint32_t)(a.ldb * 4)};
+
+  // ---------------------------------------------------------------- per-row epilogues
+  // Each block's epilogue is cut into its 4 accumulator rows; the rows of block b-1 are spread
+  // over the MFMA steps of block b (row r before the MFMAs of step (r * steps) / 4), so the
+  // VALU work and HBM stores issue in the MFMA shadow instead of stalling the matrix pipe.
+  //
+  // G1 block b, row r of layer k: Z = S(Z - s1*(W_k Var), theta_z)  main_lena.py:86 / tied :114
+  auto epi1_row = [&](const LayerP& P, rsrc_t rzo, int k, int b, int r, f32x4 c0, f32x4 c1) {
+    float u = c0[r] + c1[r];
+    if constexpr (PKIND == PK_SCALAR) u = P.s1 * u;  // V5 ss1[k]; exactly 1.0 otherwise
+    const float z = shrink(Zr[b][r] - u, prm(P, k, DLADMM_P_THETA_Z, b, r));
+    Zr[b][r] = z;
+    pin_agpr(Zr[b][r]);
+    bstore(rzo, zw.at(r), z);
+    regsum += cv ? fabsf(z) : 0.0f;
+    if (r == 3) zw.next();
   };
-  // G2 block b of layer k.  Branch-free over k: for the prologue (k = -1, pro = true) the
-  // E/L updates are discarded and T0 = A Z0 + E0 - X (main_lena.py:70) falls out of the same
-  // expression; its E/L stores go to 0-record buffers.
+  // G2 block b, row r of layer k.  Branch-free over k: for the prologue (k = -1) the E/L updates
+  // are discarded and T0 = A Z0 + E0 - X (main_lena.py:70) falls out of the same expression;
+  // its E/L stores go to 0-record buffers.
   struct OutR { rsrc_t e, l, t; };
-  auto epi2 = [&](const LayerP& P, const OutR& O, int k, int b, f32x4 c0, f32x4 c1) {
+  auto epi2_row = [&](const LayerP& P, const OutR& O, int k, int b, int r, f32x4 c0, f32x4 c1,
+                      const f32x4& xv) {
     const bool pro = k < 0;
     const int kp = pro ? 0 : k;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float Pv = c0[r] + c1[r];
-      const float x = px[r];
-      const uint32_t off = mw.at(r);
-      const float l0 = Lr[b][r];
-      float e;
-      if constexpr (EMODE == EM_V1) {
-        // E = S(X - A Z - b2*L, theta_e)                      main_lena.py:87
-        const float b2 = (PKIND == PK_ELEM) ? pb[1][r] : prm(P, kp, DLADMM_P_BETA2, b, r);
-        e = shrink((x - Pv) - b2 * l0, prm(P, kp, DLADMM_P_THETA_E, b, r));
-      } else if constexpr (EMODE == EM_VVAR) {
-        // VVar = L + b2*(A Z + E - X); E = S(E - ss2*VVar)    main_syn_l1l1_scalar.py:114-115
-        const float vv = l0 + prm(P, kp, DLADMM_P_BETA2, b, r) * ((Pv + Er[b][r]) - x);
-        e = shrink(Er[b][r] - prm(P, kp, DLADMM_P_SS2, b, r) * vv,
-                   prm(P, kp, DLADMM_P_THETA_E, b, r));
-      } else {
-        // E = ss2_1*(X - A Z) - ss2_2*L                       main_syn_lasso_scalar.py:102-103
-        e = prm(P, kp, DLADMM_P_SS2, b, r) * (x - Pv) - prm(P, kp, DLADMM_P_SS2B, b, r) * l0;
-      }
-      e = pro ? Er[b][r] : e;
-      const float t = (Pv + e) - x;                            // main_lena.py:70 / :88
-      const float b3 = (PKIND == PK_ELEM) ? pb[0][r] : prm(P, kp, DLADMM_P_BETA3, b, r);
-      const float l = pro ? l0 : l0 + b3 * t;                  // main_lena.py:89 / scalar :118
-      Er[b][r] = e;
-      Lr[b][r] = l;
-      bstore(O.e, off, e);
-      bstore(O.l, off, l);
-      bstore(O.t, off, t);
-      const float res = x - Pv;
-      fitsum += cv ? (lasso ? res * res : fabsf(res)) : 0.0f;
-      // Var of the next layer: L + b1*T  (main_lena.py:85); unused after the last layer
-      float b1n;
-      if constexpr (PKIND == PK_ELEM) b1n = pb[2][r];
-      else if constexpr (PKIND == PK_ROW) b1n = prm(P, k + 1, DLADMM_P_BETA1, b, r);
-      else b1n = P.b1n;
-      Vr[b][r] = l + b1n * t;
-      pin_agpr(Vr[b][r]);
+    float(&pe)[3][4] = pb[b & 1];
+    const float Pv = c0[r] + c1[r];
+    const float x = xv[r];
+    const uint32_t off = mw.at(r);
+    const float l0 = Lr[b][r];
+    float e;
+    if constexpr (EMODE == EM_V1) {
+      // E = S(X - A Z - b2*L, theta_e)                      main_lena.py:87
+      const float b2 = (PKIND == PK_ELEM) ? pe[1][r] : prm(P, kp, DLADMM_P_BETA2, b, r);
+      e = shrink((x - Pv) - b2 * l0, prm(P, kp, DLADMM_P_THETA_E, b, r));
+    } else if constexpr (EMODE == EM_VVAR) {
+      // VVar = L + b2*(A Z + E - X); E = S(E - ss2*VVar)    main_syn_l1l1_scalar.py:114-115
+      const float vv = l0 + prm(P, kp, DLADMM_P_BETA2, b, r) * ((Pv + Er[b][r]) - x);
+      e = shrink(Er[b][r] - prm(P, kp, DLADMM_P_SS2, b, r) * vv,
+                 prm(P, kp, DLADMM_P_THETA_E, b, r));
+    } else {
+      // E = ss2_1*(X - A Z) - ss2_2*L                       main_syn_lasso_scalar.py:102-103
+      e = prm(P, kp, DLADMM_P_SS2, b, r) * (x - Pv) - prm(P, kp, DLADMM_P_SS2B, b, r) * l0;
     }
-    mw.next();
+    e = pro ? Er[b][r] : e;
+    const float t = (Pv + e) - x;                            // main_lena.py:70 / :88
+    const float b3 = (PKIND == PK_ELEM) ? pe[0][r] : prm(P, kp, DLADMM_P_BETA3, b, r);
+    const float l = pro ? l0 : l0 + b3 * t;                  // main_lena.py:89 / scalar :118
+    Er[b][r] = e;
+    Lr[b][r] = l;
+    bstore(O.e, off, e);
+    bstore(O.l, off, l);
+    bstore(O.t, off, t);
+    const float res = x - Pv;
+    fitsum += cv ? (lasso ? res * res : fabsf(res)) : 0.0f;
+    // Var of the next layer: L + b1*T  (main_lena.py:85); unused after the last layer
+    float b1n;
+    if constexpr (PKIND == PK_ELEM) b1n = pe[2][r];
+    else if constexpr (PKIND == PK_ROW) b1n = prm(P, k + 1, DLADMM_P_BETA1, b, r);
+    else b1n = P.b1n;
+    Vr[b][r] = l + b1n * t;
+    pin_agpr(Vr[b][r]);
+    if (r == 3) mw.next();
   };
   // per-wave partial objective of layer k (k < 0: just reset the prologue's sums)
   auto flush_loss = [&](int k) {
@@ -343,11 +381,9 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     regsum = 0.f;
     fitsum = 0.f;
   };
-  auto prefetch_elem = [&](int k, int b) {  // X / betas the G2 epilogue of (k, b) will need
-#pragma unroll
-    for (int r = 0; r < 4; ++r) px[r] = bload(rx, xw.at(r));
-    xw.next();
+  auto prefetch_elem = [&](int k, int b) {  // betas the G2 epilogue of (k, b) will need
     if constexpr (PKIND == PK_ELEM) {
+      float(&pe)[3][4] = pb[b & 1];
       const uint32_t eb = (uint32_t)(m * a.ldb * 4);
       const rsrc_t r1 = mkrsrc(k >= 0 ? a.b1e[k] : nullptr, k >= 0 ? eb : 0u);
       const rsrc_t r2 = mkrsrc(k >= 0 ? a.b2e[k] : nullptr, k >= 0 ? eb : 0u);
@@ -355,9 +391,9 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const uint32_t off = bw.at(r);
-        pb[0][r] = bload(r1, off);
-        pb[1][r] = bload(r2, off);
-        pb[2][r] = bload(rn, off);
+        pe[0][r] = bload(r1, off);
+        pe[1][r] = bload(r2, off);
+        pe[2][r] = bload(rn, off);
       }
       bw.next();
     }
@@ -365,10 +401,12 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
 
   // ---------------------------------------------------------------- the K-layer loop
   // Phase order: G2(-1) [P0 = A Z0], then per layer G1(k) [W_k Var], G2(k) [A Z_k].
-  // Each block's epilogue is deferred to the start of the next block (after its ring barrier),
-  // the last block's epilogue to the start of the next phase.
+  // Every MFMA step: prefetch the fragment D steps ahead from the LDS ring, run the epilogue
+  // rows scheduled on this step, issue 4 MFMAs; a sched_barrier pins that order.
   const int64_t wl = (int64_t)F::GF * kFrag;  // floats per packed W_k
-  f32x4 q0 = {0.f, 0.f, 0.f, 0.f}, q1 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 q0 = {0.f, 0.f, 0.f, 0.f}, q1 = {0.f, 0.f, 0.f, 0.f};  // pending block accumulators
+  f32x4 xpend = {0.f, 0.f, 0.f, 0.f};                           // X rows of the pending G2 block
+  f32x4 fr[NBUF];
   for (int k = -1; k < K; ++k) {
     const bool st = a.keep_all || k == K - 1;
     const int ko = a.keep_all ? k : 0;
@@ -396,68 +434,87 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
       // read in G1(k-1)'s deferred epilogue, several ring barriers ago; its readers (G2(k)
       // epilogues, layer k+1) all come after G1(k)'s first barrier.
       if (k + 1 < K) row_tab_load(k + 1, (k + 1) % 3);
-#pragma unroll
-      for (int b = 0; b < NB; ++b) {
+      static_for<NB>([&](auto B_) {
+        constexpr int b = decltype(B_)::value;
         f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int jb = 0; jb < MB; ++jb) {
-          const int fi = b * MB + jb;
-          if (fi % CF == 0) {
-            const int ch = fi / CF;
+        static_for<MB>([&](auto J_) {
+          constexpr int jb = decltype(J_)::value;
+          constexpr int fi = b * MB + jb, fc = fi % CF;
+          if constexpr (fc == 0) {
+            constexpr int ch = fi / CF;
             acquire(ch + 1 < NCH ? wk + (int64_t)(ch + 1) * CF * kFrag : a.Ap);
+            static_for<D>([&](auto Dd) {
+              constexpr int d = decltype(Dd)::value;
+              if constexpr (fc + d < CF) fr[(fi + d) % NBUF] = frag(fc + d);
+            });
           }
-          if (jb == 0) {
-            if (b == 0) {
-              epi2(Pp, Op, k - 1, MB - 1, q0, q1);
-              flush_loss(k - 1);
-            } else {
-              epi1(P, rzo, k, b - 1, q0, q1);
+          if constexpr (fc + D < CF) fr[(fi + D) % NBUF] = frag(fc + D);
+          static_for<4>([&](auto R_) {
+            constexpr int r = decltype(R_)::value;
+            if constexpr ((r * MB) / 4 == jb) {
+              if constexpr (b == 0) {  // last G2 block of the previous phase
+                if constexpr (r == 0) xpend = xs[(w * MB + MB - 1) * 64 + lane];
+                epi2_row(Pp, Op, k - 1, MB - 1, r, q0, q1, xpend);
+                if constexpr (r == 3) flush_loss(k - 1);
+              } else {
+                epi1_row(P, rzo, k, b - 1, r, q0, q1);
+              }
             }
-          }
-          const f32x4 wv = frag(fi % CF);
+          });
+          const f32x4 wv = fr[fi % NBUF];
           c0 = mfma4(wv.x, Vr[jb][0], c0);
           c1 = mfma4(wv.y, Vr[jb][1], c1);
           c0 = mfma4(wv.z, Vr[jb][2], c0);
           c1 = mfma4(wv.w, Vr[jb][3], c1);
-          if (fi % CF == CF - 1) cur ^= 1;
-        }
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (fc == CF - 1) cur ^= 1;
+        });
         q0 = c0;
         q1 = c1;
-      }
+      });
     }
     // ---- G2(k): P[b] = sum_kb Ap[b][kb] * Z[kb]
-    const float* next_base = (k + 1 < K) ? a.Wp + (int64_t)(k + 1) * wl : nullptr;
+    const float* next_base = (k + 1 < K) ? a.Wp + (int64_t)(k + 1) * wl : a.Ap;
     mw.cur = oo;
-    xw.cur = ox;
     bw.cur = ob;
-#pragma unroll
-    for (int b = 0; b < MB; ++b) {
+    static_for<MB>([&](auto B_) {
+      constexpr int b = decltype(B_)::value;
       f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kb = 0; kb < NB; ++kb) {
-        const int fi = b * NB + kb;
-        if (fi % CF == 0) {
-          const int ch = fi / CF;
+      static_for<NB>([&](auto K_) {
+        constexpr int kb = decltype(K_)::value;
+        constexpr int fi = b * NB + kb, fc = fi % CF;
+        if constexpr (fc == 0) {
+          constexpr int ch = fi / CF;
           acquire(ch + 1 < NCH ? a.Ap + (int64_t)(ch + 1) * CF * kFrag : next_base);
+          static_for<D>([&](auto Dd) {
+            constexpr int d = decltype(Dd)::value;
+            if constexpr (fc + d < CF) fr[(fi + d) % NBUF] = frag(fc + d);
+          });
         }
-        if (kb == 0) {
-          if (b == 0) {
-            if (k >= 0) epi1(P, rzo, k, NB - 1, q0, q1);
-          } else {
-            epi2(P, O, k, b - 1, q0, q1);
+        if constexpr (fc + D < CF) fr[(fi + D) % NBUF] = frag(fc + D);
+        if constexpr (kb == 0) prefetch_elem(k, b);
+        static_for<4>([&](auto R_) {
+          constexpr int r = decltype(R_)::value;
+          if constexpr ((r * NB) / 4 == kb) {
+            if constexpr (b == 0) {  // last G1 block of this layer
+              if (k >= 0) epi1_row(P, rzo, k, NB - 1, r, q0, q1);
+            } else {
+              if constexpr (r == 0) xpend = xs[(w * MB + b - 1) * 64 + lane];
+              epi2_row(P, O, k, b - 1, r, q0, q1, xpend);
+            }
           }
-          prefetch_elem(k, b);
-        }
-        const f32x4 wv = frag(fi % CF);
+        });
+        const f32x4 wv = fr[fi % NBUF];
         c0 = mfma4(wv.x, Zr[kb][0], c0);
         c1 = mfma4(wv.y, Zr[kb][1], c1);
         c0 = mfma4(wv.z, Zr[kb][2], c0);
         c1 = mfma4(wv.w, Zr[kb][3], c1);
-        if (fi % CF == CF - 1) cur ^= 1;
-      }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (fc == CF - 1) cur ^= 1;
+      });
       q0 = c0;
       q1 = c1;
-    }
+    });
   }
   {
     const LayerP P = layer_params(K - 1);
@@ -466,7 +523,9 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
                  mkrsrc(a.Lo + (int64_t)ko * m * a.ldo, mbytes),
                  mkrsrc(a.To ? a.To + (int64_t)(a.keep_all ? K : 0) * m * a.ldo : nullptr,
                         a.To ? mbytes : 0u)};
-    epi2(P, O, K - 1, MB - 1, q0, q1);
+    xpend = xs[(w * MB + MB - 1) * 64 + lane];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) epi2_row(P, O, K - 1, MB - 1, r, q0, q1, xpend);
     flush_loss(K - 1);
   }
 }
