@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--m", type=int, default=256)
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--layers", type=int, default=15)
+    ap.add_argument("--variant", default="v4", choices=["v4", "v6"],
+                    help="v4 = main_syn_l1l1_scalar.py (configs 1-3); v6 = main_syn_lasso_scalar.py "
+                         "(config 4: --m 512 --n 2048 --layers 40)")
     ap.add_argument("--alpha", type=float, default=0.001)
     ap.add_argument("--lean", action="store_true", help="write only the last layer (not default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -71,7 +74,7 @@ def synth(m, n, B, seed, dev):
     return A, X, Z0, E0, L0
 
 
-def cpu_baseline(m, n, K, B):
+def cpu_baseline(m, n, K, B, variant="v4"):
     """The oracle (CPU restatement of the reference forward, numpy fp32 + BLAS) on a bounded
     sample of the same workload: B columns, median of 3 forwards after 1 warmup."""
     from oracle import dladmm_oracle as oracle
@@ -84,8 +87,8 @@ def cpu_baseline(m, n, K, B):
     except Exception:  # pragma: no cover
         cores = os.cpu_count()
     inp = problems.make_inputs(m, n, B, 1126)
-    sd = problems.make_state_dict("v4", m, n, B, K, inp["A"], 1126)
-    args = ("v4", inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd, K)
+    sd = problems.make_state_dict(variant, m, n, B, K, inp["A"], 1126)
+    args = (variant, inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd, K)
     oracle.forward(*args)
     ts = []
     for _ in range(3):
@@ -94,7 +97,7 @@ def cpu_baseline(m, n, K, B):
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
     return {"value": B / t, "unit": "samples/s", "cores": int(cores), "kind": "port",
-            "sample": f"oracle/dladmm_oracle.py V4 forward, m={m} n={n} K={K}, B={B} columns, "
+            "sample": f"oracle/dladmm_oracle.py {variant.upper()} forward, m={m} n={n} K={K}, B={B} columns, "
                       f"fp32 numpy+BLAS, median of 3 after 1 warmup ({t*1e3:.0f} ms/forward)"}
 
 
@@ -112,7 +115,9 @@ def main():
 
     m, n, K, B = a.m, a.n, a.layers, a.batch
     A, X, Z0, E0, L0 = synth(m, n, B, rank, dev)
-    net = dl.DLADMMNetScalar(m=m, n=0, d=n, batch_size=B, A=A, Z0=Z0, E0=E0, L0=L0, layers=K)
+    cls = {"v4": dl.DLADMMNetScalar, "v6": dl.DLADMMNetLasso}[a.variant]
+    net = cls(m=m, n=0, d=n, batch_size=B, A=A, Z0=Z0, E0=E0, L0=L0, layers=K)
+    lk = dl._lib.LOSS_L1L1 if a.variant == "v4" else dl._lib.LOSS_LASSO
     net.requires_grad_(False)
     keep_all = not a.lean
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.steps)]
@@ -123,7 +128,7 @@ def main():
     ddist = importlib.import_module("d-ladmm_amd.dist")
 
     def step(evpair=None):
-        r = net.run(X, keep_all=keep_all, loss_kind=dl._lib.LOSS_L1L1, kernel_events=evpair)
+        r = net.run(X, keep_all=keep_all, loss_kind=lk, kernel_events=evpair)
         # one RCCL all-reduce of the [K, 2] objective sums over xGMI (no-op at N = 1)
         obj = ddist.global_objectives(r.loss_sums, a.alpha, B * world)
         return r, obj
@@ -154,6 +159,10 @@ def main():
     obj = obj.cpu().numpy()
 
     if rank == 0:
+        path = "fused" if (m <= 256 and n <= 512 and os.environ.get("DLADMM_PATH", "")[:1] != "l") \
+            else "per-layer"
+        kname = ("dladmm::fused_kernel (one launch)" if path == "fused" else
+                 f"dladmm::layer_kernel x {2 * K + 1} launches (timed together)")
         total = B * world * a.steps
         value = total / elapsed
         flop = (4 * K + 2) * m * n * B                      # per launch (one rank's shard)
@@ -167,7 +176,8 @@ def main():
         if os.path.exists(a.traffic_json):
             try:
                 tj = json.load(open(a.traffic_json))
-                if tj.get("workload") == f"v4 m={m} n={n} K={K} B={B} keep_all={int(keep_all)}":
+                if tj.get("workload") == \
+                        f"{a.variant} m={m} n={n} K={K} B={B} keep_all={int(keep_all)}":
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
@@ -186,10 +196,12 @@ def main():
             "data": "synthetic (gen_syn_data.py distribution generated on device; reference-init "
                     "V4 parameters, random W = 0.4(A^T + 1e-3 N))",
             "config": {
-                "workload": f"DLADMMNet_scalar (V4) forward m={m} n={n} K={K} B={B}/GPU, all "
-                            f"layers' Z/E/L/T written{'' if keep_all else ' (lean: last only)'} + "
-                            "fused per-layer L1L1 objective",
-                "variant": "v4", "m": m, "n": n, "layers": K, "batch_per_gpu": B,
+                "workload": f"{net.name()} ({a.variant.upper()}) forward m={m} n={n} K={K} "
+                            f"B={B}/GPU, all layers' Z/E/L/T written"
+                            f"{'' if keep_all else ' (lean: last only)'} + fused per-layer "
+                            f"{'L1L1' if a.variant == 'v4' else 'LASSO'} objective",
+                "variant": a.variant, "m": m, "n": n, "layers": K, "batch_per_gpu": B,
+                "path": path,
                 "global_batch": B * world, "keep_all": keep_all,
                 "parallelism": f"batch-shard dp{world} (one RCCL all-reduce of [K,2] sums)",
             },
@@ -200,7 +212,7 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved / PEAK_F32_MFMA,
                 "traffic": traffic,
-                "kernel": "dladmm::fused_kernel<256,512,VVAR,SCALAR>",
+                "kernel": kname,
                 "kernel_ms": kern_avg * 1e3,
                 "flop_per_launch": flop,
                 "algorithmic_bytes_per_launch": bytes_launch,
@@ -209,7 +221,7 @@ def main():
             "objective_last_layer": float(obj[-1]),
         }
         if world == 1 and not a.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(m, n, K, a.cpu_batch)
+            res["cpu_baseline"] = cpu_baseline(m, n, K, a.cpu_batch, a.variant)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -1,0 +1,103 @@
+// dladmm_common.h -- device helpers shared by the fused and the per-layer D-LADMM kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "../../include/dladmm.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace dladmm {
+
+
+enum { EM_V1 = 0, EM_VVAR = 1, EM_LASSO = 2 };   // E-step form
+enum { PK_SCALAR = 0, PK_ROW = 1, PK_ELEM = 2 };  // parameter broadcast class
+
+constexpr int kWaves = 4;
+constexpr int kTileCols = 16 * kWaves;  // batch columns per workgroup
+constexpr int kFrag = 256;              // floats per packed 16x16 fragment (1 KiB)
+
+// literal relu(x - th) - relu(-1.0*x - th) (main_lena.py:52-53); NaN propagates like torch relu
+__device__ __forceinline__ float relu_(float v) { return (v <= 0.0f) ? 0.0f : v; }
+__device__ __forceinline__ float shrink(float x, float th) {
+  return relu_(x - th) - relu_(-x - th);
+}
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void glds16(const float* gsrc, f32x4* ldst) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)gsrc,
+                                   (void __attribute__((address_space(3)))*)ldst, 16, 0, 0);
+}
+
+// All waves: own LDS-DMA + LDS reads complete, then workgroup barrier.  One opaque statement,
+// so the compiler can neither hoist ring reads above it nor sink earlier ones below it.
+#ifndef DLADMM_SYNC_MODE
+#define DLADMM_SYNC_MODE 0  // experiment knob: 1 = no vmcnt wait, 2 = no barrier (WRONG results)
+#endif
+__device__ __forceinline__ void ring_barrier() {
+#if DLADMM_SYNC_MODE == 0
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#elif DLADMM_SYNC_MODE == 1
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+}
+
+// Pin a value to the accumulation register file (AGPR).  The MFMA operands Z and Var live
+// there for the whole forward (MFMA srcA/srcB may be AGPRs on gfx950), leaving the 256 arch
+// VGPRs for E, L, fragments and epilogue temporaries.
+__device__ __forceinline__ void pin_agpr(float& x) { asm("" : "+a"(x)); }
+
+// Compile-time loop: fn(std::integral_constant<int, 0..N-1>) in order.  The unrolled GEMM
+// phases are written with it (not #pragma unroll) so every step's body is specialised in the
+// front end -- dead epilogue branches never reach the optimiser.
+template <typename Fn, int... Is>
+__device__ __forceinline__ void static_for_impl(Fn&& fn, std::integer_sequence<int, Is...>) {
+  (fn(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename Fn>
+__device__ __forceinline__ void static_for(Fn&& fn) {
+  static_for_impl(fn, std::make_integer_sequence<int, N>{});
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+constexpr uint32_t kOOB = 0x80000000u;  // lane offset that is out of range for every buffer
+
+// raw buffer resource; accesses at byte offsets >= bytes are dropped (stores) / read 0 (loads)
+__device__ __forceinline__ rsrc_t mkrsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float bload(rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ void bstore(rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)off, 0, 0);
+}
+typedef const __attribute__((address_space(4))) float* cfloat_p;  // scalar-loaded
+
+// Byte offset walker over the rows 16b + 4g + r of a [rows][ld] matrix, one block at a time.
+// The running offset is made opaque after every step so the compiler cannot precompute (and
+// keep live) one offset register per row of the unrolled layer body.
+struct Walk {
+  uint32_t cur, ld4;
+  __device__ __forceinline__ uint32_t at(int r) const { return cur + (uint32_t)r * ld4; }
+  __device__ __forceinline__ void next() {
+    cur += 16u * ld4;
+    asm volatile("" : "+v"(cur));
+  }
+};
+
+}  // namespace dladmm

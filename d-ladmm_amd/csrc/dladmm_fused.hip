@@ -20,95 +20,10 @@
 // Elementwise arithmetic keeps the reference's evaluation order and is compiled with
 // -ffp-contract=off so every mul/add rounds like the separate torch ops do.
 
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-
-#include "../../include/dladmm.h"
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-#include <utility>
+#include "dladmm_common.h"
+#include "dladmm_internal.h"
 
 namespace dladmm {
-
-enum { EM_V1 = 0, EM_VVAR = 1, EM_LASSO = 2 };   // E-step form
-enum { PK_SCALAR = 0, PK_ROW = 1, PK_ELEM = 2 };  // parameter broadcast class
-
-constexpr int kWaves = 4;
-constexpr int kTileCols = 16 * kWaves;  // batch columns per workgroup
-constexpr int kFrag = 256;              // floats per packed 16x16 fragment (1 KiB)
-
-struct FusedArgs {
-  int m, n, B, K;
-  int keep_all, loss_kind, nwaves;
-  int pad0;
-  const float* X;  int64_t ldx;
-  const float* Z0; int64_t ldz0;
-  const float* E0; int64_t lde0;
-  const float* L0; int64_t ldl0;
-  const float* Ap;   // packed A   [MB][NB] fragments
-  const float* Wp;   // packed W_k [K][NB][MB] fragments
-  const float* scal; // [K][8]
-  const float* rowp; int64_t rstride;  // [K][8][rstride]
-  int64_t ldb;
-  const float* b1e[DLADMM_MAX_LAYERS];
-  const float* b2e[DLADMM_MAX_LAYERS];
-  float* Zo; float* Eo; float* Lo; float* To; int64_t ldo;
-  float* lossp;      // [K][2][nwaves]
-};
-
-// literal relu(x - th) - relu(-1.0*x - th) (main_lena.py:52-53); NaN propagates like torch relu
-__device__ __forceinline__ float relu_(float v) { return (v <= 0.0f) ? 0.0f : v; }
-__device__ __forceinline__ float shrink(float x, float th) {
-  return relu_(x - th) - relu_(-x - th);
-}
-
-__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ void glds16(const float* gsrc, f32x4* ldst) {
-  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)gsrc,
-                                   (void __attribute__((address_space(3)))*)ldst, 16, 0, 0);
-}
-
-// All waves: own LDS-DMA + LDS reads complete, then workgroup barrier.  One opaque statement,
-// so the compiler can neither hoist ring reads above it nor sink earlier ones below it.
-#ifndef DLADMM_SYNC_MODE
-#define DLADMM_SYNC_MODE 0  // experiment knob: 1 = no vmcnt wait, 2 = no barrier (WRONG results)
-#endif
-__device__ __forceinline__ void ring_barrier() {
-#if DLADMM_SYNC_MODE == 0
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#elif DLADMM_SYNC_MODE == 1
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#else
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
-}
-
-// Pin a value to the accumulation register file (AGPR).  The MFMA operands Z and Var live
-// there for the whole forward (MFMA srcA/srcB may be AGPRs on gfx950), leaving the 256 arch
-// VGPRs for E, L, fragments and epilogue temporaries.
-__device__ __forceinline__ void pin_agpr(float& x) { asm("" : "+a"(x)); }
-
-// Compile-time loop: fn(std::integral_constant<int, 0..N-1>) in order.  The unrolled GEMM
-// phases are written with it (not #pragma unroll) so every step's body is specialised in the
-// front end -- dead epilogue branches never reach the optimiser.
-template <typename Fn, int... Is>
-__device__ __forceinline__ void static_for_impl(Fn&& fn, std::integer_sequence<int, Is...>) {
-  (fn(std::integral_constant<int, Is>{}), ...);
-}
-template <int N, typename Fn>
-__device__ __forceinline__ void static_for(Fn&& fn) {
-  static_for_impl(fn, std::make_integer_sequence<int, N>{});
-}
-
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
 
 template <int MP, int NP, int EMODE, int PKIND>
 struct Fused {
@@ -127,33 +42,6 @@ struct Fused {
   static_assert(MP % 16 == 0 && NP % 16 == 0, "padded dims must be multiples of 16");
   static_assert(GF % CF == 0, "chunking");
   static_assert(TAB % 4 == 0, "table alignment");
-};
-
-using rsrc_t = __amdgpu_buffer_rsrc_t;
-constexpr uint32_t kOOB = 0x80000000u;  // lane offset that is out of range for every buffer
-
-// raw buffer resource; accesses at byte offsets >= bytes are dropped (stores) / read 0 (loads)
-__device__ __forceinline__ rsrc_t mkrsrc(const void* p, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ float bload(rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
-}
-__device__ __forceinline__ void bstore(rsrc_t r, uint32_t off, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)off, 0, 0);
-}
-typedef const __attribute__((address_space(4))) float* cfloat_p;  // scalar-loaded
-
-// Byte offset walker over the rows 16b + 4g + r of a [rows][ld] matrix, one block at a time.
-// The running offset is made opaque after every step so the compiler cannot precompute (and
-// keep live) one offset register per row of the unrolled layer body.
-struct Walk {
-  uint32_t cur, ld4;
-  __device__ __forceinline__ uint32_t at(int r) const { return cur + (uint32_t)r * ld4; }
-  __device__ __forceinline__ void next() {
-    cur += 16u * ld4;
-    asm volatile("" : "+v"(cur));
-  }
 };
 
 template <int MP, int NP, int EMODE, int PKIND>
@@ -530,126 +418,6 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   }
 }
 
-// ------------------------------------------------------------------------ weight packing
-struct PackArgs {
-  const float* src[DLADMM_MAX_LAYERS + 1];
-  int R, C, RB, CB;
-  int64_t ld;
-  float* dst;
-};
-
-// dst[t][ib][jb][lane][q] = src_t[16 ib + (lane & 15)][16 jb + 4 (lane >> 4) + q], 0 outside
-__global__ __launch_bounds__(256) void pack_frags_kernel(const PackArgs p) {
-  const int t = blockIdx.y;
-  const int64_t fr = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (fr >= (int64_t)p.RB * p.CB) return;
-  const int lane = threadIdx.x & 63;
-  const int ib = (int)(fr / p.CB), jb = (int)(fr % p.CB);
-  const int row = 16 * ib + (lane & 15);
-  const int c0 = 16 * jb + 4 * (lane >> 4);
-  const float* s = p.src[t];
-  f32x4 v;
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    v[q] = (row < p.R && c0 + q < p.C) ? s[(int64_t)row * p.ld + c0 + q] : 0.0f;
-  reinterpret_cast<f32x4*>(p.dst)[((int64_t)t * p.RB * p.CB + fr) * 64 + lane] = v;
-}
-
-// ------------------------------------------------------------------------ loss reduction
-// sums[i] = sum_w part[i][w] in fp64, fixed order (bitwise reproducible)
-__global__ __launch_bounds__(256) void loss_reduce_kernel(const float* part, int nw, double* sums) {
-  __shared__ double red[256];
-  const int i = blockIdx.x;
-  double s = 0.0;
-  for (int wv = threadIdx.x; wv < nw; wv += 256) s += (double)part[(int64_t)i * nw + wv];
-  red[threadIdx.x] = s;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) sums[i] = red[0];
-}
-
-}  // namespace dladmm
-
-// ======================================================================== host side / C ABI
-namespace dladmm {
-
-struct Shape { int MP, NP; };
-// Register-resident instantiations (state = NP/4 + MP VGPRs per lane; <= 384 at 256 x 512).
-// A problem runs on the smallest instantiation that covers it; zero padding is exact
-// (padded rows of A/W are 0, so padded state rows stay 0 -- see DESIGN.md).
-constexpr Shape kShapes[] = {{16, 32}, {64, 256}, {256, 512}};
-constexpr int kNumShapes = sizeof(kShapes) / sizeof(kShapes[0]);
-
-inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
-
-inline int pick_shape(int m, int n) {
-  for (int i = 0; i < kNumShapes; ++i)
-    if (m <= kShapes[i].MP && n <= kShapes[i].NP) return i;
-  return -1;
-}
-
-struct Plan {
-  int shape, MP, NP, tiles, nwaves;
-  size_t off_ap, off_wp, off_loss, total;
-};
-
-inline int validate(const dladmm_fwd_desc* d) {
-  if (!d) return DLADMM_E_NULL;
-  if (d->abi_version != DLADMM_ABI_VERSION) return DLADMM_E_ABI_VERSION;
-  if (d->variant < DLADMM_V1_LENA || d->variant > DLADMM_V6_LASSO) return DLADMM_E_VARIANT;
-  if (d->m < 1 || d->n < 1 || d->batch < 1) return DLADMM_E_SHAPE;
-  if (d->layers < 1 || d->layers > DLADMM_MAX_LAYERS) return DLADMM_E_LAYERS;
-  if (d->loss_kind < 0 || d->loss_kind > 2) return DLADMM_E_UNSUPPORTED;
-  if (!d->X || !d->A || !d->Z0 || !d->E0 || !d->L0 || !d->W || !d->Z || !d->E || !d->L)
-    return DLADMM_E_NULL;
-  for (int k = 0; k < d->layers; ++k)
-    if (!d->W[k]) return DLADMM_E_NULL;
-  if (d->loss_kind && !d->loss_sums) return DLADMM_E_NULL;
-  const int v = d->variant;
-  if (v == DLADMM_V2_LTHETA || v == DLADMM_V3_FULL) {
-    if (!d->row_params) return DLADMM_E_NULL;
-    if (d->row_stride < d->m || d->row_stride < d->n) return DLADMM_E_SHAPE;
-  } else if (!d->scalar_params) {
-    return DLADMM_E_NULL;
-  }
-  if (v == DLADMM_V1_LENA) {
-    if (!d->beta1_elem || !d->beta2_elem) return DLADMM_E_NULL;
-    for (int k = 0; k < d->layers; ++k)
-      if (!d->beta1_elem[k] || !d->beta2_elem[k]) return DLADMM_E_NULL;
-    if (d->ld_beta < d->batch) return DLADMM_E_SHAPE;
-  }
-  const int64_t B = d->batch;
-  if (d->ld_x < B || d->ld_z0 < B || d->ld_e0 < B || d->ld_l0 < B || d->ld_out < B)
-    return DLADMM_E_SHAPE;
-  if (d->ld_a < d->n || d->ld_w < d->m) return DLADMM_E_SHAPE;
-  // the kernel addresses every per-column matrix with 32-bit buffer offsets (< 2^31 bytes)
-  const int64_t lim = (int64_t)1 << 31;
-  const int64_t mx = d->m > d->n ? d->m : d->n;
-  if (mx * d->ld_x * 4 >= lim || mx * d->ld_z0 * 4 >= lim || mx * d->ld_e0 * 4 >= lim ||
-      mx * d->ld_l0 * 4 >= lim || mx * d->ld_out * 4 >= lim ||
-      (v == DLADMM_V1_LENA && mx * d->ld_beta * 4 >= lim))
-    return DLADMM_E_SHAPE;
-  return 0;
-}
-
-inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
-  const int s = pick_shape(d->m, d->n);
-  if (s < 0) return DLADMM_E_UNSUPPORTED;
-  p->shape = s;
-  p->MP = kShapes[s].MP;
-  p->NP = kShapes[s].NP;
-  p->tiles = (d->batch + kTileCols - 1) / kTileCols;
-  p->nwaves = p->tiles * kWaves;
-  const size_t frag_bytes = (size_t)p->MP * p->NP * sizeof(float);
-  p->off_ap = 0;
-  p->off_wp = align256(frag_bytes);
-  p->off_loss = p->off_wp + align256(frag_bytes * d->layers);
-  p->total = p->off_loss + align256((size_t)2 * d->layers * p->nwaves * sizeof(float));
-  return 0;
-}
 
 template <int MP, int NP, int EM, int PK>
 hipError_t launch_fused(const FusedArgs& a, int grid, hipStream_t s) {
@@ -670,7 +438,8 @@ hipError_t dispatch_variant(int variant, const FusedArgs& a, int grid, hipStream
   return hipErrorInvalidValue;
 }
 
-hipError_t dispatch_shape(int shape, int variant, const FusedArgs& a, int grid, hipStream_t s) {
+hipError_t launch_fused_shape(int shape, int variant, const FusedArgs& a, int grid,
+                              hipStream_t s) {
   switch (shape) {
     case 0: return dispatch_variant<16, 32>(variant, a, grid, s);
     case 1: return dispatch_variant<64, 256>(variant, a, grid, s);
@@ -680,97 +449,3 @@ hipError_t dispatch_shape(int shape, int variant, const FusedArgs& a, int grid, 
 }
 
 }  // namespace dladmm
-
-extern "C" {
-
-int dladmm_abi_version(void) { return DLADMM_ABI_VERSION; }
-
-size_t dladmm_fwd_workspace_bytes(const dladmm_fwd_desc* d) {
-  using namespace dladmm;
-  if (validate(d)) return 0;
-  Plan p;
-  if (make_plan(d, &p)) return 0;
-  return p.total;
-}
-
-int dladmm_fwd_path(const dladmm_fwd_desc* d) {
-  using namespace dladmm;
-  if (int e = validate(d)) return e;
-  return pick_shape(d->m, d->n) >= 0 ? 1 : DLADMM_E_UNSUPPORTED;
-}
-
-int dladmm_fwd_f32(const dladmm_fwd_desc* d, void* stream) {
-  using namespace dladmm;
-  if (int e = validate(d)) return e;
-  Plan p;
-  if (int e = make_plan(d, &p)) return e;
-  if (!d->workspace || d->workspace_bytes < p.total) return DLADMM_E_WORKSPACE;
-  if (((uintptr_t)d->workspace) & 255) return DLADMM_E_ALIGN;
-  hipStream_t s = (hipStream_t)stream;
-  char* ws = (char*)d->workspace;
-  float* Ap = (float*)(ws + p.off_ap);
-  float* Wp = (float*)(ws + p.off_wp);
-  float* lossp = (float*)(ws + p.off_loss);
-  const int MB = p.MP / 16, NB = p.NP / 16;
-
-  // 1. pack A and every W_k into MFMA fragment order (zero-padded to MP x NP)
-  PackArgs pa{};
-  pa.src[0] = d->A;
-  pa.R = d->m; pa.C = d->n; pa.RB = MB; pa.CB = NB; pa.ld = d->ld_a; pa.dst = Ap;
-  hipLaunchKernelGGL(pack_frags_kernel, dim3((MB * NB + 3) / 4, 1), dim3(256), 0, s, pa);
-  PackArgs pw{};
-  for (int k = 0; k < d->layers; ++k) pw.src[k] = d->W[k];
-  pw.R = d->n; pw.C = d->m; pw.RB = NB; pw.CB = MB; pw.ld = d->ld_w; pw.dst = Wp;
-  hipLaunchKernelGGL(pack_frags_kernel, dim3((MB * NB + 3) / 4, d->layers), dim3(256), 0, s, pw);
-  if (hipError_t e = hipGetLastError()) return (int)e;
-
-  // 2. the fused K-layer forward
-  FusedArgs a{};
-  a.m = d->m; a.n = d->n; a.B = d->batch; a.K = d->layers;
-  a.keep_all = d->keep_all ? 1 : 0; a.loss_kind = d->loss_kind; a.nwaves = p.nwaves;
-  a.X = d->X; a.ldx = d->ld_x;
-  a.Z0 = d->Z0; a.ldz0 = d->ld_z0;
-  a.E0 = d->E0; a.lde0 = d->ld_e0;
-  a.L0 = d->L0; a.ldl0 = d->ld_l0;
-  a.Ap = Ap; a.Wp = Wp;
-  a.scal = d->scalar_params;
-  a.rowp = d->row_params; a.rstride = d->row_stride;
-  a.ldb = d->ld_beta;
-  if (d->variant == DLADMM_V1_LENA)
-    for (int k = 0; k < d->layers; ++k) { a.b1e[k] = d->beta1_elem[k]; a.b2e[k] = d->beta2_elem[k]; }
-  a.Zo = d->Z; a.Eo = d->E; a.Lo = d->L; a.To = d->T; a.ldo = d->ld_out;
-  a.lossp = lossp;
-  if (d->ev_kernel_start) {
-    if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_start, s)) return (int)e;
-  }
-  if (hipError_t e = dispatch_shape(p.shape, d->variant, a, p.tiles, s)) return (int)e;
-  if (d->ev_kernel_stop) {
-    if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_stop, s)) return (int)e;
-  }
-
-  // 3. per-layer loss sums, fixed-order fp64 reduction of the per-wave partials
-  if (d->loss_kind) {
-    hipLaunchKernelGGL(loss_reduce_kernel, dim3(2 * d->layers), dim3(256), 0, s,
-                       (const float*)lossp, p.nwaves, d->loss_sums);
-    if (hipError_t e = hipGetLastError()) return (int)e;
-  }
-  return 0;
-}
-
-const char* dladmm_error_string(int code) {
-  switch (code) {
-    case 0: return "success";
-    case DLADMM_E_ABI_VERSION: return "dladmm: descriptor abi_version mismatch";
-    case DLADMM_E_VARIANT: return "dladmm: unknown variant";
-    case DLADMM_E_SHAPE: return "dladmm: invalid shape or leading dimension";
-    case DLADMM_E_LAYERS: return "dladmm: layers must be in [1, DLADMM_MAX_LAYERS]";
-    case DLADMM_E_NULL: return "dladmm: required pointer is NULL";
-    case DLADMM_E_WORKSPACE: return "dladmm: workspace missing or too small";
-    case DLADMM_E_UNSUPPORTED: return "dladmm: unsupported configuration";
-    case DLADMM_E_ALIGN: return "dladmm: workspace must be 256-byte aligned";
-  }
-  if (code > 0) return hipGetErrorString((hipError_t)code);
-  return "dladmm: unknown error";
-}
-
-}  // extern "C"

@@ -1,0 +1,72 @@
+// dladmm_internal.h -- host-side contracts between the C ABI (dladmm_capi.hip) and the kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dladmm_common.h"
+
+namespace dladmm {
+
+struct FusedArgs {
+  int m, n, B, K;
+  int keep_all, loss_kind, nwaves;
+  int pad0;
+  const float* X;  int64_t ldx;
+  const float* Z0; int64_t ldz0;
+  const float* E0; int64_t lde0;
+  const float* L0; int64_t ldl0;
+  const float* Ap;   // packed A   [MB][NB] fragments
+  const float* Wp;   // packed W_k [K][NB][MB] fragments
+  const float* scal; // [K][8]
+  const float* rowp; int64_t rstride;  // [K][8][rstride]
+  int64_t ldb;
+  const float* b1e[DLADMM_MAX_LAYERS];
+  const float* b2e[DLADMM_MAX_LAYERS];
+  float* Zo; float* Eo; float* Lo; float* To; int64_t ldo;
+  float* lossp;      // [K][2][nwaves]
+};
+
+
+// Register-resident instantiations of the fused kernel, by index: (MP, NP).
+constexpr int kNumShapes = 3;
+constexpr int kShapeMP[kNumShapes] = {16, 64, 256};
+constexpr int kShapeNP[kNumShapes] = {32, 256, 512};
+
+hipError_t launch_fused_shape(int shape, int variant, const FusedArgs& a, int grid,
+                              hipStream_t s);
+
+}  // namespace dladmm
+
+namespace dladmm {
+
+// ---- per-layer path (dladmm_layered.hip)
+constexpr int kLayerWaves = 8;                      // waves per layer-kernel workgroup
+constexpr int kLayerCols = 16 * kLayerWaves;        // batch columns per workgroup
+
+struct LayerArgs {
+  int m, n, B, K, k;          // k = layer index; -1 = prologue (T0, Var0)
+  int loss_kind, nslots;      // loss partial slots per (2k+s) row of lossp
+  int KB;                     // 16-row blocks of the contraction
+  int MBp;                    // packed output row-blocks (padded to the slice size)
+  int Krows;                  // valid rows of the B operand
+  const float* Wp;            // packed weights, k-major fragment order [KB][MBp]
+  const float* S; int64_t ldS;          // B operand: Var (G1) or Z_k / Z0 (G2)
+  const float* Zprev; int64_t ldzp;     // G1: Z_{k-1}
+  const float* X; int64_t ldx;          // G2
+  const float* Eprev; int64_t ldep;     // G2: E_{k-1}
+  const float* Lprev; int64_t ldlp;     // G2: L_{k-1}
+  float* Zo; float* Eo; float* Lo; float* To; int64_t ldo;
+  float* Vo; int64_t ldv;               // Var of layer k+1 (workspace)
+  const float* scal;
+  const float* rowp; int64_t rstride;
+  const float* b1e; const float* b2e; const float* b1n_e; int64_t ldb;  // V1 betas
+  float* lossp;
+};
+
+// phase 0 = G1 (W_k Var -> Z_k), 1 = G2 (A Z_k -> E_k, L_k, T_{k+1}, Var_{k+1}),
+// 2 = prologue G2 (A Z0 -> T_0, Var_0).  sb = output blocks per slice (16 or 32).
+hipError_t launch_layer(int phase, int variant, const LayerArgs& a, dim3 grid, int sb,
+                        hipStream_t s);
+
+}  // namespace dladmm

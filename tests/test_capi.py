@@ -62,7 +62,11 @@ def test_validation_codes(dl, field, value, code):
     assert L.dladmm_error_string(code).decode().startswith("dladmm:")
 
 
-def test_unsupported_shape_reported(dl):
+def test_large_shapes_take_the_per_layer_path(dl):
+    """m > 256 or n > 512 (BASELINE config 4: 512 x 2048) exceed the fused kernel's register
+    budget and run as per-layer kernel pairs (path 2)."""
     L = dl._lib.lib()
-    d, _keep = _desc(dl, m=512, n=2048, ld_a=2048, ld_w=512)
-    assert L.dladmm_fwd_path(ctypes.byref(d)) == -7
+    d, _keep = _desc(dl, m=512, n=2048, ld_a=2048, ld_w=512, batch=65536, ld_x=65536,
+                     ld_z0=65536, ld_e0=65536, ld_l0=65536, ld_out=65536)
+    assert L.dladmm_fwd_path(ctypes.byref(d)) == 2
+    assert L.dladmm_fwd_workspace_bytes(ctypes.byref(d)) > 15 * 2048 * 512 * 4

@@ -40,16 +40,10 @@ def make_net(dl, variant, inp, sd, K):
     return net
 
 
-def fused_supported(d):
-    return d["m"] <= 256 and d["n"] <= 512
-
-
 @pytest.mark.parametrize("name", sorted(P.FIXTURES))
 def test_matches_reference_golden(name, dl):
     g, meta = load_golden(name)
     d = meta["defn"]
-    if not fused_supported(d):
-        pytest.skip("shape needs the per-layer path")
     inp, sd = P.build_problem(d)
     net = make_net(dl, d["variant"], inp, sd, d["K"])
     X = torch.from_numpy(inp["X"]).cuda()
@@ -234,3 +228,38 @@ def test_baseline_size_column_subset_and_fused_loss(dl, oracle):
         Zk = r.Z[k].double()
         sep.append(float((0.001 * Zk.abs().sum() + (Xd.double() - Ad @ Zk).abs().sum()) / B))
     np.testing.assert_allclose(obj.cpu().numpy(), np.array(sep), rtol=1e-5)
+
+
+# ------------------------------------------------------------------ per-layer path (path 2)
+@pytest.mark.parametrize("variant", ["v1", "v2", "v3", "v4", "v5", "v6"])
+def test_per_layer_path_vs_oracle(variant, dl, oracle):
+    """m > 256: beyond the fused kernel's register budget -> per-layer kernel pairs."""
+    m, n, B, K = 300, 600, 150, 6
+    inp, sd, ref = _oracle_case(oracle, variant, m, n, B, K, seed=9000 + K,
+                                wscale=0.4 if variant in ("v1", "v2") else None)
+    net = make_net(dl, variant, inp, sd, K)
+    with torch.no_grad():
+        out = net(torch.from_numpy(inp["X"]).cuda())
+    _compare(out, ref, tag=f"layered {variant}")
+
+
+@pytest.mark.parametrize("variant", ["v4", "v1", "v6"])
+def test_forced_per_layer_path_matches_fused(variant, dl, monkeypatch):
+    """The same problem through both paths (DLADMM_PATH=layered forces path 2): outputs agree
+    to fp32 summation-order noise, the lean mode and the fused objective too."""
+    m, n, B, K = 256, 512, 333, 5
+    inp = P.make_inputs(m, n, B, 9100)
+    sd = P.make_state_dict(variant, m, n, B, K, inp["A"], 9100, perturb=0.1, wscale=0.4)
+    net = make_net(dl, variant, inp, sd, K)
+    X = torch.from_numpy(inp["X"]).cuda()
+    with torch.no_grad():
+        rf, of = net.layer_objectives(X, 0.001, "l1l1")
+        monkeypatch.setenv("DLADMM_PATH", "layered")
+        rl, ol = net.layer_objectives(X, 0.001, "l1l1")
+        lean = net.run(X, keep_all=False)
+        monkeypatch.delenv("DLADMM_PATH")
+    for a, b in ((rf.Z, rl.Z), (rf.E, rl.E), (rf.L, rl.L)):
+        for k in range(K):
+            assert nrel(b[k].cpu().numpy(), a[k].cpu().numpy()) <= 2e-6
+    assert torch.equal(lean.Z[0], rl.Z[-1]) and torch.equal(lean.L[0], rl.L[-1])
+    np.testing.assert_allclose(ol.cpu().numpy(), of.cpu().numpy(), rtol=2e-6)
