@@ -30,9 +30,21 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ void glds16(const float* gsrc, f32x4* ldst) {
-  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)gsrc,
-                                   (void __attribute__((address_space(3)))*)ldst, 16, 0, 0);
+// LDS-DMA of one 1 KiB fragment: lane l copies 16 B from sbase + voff to ldst + 16 l.
+// sbase and ldst are wave-uniform.  Written as inline asm on purpose: when the compiler sees an
+// LDS-DMA (the __builtin_amdgcn_global_load_lds form) in a loop it stops counting LDS reads and
+// emits lgkmcnt(0) before every fragment use, which collapses the fragment read-ahead to one
+// step.  The hardware counts LDS-DMA on vmcnt only; ring_barrier() waits for it explicitly.
+// M0 is compiler-reserved, so it is saved and restored inside the same statement.
+__device__ __forceinline__ void glds16(const float* sbase, uint32_t voff, f32x4* ldst) {
+  unsigned keep;
+  const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ldst);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(dst)
+      : "memory");
 }
 
 // All waves: own LDS-DMA + LDS reads complete, then workgroup barrier.  One opaque statement,

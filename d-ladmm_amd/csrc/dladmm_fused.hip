@@ -63,7 +63,7 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   const bool cv = col < a.B;
   const int m = a.m, n = a.n, K = a.K;
   const bool lossz = a.loss_kind != 0;
-  const bool lasso = a.loss_kind == DLADMM_LOSS_LASSO;
+  const bool lasso = __builtin_amdgcn_readfirstlane(a.loss_kind) == DLADMM_LOSS_LASSO;
 
   // per-lane byte offset of (row 4g, column col) in a [rows][ld] fp32 matrix; kOOB for padding
   auto lane_off = [&](int64_t ld) -> uint32_t {
@@ -87,10 +87,10 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
 #pragma unroll
     for (int i = 0; i < (CF + 3) / 4; ++i) {
       if constexpr (CF % 4 == 0) {
-        glds16(base + (i * 4 + w) * kFrag + lane * 4, dst + (i * 4 + w) * 64);
+        glds16(base + (i * 4 + w) * kFrag, lane * 16, dst + (i * 4 + w) * 64);
       } else {
         const int f = i * 4 + w;
-        if (f < CF) glds16(base + f * kFrag + lane * 4, dst + f * 64);
+        if (f < CF) glds16(base + f * kFrag, lane * 16, dst + f * 64);
       }
     }
   };
@@ -206,7 +206,8 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     Zr[b][r] = z;
     pin_agpr(Zr[b][r]);
     bstore(rzo, zw.at(r), z);
-    regsum += cv ? fabsf(z) : 0.0f;
+    // no column mask: padded columns hold exactly zero state (X = Z0 = E0 = L0 = 0)
+    regsum += fabsf(z);
     if (r == 3) zw.next();
   };
   // G2 block b, row r of layer k.  Branch-free over k: for the prologue (k = -1) the E/L updates
@@ -246,7 +247,7 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     bstore(O.l, off, l);
     bstore(O.t, off, t);
     const float res = x - Pv;
-    fitsum += cv ? (lasso ? res * res : fabsf(res)) : 0.0f;
+    fitsum += fabsf(res) * (lasso ? fabsf(res) : 1.0f);  // |r| or r^2; branch-free
     // Var of the next layer: L + b1*T  (main_lena.py:85); unused after the last layer
     float b1n;
     if constexpr (PKIND == PK_ELEM) b1n = pe[2][r];

@@ -69,7 +69,7 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_kernel(const LayerArgs a) {
 #pragma unroll
     for (int i = 0; i < (CF + NW - 1) / NW; ++i) {
       const int f = i * NW + w;
-      if (CF % NW == 0 || f < CF) glds16(base + f * kFrag + lane * 4, dst + f * 64);
+      if (CF % NW == 0 || f < CF) glds16(base + f * kFrag, lane * 16, dst + f * 64);
     }
   };
 
