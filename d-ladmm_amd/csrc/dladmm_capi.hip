@@ -12,9 +12,12 @@ namespace dladmm {
 struct PackArgs {
   const float* src[DLADMM_MAX_LAYERS + 1];
   int R, C, RB, CB;  // valid rows/cols of each source; row-blocks (padded) / col-blocks packed
-  int kmajor;        // 0: fragment (ib, jb) at ib*CB + jb   1: at jb*RB + ib (per-layer path)
+  int order;         // fragment (ib, jb) at: 0 ib*CB + jb; 1 jb*RB + ib (per-layer path);
+                     // 2 ((ib/2)*CB + jb)*2 + ib%2 (fused path: output blocks in pairs)
   int64_t ld;
   float* dst;
+  float sign;          // every element is multiplied by sign * (scal ? scal[t][S1] : 1)
+  const float* scal;   // device [T][DLADMM_NSCALAR] (V4-V6 s1) or null
 };
 
 // fragment (ib, jb) of source t: dst[..][lane][q] = src_t[16 ib + (lane & 15)][16 jb + 4 (lane >> 4) + q]
@@ -24,15 +27,18 @@ __global__ __launch_bounds__(256) void pack_frags_kernel(const PackArgs p) {
   const int64_t fr = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (fr >= (int64_t)p.RB * p.CB) return;
   const int lane = threadIdx.x & 63;
-  const int ib = p.kmajor ? (int)(fr % p.RB) : (int)(fr / p.CB);
-  const int jb = p.kmajor ? (int)(fr / p.RB) : (int)(fr % p.CB);
+  int ib, jb;
+  if (p.order == 0) { ib = (int)(fr / p.CB); jb = (int)(fr % p.CB); }
+  else if (p.order == 1) { ib = (int)(fr % p.RB); jb = (int)(fr / p.RB); }
+  else { const int64_t q = fr >> 1; jb = (int)(q % p.CB); ib = 2 * (int)(q / p.CB) + (int)(fr & 1); }
+  const float f = p.sign * (p.scal ? p.scal[t * DLADMM_NSCALAR + DLADMM_P_S1] : 1.0f);
   const int row = 16 * ib + (lane & 15);
   const int c0 = 16 * jb + 4 * (lane >> 4);
   const float* s = p.src[t];
   f32x4 v;
 #pragma unroll
   for (int q = 0; q < 4; ++q)
-    v[q] = (row < p.R && c0 + q < p.C) ? s[(int64_t)row * p.ld + c0 + q] : 0.0f;
+    v[q] = (row < p.R && c0 + q < p.C) ? f * s[(int64_t)row * p.ld + c0 + q] : 0.0f;
   reinterpret_cast<f32x4*>(p.dst)[((int64_t)t * p.RB * p.CB + fr) * 64 + lane] = v;
 }
 
@@ -168,10 +174,12 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
 
 // ---- pack helpers
 inline hipError_t pack(const float* const* srcs, int T, int R, int C, int64_t ld, int RB, int CB,
-                       int kmajor, float* dst, hipStream_t s) {
+                       int order, float* dst, hipStream_t s, float sign = 1.0f,
+                       const float* scal = nullptr) {
   PackArgs pa{};
   for (int t = 0; t < T; ++t) pa.src[t] = srcs[t];
-  pa.R = R; pa.C = C; pa.RB = RB; pa.CB = CB; pa.kmajor = kmajor; pa.ld = ld; pa.dst = dst;
+  pa.R = R; pa.C = C; pa.RB = RB; pa.CB = CB; pa.order = order; pa.ld = ld; pa.dst = dst;
+  pa.sign = sign; pa.scal = scal;
   hipLaunchKernelGGL(pack_frags_kernel, dim3((RB * CB + 3) / 4, T), dim3(256), 0, s, pa);
   return hipGetLastError();
 }
@@ -181,10 +189,14 @@ inline int run_fused(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStrea
   float* Wp = (float*)(ws + p.off_wp);
   float* lossp = (float*)(ws + p.off_loss);
   const int MB = p.MP / 16, NB = p.NP / 16;
-  // 1. pack A and every W_k into MFMA fragment order (zero-padded to MP x NP)
+  // 1. pack A and every -s1_k W_k into paired MFMA fragment order (zero-padded to MP x NP);
+  //    s1 is ss1[k] for V5 and 1.0 in the V4/V6 tables; V1-V3 have no step size
   const float* asrc[1] = {d->A};
-  if (hipError_t e = pack(asrc, 1, d->m, d->n, d->ld_a, MB, NB, 0, Ap, s)) return (int)e;
-  if (hipError_t e = pack(d->W, d->layers, d->n, d->m, d->ld_w, NB, MB, 0, Wp, s)) return (int)e;
+  const bool has_s1 = d->variant >= DLADMM_V4_SCALAR;
+  if (hipError_t e = pack(asrc, 1, d->m, d->n, d->ld_a, MB, NB, 2, Ap, s)) return (int)e;
+  if (hipError_t e = pack(d->W, d->layers, d->n, d->m, d->ld_w, NB, MB, 2, Wp, s, -1.0f,
+                          has_s1 ? d->scalar_params : nullptr))
+    return (int)e;
   // 2. the fused K-layer forward
   FusedArgs a{};
   a.m = d->m; a.n = d->n; a.B = d->batch; a.K = d->layers;

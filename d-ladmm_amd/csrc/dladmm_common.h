@@ -26,6 +26,21 @@ __device__ __forceinline__ float shrink(float x, float th) {
   return relu_(x - th) - relu_(-x - th);
 }
 
+// Two-VALU-op form for a wave-uniform threshold: x + sg * clamp(x, -|th|, |th|), sg = -1 for
+// th >= 0 and +1 for th < 0 (fma by +-1 is a single exact add/sub).
+//  * th >= 0: bit-identical to the literal form (x > th: fl(x - th) both ways; x < -th:
+//    -fl(-x - th) = fl(x + th); otherwise +0);
+//  * th < 0 (both relus open): identical for |x| >= |th|; for |x| < |th| it returns 2x where
+//    the literal form rounds fl(fl(x - th) - fl(-x - th)) -- within one ulp of |th|.
+// No per-element branch: a uniform branch per row splits the unrolled body and costs spills.
+struct ShrinkP { float ath, sg; };
+__device__ __forceinline__ ShrinkP shrink_params(float th) {
+  return ShrinkP{fabsf(th), th >= 0.0f ? -1.0f : 1.0f};
+}
+__device__ __forceinline__ float shrink_u(float x, ShrinkP p) {
+  return __builtin_fmaf(p.sg, __builtin_amdgcn_fmed3f(x, -p.ath, p.ath), x);
+}
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -98,6 +113,10 @@ __device__ __forceinline__ float bload(rsrc_t r, uint32_t off) {
 __device__ __forceinline__ void bstore(rsrc_t r, uint32_t off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)off, 0, 0);
 }
+// store with a wave-uniform row offset in soffset: no per-lane address arithmetic
+__device__ __forceinline__ void bstore_s(rsrc_t r, uint32_t voff, uint32_t soff, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)voff, (int)soff, 0);
+}
 typedef const __attribute__((address_space(4))) float* cfloat_p;  // scalar-loaded
 
 // Byte offset walker over the rows 16b + 4g + r of a [rows][ld] matrix, one block at a time.
@@ -109,6 +128,23 @@ struct Walk {
   __device__ __forceinline__ void next() {
     cur += 16u * ld4;
     asm volatile("" : "+v"(cur));
+  }
+};
+
+// Uniform (SGPR) byte offset of rows 16b + r of a [rows][ld] matrix, one block at a time; the
+// lane's own 4g row and column live in the buffer instruction's voffset.
+struct SWalk {
+  uint32_t cur, ld4;
+  __device__ __forceinline__ uint32_t at(int r) const { return cur + (uint32_t)r * ld4; }
+  __device__ __forceinline__ void next() {
+    // readfirstlane: the value is uniform, but the uniformity analysis may not prove it after
+    // divergent regions (per-row table loads), and the asm below needs an SGPR
+    cur = __builtin_amdgcn_readfirstlane(cur + 16u * ld4);
+    asm volatile("" : "+s"(cur));
+  }
+  __device__ __forceinline__ void reset() {
+    cur = 0u;
+    asm volatile("" : "+s"(cur));
   }
 };
 

@@ -6,22 +6,36 @@
 //
 // Design (DESIGN.md has the full derivation):
 //  * one workgroup = 4 waves = a tile of 64 batch columns; wave w owns columns 16w..16w+15;
-//  * the whole per-column state -- Z (n), E, L, X and T/Var (m each) -- stays in registers for
-//    all K layers, laid out exactly like the C/D fragment of v_mfma_f32_16x16x4_f32:
-//    lane l holds column (l & 15) and feature rows 16*b + 4*(l >> 4) + r, r = 0..3;
-//  * with that layout the accumulator of one GEMM IS the B operand of the next: U = W_k*Var
-//    lands in Z's layout, P = A*Z lands in E/L/T's layout, and every shrink / AXPY of the
-//    reference is lane-local -- no LDS transpose, no HBM round trip for the state;
-//  * W_k and A are pre-packed (pack_frags_kernel) into "fragment order" (1 KiB per 16x16
-//    fragment = exactly what one wave's lanes need for 4 MFMAs), streamed from L2/MALL by
-//    global_load_lds_dwordx4 into a double-buffered LDS ring shared by the 4 waves;
-//  * epilogues are deferred by one block so each block's HBM stores overlap the next block's
-//    MFMAs instead of being drained by the next ring barrier.
-// Elementwise arithmetic keeps the reference's evaluation order and is compiled with
-// -ffp-contract=off so every mul/add rounds like the separate torch ops do.
+//  * the whole per-column state -- Z (n), E, L and Var (m each) -- stays in registers for all K
+//    layers, laid out exactly like the C/D fragment of v_mfma_f32_16x16x4_f32: lane l holds
+//    column (l & 15) and feature rows 16*b + 4*(l >> 4) + r, r = 0..3; X sits in LDS;
+//  * with that layout the accumulator of one GEMM IS the B operand of the next: W_k*Var lands
+//    in Z's layout, A*Z lands in E/L/T's layout, and every shrink / AXPY of the reference is
+//    lane-local -- no LDS transpose, no HBM round trip for the state;
+//  * two output blocks are computed together (two independent MFMA chains, so neither waits
+//    on the MFMA's dependent-issue latency and no partial sums need combining); W_k is packed
+//    as -s1*W_k so the Z update is one add.  The chains start at zero: starting them at Z or
+//    -X (saving that add) accumulates every rounding at the state's magnitude and measurably
+//    loses accuracy against the reference on cancelling residuals;
+//  * W_k and A are pre-packed (pack_frags_kernel) into paired fragment order (1 KiB per 16x16
+//    fragment = what one wave's lanes need for 4 MFMAs) and streamed from L2/MALL by
+//    LDS-DMA into a 3-slot LDS ring shared by the 4 waves (one chunk read, one landed, one in
+//    flight), so the next chunk's first fragments are read ahead before the current one ends;
+//  * each pair's epilogue (shrink, E/L/T/Var updates, HBM stores, objective partial sums) is
+//    cut into its 8 rows and spread over the MFMA steps of the next pair.
+// Elementwise arithmetic is compiled with -ffp-contract=off; a uniform-threshold shrink uses
+// the clamp form x -+ med3(x, -|th|, |th|), which equals the reference's two-relu form for
+// th >= 0 bit for bit (common.h).
 
 #include "dladmm_common.h"
 #include "dladmm_internal.h"
+
+#ifndef DLADMM_ABLATE
+#define DLADMM_ABLATE 0  // timing experiments only, see tools/ablate.py
+#endif
+#ifndef DLADMM_CHUNK
+#define DLADMM_CHUNK 16
+#endif
 
 namespace dladmm {
 
@@ -30,26 +44,26 @@ struct Fused {
   static constexpr int MB = MP / 16;
   static constexpr int NB = NP / 16;
   static constexpr int GF = MB * NB;                // fragments per GEMM
-#ifndef DLADMM_CHUNK
-#define DLADMM_CHUNK 16
-#endif
   static constexpr int CF = GF < DLADMM_CHUNK ? GF : DLADMM_CHUNK;  // fragments per ring chunk
   static constexpr int NCH = GF / CF;               // chunks per GEMM
   static constexpr int TAB = 6 * MP + NP;           // per-row param table (floats)
-  static constexpr int RING_F4 = 2 * CF * 64;
+  static constexpr int RING_F4 = 3 * CF * 64;       // 3 slots
   static constexpr int TAB_F4 = (PKIND == PK_ROW) ? (3 * TAB) / 4 : 0;  // 3 layer buffers
-  static constexpr int X_F4 = kWaves * MB * 64;  // the tile's X, resident in LDS (fragment order)
-  static_assert(MP % 16 == 0 && NP % 16 == 0, "padded dims must be multiples of 16");
-  static_assert(GF % CF == 0, "chunking");
+  static constexpr int X_F4 = kWaves * MB * 64;     // the tile's X, resident in LDS
+  static_assert(MB % 2 == 0 && NB % 2 == 0, "output blocks are processed in pairs");
+  static_assert(GF % CF == 0 && CF % 2 == 0, "chunking");
   static_assert(TAB % 4 == 0, "table alignment");
+  static_assert((RING_F4 + X_F4 + TAB_F4) * 16 <= 160 * 1024, "LDS budget");
 };
+
+// pending epilogue row i (0..7: block half i/4, row i%4) runs at step (i * SP) / 8 of a pair of
+// SP steps
+constexpr bool rows_at(int step, int SP, int i) { return (i * SP) / 8 == step; }
 
 template <int MP, int NP, int EMODE, int PKIND>
 __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   using F = Fused<MP, NP, EMODE, PKIND>;
   constexpr int MB = F::MB, NB = F::NB, CF = F::CF, NCH = F::NCH, TAB = F::TAB;
-  constexpr int D = 2;         // fragments read ahead of the MFMAs that consume them
-  constexpr int NBUF = D + 1;  // fragment registers in rotation
   __shared__ f32x4 smem[F::RING_F4 + F::X_F4 + F::TAB_F4];
   f32x4* ring = smem;
   f32x4* xs = smem + F::RING_F4;  // xs[w][b][lane] = X rows 16b+4g+0..3 of this lane's column
@@ -70,37 +84,45 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     return cv ? (uint32_t)((col + (int64_t)(4 * g) * ld) * 4) : kOOB;
   };
 
+  // V1 never reads E after the prologue (its E-step has no E term), so E is not state there:
+  // the prologue's E0 arrives through the per-element prefetch instead (b2's slot).
+  constexpr bool kEState = !(EMODE == EM_V1 && PKIND == PK_ELEM);
   float Zr[NB][4], Er[MB][4], Lr[MB][4], Vr[MB][4];
-  float pb[2][3][4];  // per-element betas (PK_ELEM) of the G2 blocks in flight, by block parity
-  float regsum = 0.f, fitsum = 0.f;
+  float pb[2][3][4];  // PK_ELEM: betas (b3, b2, b1 of k+1) of the pending G2 pair
+  float pn[2][3][4];  // PK_ELEM: the same for the pair being computed (loads in flight)
+  float regsum = 0.f, fit1 = 0.f, fit2 = 0.f;
 
   // ---------------------------------------------------------------- ring (LDS-DMA) stream
-  int cur = 0;  // slot of the chunk being consumed
-  auto issue = [&](const float* src, int slot) {
-    // opaque uniform base: stops the compiler from precomputing (and keeping live) the
-    // 64-bit per-lane address of every chunk of the stream; the load becomes
-    // global_load_lds_dwordx4 voff, s[base] with a loop-invariant 32-bit lane offset
-    uint64_t sb = (uint64_t)src;
+  // The stream is the GEMM sequence A (prologue), W_0, A, W_1, A, ..., W_{K-1}, A, then A again
+  // as harmless filler.  GEMM gi: 0 = prologue A, 2k+1 = W_k, 2k+2 = A.
+  const int64_t wl = (int64_t)F::GF * kFrag;  // floats per packed W_k
+  auto gsrc = [&](int gi) -> const float* {
+    const int kk = gi >> 1;
+    return ((gi & 1) && kk < K) ? a.Wp + (int64_t)kk * wl : a.Ap;
+  };
+  // source of chunk ch (may run past the GEMM) of GEMM gi
+  // The GEMM base goes through an opaque statement before the chunk offset is added: otherwise
+  // the compiler precomputes the (loop-invariant) address of every chunk of A and keeps them
+  // all live in SGPRs.
+  auto chunk_src = [&](int gi, int ch) -> const float* {
+    uint64_t sb = (uint64_t)gsrc(gi + ch / NCH);
     asm volatile("" : "+s"(sb));
-    const float* base = (const float*)sb;
+    return (const float*)sb + (ch % NCH) * CF * kFrag;
+  };
+  auto issue = [&](const float* base, int slot) {
     f32x4* dst = ring + slot * (CF * 64);
+#if DLADMM_ABLATE & 1  // timing experiment: no weight stream (WRONG results)
+    if (base != a.Ap) return;
+#endif
 #pragma unroll
     for (int i = 0; i < (CF + 3) / 4; ++i) {
-      if constexpr (CF % 4 == 0) {
-        glds16(base + (i * 4 + w) * kFrag, lane * 16, dst + (i * 4 + w) * 64);
-      } else {
-        const int f = i * 4 + w;
-        if (f < CF) glds16(base + f * kFrag, lane * 16, dst + f * 64);
-      }
+      const int f = i * 4 + w;
+      if (CF % 4 == 0 || f < CF) glds16(base + f * kFrag, lane * 16, dst + f * 64);
     }
   };
-  // ring barrier for the chunk about to be consumed, then prefetch the next chunk into the
-  // other slot (always a valid source: past the end of the stream it re-reads packed A)
-  auto acquire = [&](const float* next_src) {
-    ring_barrier();
-    issue(next_src, cur ^ 1);
-  };
-  auto frag = [&](int fc) -> f32x4 { return ring[cur * (CF * 64) + fc * 64 + lane]; };
+  auto slot_add = [](int s, int d) -> int { s += d; return s >= 3 ? s - 3 : s; };
+  int cur = 0;  // ring slot of the chunk being consumed
+  auto frag = [&](int slot, int fc) -> f32x4 { return ring[(slot * CF + fc) * 64 + lane]; };
 
   // ---------------------------------------------------------------- parameters
   auto row_tab_load = [&](int k, int buf) {  // per-row params of layer k -> tab[buf]
@@ -117,42 +139,27 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   };
   // uniform per-layer scalars (s_load).  k = -1 (prologue) reads layer 0; b1n = beta1 of the
   // layer whose Var the G2 epilogue of layer k produces (k+1, clamped).
-  struct LayerP { float b1, b2, b3, ss2, ss2b, the, thz, s1, b1n; };
+  struct LayerP { float b1n, b2, b3, ss2, ss2b; ShrinkP the, thz; };
   auto layer_params = [&](int k) -> LayerP {
     LayerP p{};
     if constexpr (PKIND != PK_ROW) {
       const int kk = k < 0 ? 0 : k;
       const int kn = k < 0 ? 0 : (k + 1 < K ? k + 1 : k);
       cfloat_p sp = (cfloat_p)a.scal + kk * DLADMM_NSCALAR;
-      p.b1 = sp[DLADMM_P_BETA1];
       p.b2 = sp[DLADMM_P_BETA2];
       p.b3 = sp[DLADMM_P_BETA3];
       p.ss2 = sp[DLADMM_P_SS2];
       p.ss2b = sp[DLADMM_P_SS2B];
-      p.the = sp[DLADMM_P_THETA_E];
-      p.thz = sp[DLADMM_P_THETA_Z];
-      p.s1 = sp[DLADMM_P_S1];
+      p.the = shrink_params(sp[DLADMM_P_THETA_E]);
+      p.thz = shrink_params(sp[DLADMM_P_THETA_Z]);
       p.b1n = ((cfloat_p)a.scal)[kn * DLADMM_NSCALAR + DLADMM_P_BETA1];
     }
     return p;
   };
-  // value of param `slot` for (layer k, block b, reg r)
-  auto prm = [&](const LayerP& P, int k, int slot, int b, int r) -> float {
-    if constexpr (PKIND == PK_ROW) {
-      const int off = (slot == DLADMM_P_THETA_Z) ? 6 * MP : slot * MP;
-      return tab[(k % 3) * TAB + off + 16 * b + 4 * g + r];
-    } else {
-      switch (slot) {
-        case DLADMM_P_BETA1: return P.b1;
-        case DLADMM_P_BETA2: return P.b2;
-        case DLADMM_P_BETA3: return P.b3;
-        case DLADMM_P_SS2: return P.ss2;
-        case DLADMM_P_SS2B: return P.ss2b;
-        case DLADMM_P_THETA_E: return P.the;
-        case DLADMM_P_THETA_Z: return P.thz;
-        default: return P.s1;
-      }
-    }
+  // value of param `slot` for (layer k, block b, reg r) of the per-row table
+  auto rowp = [&](int k, int slot, int b, int r) -> float {
+    const int off = (slot == DLADMM_P_THETA_Z) ? 6 * MP : slot * MP;
+    return tab[(k % 3) * TAB + off + 16 * b + 4 * g + r];
   };
 
   // ---------------------------------------------------------------- initial state
@@ -176,7 +183,7 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         xv[r] = bload(rx, ox + (uint32_t)((16 * b + r) * a.ldx * 4));
-        Er[b][r] = bload(re, oe + (uint32_t)((16 * b + r) * a.lde0 * 4));
+        if constexpr (kEState) Er[b][r] = bload(re, oe + (uint32_t)((16 * b + r) * a.lde0 * 4));
         Lr[b][r] = bload(rl, ol + (uint32_t)((16 * b + r) * a.ldl0 * 4));
         Vr[b][r] = 0.0f;
         pin_agpr(Vr[b][r]);
@@ -185,74 +192,92 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     }
   }
   row_tab_load(0, 0);
-  issue(a.Ap, 0);
 
-  const uint32_t oo = lane_off(a.ldo);                    // output lane offset
-  const uint32_t ob = lane_off(a.ldb);                    // per-element beta lane offset
+  const uint32_t vo = lane_off(a.ldo);  // output lane offset (voffset of every store)
+  const uint32_t vb = lane_off(a.ldb);  // per-element beta lane offset
   const uint32_t zbytes = (uint32_t)(n * a.ldo * 4), mbytes = (uint32_t)(m * a.ldo * 4);
-  Walk zw{oo, (uint32_t)(a.ldo * 4)}, mw{oo, (uint32_t)(a.ldo * 4)};
-  Walk bw{ob, (uint32_t)(a.ldb * 4)};
+  SWalk zw{0u, (uint32_t)(a.ldo * 4)}, mw{0u, (uint32_t)(a.ldo * 4)};
+  SWalk bw{0u, (uint32_t)(a.ldb * 4)};
 
   // ---------------------------------------------------------------- per-row epilogues
-  // Each block's epilogue is cut into its 4 accumulator rows; the rows of block b-1 are spread
-  // over the MFMA steps of block b (row r before the MFMAs of step (r * steps) / 4), so the
-  // VALU work and HBM stores issue in the MFMA shadow instead of stalling the matrix pipe.
-  //
   // G1 block b, row r of layer k: Z = S(Z - s1*(W_k Var), theta_z)  main_lena.py:86 / tied :114
-  auto epi1_row = [&](const LayerP& P, rsrc_t rzo, int k, int b, int r, f32x4 c0, f32x4 c1) {
-    float u = c0[r] + c1[r];
-    if constexpr (PKIND == PK_SCALAR) u = P.s1 * u;  // V5 ss1[k]; exactly 1.0 otherwise
-    const float z = shrink(Zr[b][r] - u, prm(P, k, DLADMM_P_THETA_Z, b, r));
+  // (q = -s1 W_k Var: the chain ran on the negated packed weights)
+  auto epi1_row = [&](const LayerP& P, rsrc_t rzo, int k, int b, int r, const f32x4& q) {
+#if DLADMM_ABLATE & 2  // timing experiment: no epilogue work (WRONG results)
+    Zr[b][r] = q[r]; pin_agpr(Zr[b][r]); return;
+#endif
+    const float u = Zr[b][r] + q[r];
+    float z;
+    if constexpr (PKIND == PK_ROW) {
+      z = shrink(u, rowp(k, DLADMM_P_THETA_Z, b, r));
+    } else {
+      z = shrink_u(u, P.thz);
+    }
     Zr[b][r] = z;
     pin_agpr(Zr[b][r]);
-    bstore(rzo, zw.at(r), z);
+    bstore_s(rzo, vo, zw.at(r), z);
     // no column mask: padded columns hold exactly zero state (X = Z0 = E0 = L0 = 0)
     regsum += fabsf(z);
     if (r == 3) zw.next();
   };
-  // G2 block b, row r of layer k.  Branch-free over k: for the prologue (k = -1) the E/L updates
-  // are discarded and T0 = A Z0 + E0 - X (main_lena.py:70) falls out of the same expression;
-  // its E/L stores go to 0-record buffers.
+  // G2 block b, row r of layer k (q = A Z_k, xv = X rows).  For the prologue (pro: k = -1) E and
+  // L stay E0, L0 and T0 = A Z0 + E0 - X (main_lena.py:70) falls out of the same expression;
+  // its E/L stores go to 0-record buffers.  pro is a compile-time constant except in the rows
+  // of the prologue's last pair, which run inside G1(0).  h = block half of the pair (PK_ELEM).
+  // The reference's operation order is kept throughout.
   struct OutR { rsrc_t e, l, t; };
-  auto epi2_row = [&](const LayerP& P, const OutR& O, int k, int b, int r, f32x4 c0, f32x4 c1,
-                      const f32x4& xv) {
-    const bool pro = k < 0;
-    const int kp = pro ? 0 : k;
-    float(&pe)[3][4] = pb[b & 1];
-    const float Pv = c0[r] + c1[r];
-    const float x = xv[r];
-    const uint32_t off = mw.at(r);
+  auto epi2_row = [&](const LayerP& P, const OutR& O, int k, bool pro, int b, int h, int r,
+                      const f32x4& q, const f32x4& xv) {
+#if DLADMM_ABLATE & 2
+    Vr[b][r] = q[r]; pin_agpr(Vr[b][r]); return;
+#endif
+    const int kp = k < 0 ? 0 : k;
+    const float Pv = q[r], x = xv[r];
     const float l0 = Lr[b][r];
+    const float e0 = kEState ? Er[b][r] : pb[h][1][r];  // V1: E0 in b2's slot (pro rows only)
+    float b2 = P.b2, b3 = P.b3, b1n = P.b1n;
+    if constexpr (PKIND == PK_ELEM) {
+      b3 = pb[h][0][r];
+      b2 = pb[h][1][r];
+      b1n = pb[h][2][r];
+    } else if constexpr (PKIND == PK_ROW) {
+      b2 = rowp(kp, DLADMM_P_BETA2, b, r);
+      b3 = rowp(kp, DLADMM_P_BETA3, b, r);
+      b1n = rowp(k + 1, DLADMM_P_BETA1, b, r);
+    }
     float e;
     if constexpr (EMODE == EM_V1) {
       // E = S(X - A Z - b2*L, theta_e)                      main_lena.py:87
-      const float b2 = (PKIND == PK_ELEM) ? pe[1][r] : prm(P, kp, DLADMM_P_BETA2, b, r);
-      e = shrink((x - Pv) - b2 * l0, prm(P, kp, DLADMM_P_THETA_E, b, r));
+      const float u = (x - Pv) - b2 * l0;
+      if constexpr (PKIND == PK_ROW) e = shrink(u, rowp(kp, DLADMM_P_THETA_E, b, r));
+      else e = shrink_u(u, P.the);
     } else if constexpr (EMODE == EM_VVAR) {
       // VVar = L + b2*(A Z + E - X); E = S(E - ss2*VVar)    main_syn_l1l1_scalar.py:114-115
-      const float vv = l0 + prm(P, kp, DLADMM_P_BETA2, b, r) * ((Pv + Er[b][r]) - x);
-      e = shrink(Er[b][r] - prm(P, kp, DLADMM_P_SS2, b, r) * vv,
-                 prm(P, kp, DLADMM_P_THETA_E, b, r));
+      if constexpr (PKIND == PK_ROW) {
+        const float vv = l0 + b2 * ((Pv + e0) - x);
+        e = shrink(e0 - rowp(kp, DLADMM_P_SS2, b, r) * vv, rowp(kp, DLADMM_P_THETA_E, b, r));
+      } else {
+        const float vv = l0 + b2 * ((Pv + e0) - x);
+        e = shrink_u(e0 - P.ss2 * vv, P.the);
+      }
     } else {
       // E = ss2_1*(X - A Z) - ss2_2*L                       main_syn_lasso_scalar.py:102-103
-      e = prm(P, kp, DLADMM_P_SS2, b, r) * (x - Pv) - prm(P, kp, DLADMM_P_SS2B, b, r) * l0;
+      e = P.ss2 * (x - Pv) - P.ss2b * l0;
     }
-    e = pro ? Er[b][r] : e;
+    e = pro ? e0 : e;
     const float t = (Pv + e) - x;                            // main_lena.py:70 / :88
-    const float b3 = (PKIND == PK_ELEM) ? pe[0][r] : prm(P, kp, DLADMM_P_BETA3, b, r);
-    const float l = pro ? l0 : l0 + b3 * t;                  // main_lena.py:89 / scalar :118
-    Er[b][r] = e;
+    float l = l0 + b3 * t;                                   // main_lena.py:89 / scalar :118
+    l = pro ? l0 : l;
+    if constexpr (kEState) Er[b][r] = e;
     Lr[b][r] = l;
-    bstore(O.e, off, e);
-    bstore(O.l, off, l);
-    bstore(O.t, off, t);
+    const uint32_t so = mw.at(r);
+    bstore_s(O.e, vo, so, e);
+    bstore_s(O.l, vo, so, l);
+    bstore_s(O.t, vo, so, t);
     const float res = x - Pv;
-    fitsum += fabsf(res) * (lasso ? fabsf(res) : 1.0f);  // |r| or r^2; branch-free
+    fit1 += fabsf(res);                                      // |X - A Z|
+    fit2 = __builtin_fmaf(res, res, fit2);                   // (X - A Z)^2
     // Var of the next layer: L + b1*T  (main_lena.py:85); unused after the last layer
-    float b1n;
-    if constexpr (PKIND == PK_ELEM) b1n = pe[2][r];
-    else if constexpr (PKIND == PK_ROW) b1n = prm(P, k + 1, DLADMM_P_BETA1, b, r);
-    else b1n = P.b1n;
     Vr[b][r] = l + b1n * t;
     pin_agpr(Vr[b][r]);
     if (r == 3) mw.next();
@@ -260,163 +285,223 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   // per-wave partial objective of layer k (k < 0: just reset the prologue's sums)
   auto flush_loss = [&](int k) {
     if (lossz && k >= 0) {
-      const float rs = wave_sum(regsum), fs = wave_sum(fitsum);
+      const float rs = wave_sum(regsum);
+      const float fs = lasso ? 0.5f * wave_sum(fit2) : wave_sum(fit1);
       if (lane == 0) {
         const int gw = blockIdx.x * kWaves + w;
         a.lossp[(int64_t)(2 * k + 0) * a.nwaves + gw] = rs;
-        a.lossp[(int64_t)(2 * k + 1) * a.nwaves + gw] = lasso ? 0.5f * fs : fs;
+        a.lossp[(int64_t)(2 * k + 1) * a.nwaves + gw] = fs;
       }
     }
     regsum = 0.f;
-    fitsum = 0.f;
+    fit1 = 0.f;
+    fit2 = 0.f;
   };
-  auto prefetch_elem = [&](int k, int b) {  // betas the G2 epilogue of (k, b) will need
+  // PK_ELEM: start the loads of the betas the G2 epilogue of (k, pair p) will need: b3, b2 and
+  // the next layer's b1.  The prologue (k = -1) loads E0 into b2's slot and b1 of layer 0.
+  const uint32_t ve = lane_off(a.lde0);
+  SWalk ew{0u, (uint32_t)(a.lde0 * 4)};
+  auto prefetch_elem = [&](int k, bool pro) {
     if constexpr (PKIND == PK_ELEM) {
-      float(&pe)[3][4] = pb[b & 1];
       const uint32_t eb = (uint32_t)(m * a.ldb * 4);
-      const rsrc_t r1 = mkrsrc(k >= 0 ? a.b1e[k] : nullptr, k >= 0 ? eb : 0u);
-      const rsrc_t r2 = mkrsrc(k >= 0 ? a.b2e[k] : nullptr, k >= 0 ? eb : 0u);
+      const rsrc_t r1 = mkrsrc(pro ? nullptr : a.b1e[k], pro ? 0u : eb);
+      const rsrc_t r2 = pro ? mkrsrc(a.E0, (uint32_t)(m * a.lde0 * 4)) : mkrsrc(a.b2e[k], eb);
       const rsrc_t rn = mkrsrc(k + 1 < K ? a.b1e[k + 1] : nullptr, k + 1 < K ? eb : 0u);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const uint32_t off = bw.at(r);
-        pe[0][r] = bload(r1, off);
-        pe[1][r] = bload(r2, off);
-        pe[2][r] = bload(rn, off);
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t so = bw.at(r);
+          pn[h][0][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r1, (int)vb, (int)so, 0));
+          pn[h][1][r] = pro ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r2, (int)ve, (int)ew.at(r), 0))
+                            : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r2, (int)vb, (int)so, 0));
+          pn[h][2][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rn, (int)vb, (int)so, 0));
+        }
+        bw.next();
+        if (pro) ew.next();
       }
-      bw.next();
+    }
+  };
+  auto take_elem = [&]() {  // the pair that just finished becomes the pending one
+    if constexpr (PKIND == PK_ELEM) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pb[h][i][r] = pn[h][i][r];
     }
   };
 
-  // ---------------------------------------------------------------- the K-layer loop
-  // Phase order: G2(-1) [P0 = A Z0], then per layer G1(k) [W_k Var], G2(k) [A Z_k].
-  // Every MFMA step: prefetch the fragment D steps ahead from the LDS ring, run the epilogue
-  // rows scheduled on this step, issue 4 MFMAs; a sched_barrier pins that order.
-  const int64_t wl = (int64_t)F::GF * kFrag;  // floats per packed W_k
-  f32x4 q0 = {0.f, 0.f, 0.f, 0.f}, q1 = {0.f, 0.f, 0.f, 0.f};  // pending block accumulators
-  f32x4 xpend = {0.f, 0.f, 0.f, 0.f};                           // X rows of the pending G2 block
-  f32x4 fr[NBUF];
-  for (int k = -1; k < K; ++k) {
+  // ---------------------------------------------------------------- one MFMA step
+  // Step s of GEMM gi (compile-time s, runtime gi): fragments 2s, 2s+1 of the GEMM's stream.
+  // Order inside a step: read ahead the next step's two fragments (at a chunk's last step:
+  // ring barrier, next chunk's first fragments, LDS-DMA of the chunk after it), then the
+  // epilogue rows scheduled here, then 8 MFMAs on two independent chains; a sched_barrier
+  // pins that order.  fr[] rotates over 4 registers (2 steps x 2 fragments).
+  f32x4 fr[4];
+  auto step_head = [&](auto S_, int gi) {
+    constexpr int s = decltype(S_)::value;
+    constexpr int fi = 2 * s, fc = fi % CF, ch = fi / CF;
+    if constexpr (fc + 2 < CF) {
+      fr[(fi + 2) % 4] = frag(cur, fc + 2);
+      fr[(fi + 3) % 4] = frag(cur, fc + 3);
+    } else {
+      ring_barrier();  // chunk ch+1 landed for every wave; every wave is done with chunk ch-1
+      issue(chunk_src(gi, ch + 2), slot_add(cur, 2));
+      const int nx = slot_add(cur, 1);
+      fr[(fi + 2) % 4] = frag(nx, 0);
+      fr[(fi + 3) % 4] = frag(nx, 1);
+    }
+  };
+  auto step_tail = [&](auto S_) {
+    constexpr int s = decltype(S_)::value;
+    constexpr int fc = (2 * s) % CF;
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (fc + 2 >= CF) cur = slot_add(cur, 1);
+  };
+
+  // prime the ring: chunks 0 and 1, then the first step's fragments
+  issue(chunk_src(0, 0), 0);
+  issue(chunk_src(0, 1), 1);
+  ring_barrier();
+  fr[0] = frag(0, 0);
+  fr[1] = frag(0, 1);
+
+  // ---------------------------------------------------------------- the GEMM passes
+  f32x4 qa = {0.f, 0.f, 0.f, 0.f}, qb = {0.f, 0.f, 0.f, 0.f};  // pending pair accumulators
+  f32x4 xa, xb;  // X rows of the pending G2 pair
+  auto load_x = [&](int p) {
+    xa = xs[(w * MB + 2 * p) * 64 + lane];
+    xb = xs[(w * MB + 2 * p + 1) * 64 + lane];
+  };
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+
+  // G1(k): -s1 W_k Var, chains of blocks (2p, 2p+1) over jb = 0..MB-1.  Pair 0 runs the
+  // rows of the last G2 pair of layer k-1 (Pp, Op; the prologue's when k = 0).
+  auto g1_pass = [&](int k, const LayerP& P, rsrc_t rzo, const LayerP& Pp, const OutR& Op) {
+    const int gi = 2 * k + 1;
+    zw.reset();
+    // layer k+1's row table -> buffer (k+1)%3.  Its previous content (layer k-2) was last
+    // read in G1(k-1)'s deferred epilogue, several ring barriers ago.
+    if (k + 1 < K) row_tab_load(k + 1, (k + 1) % 3);
+    static_for<NB / 2>([&](auto P_) {
+      constexpr int p = decltype(P_)::value;
+      f32x4 ca = zero4, cb = zero4;
+      if constexpr (p == 0) {
+        take_elem();
+        load_x(MB / 2 - 1);
+      }
+      static_for<MB>([&](auto J_) {
+        constexpr int jb = decltype(J_)::value;
+        constexpr int s = p * MB + jb;
+        step_head(std::integral_constant<int, s>{}, gi);
+        static_for<8>([&](auto I_) {
+          constexpr int i = decltype(I_)::value;
+          constexpr int h = i / 4, r = i % 4;
+          if constexpr (rows_at(jb, MB, i)) {
+            if constexpr (p == 0) {
+              epi2_row(Pp, Op, k - 1, k == 0, MB - 2 + h, h, r, h ? qb : qa, h ? xb : xa);
+              if constexpr (i == 7) flush_loss(k - 1);
+            } else {
+              epi1_row(P, rzo, k, 2 * p - 2 + h, r, h ? qb : qa);
+            }
+          }
+        });
+        const f32x4 wa = fr[(2 * s) % 4], wb = fr[(2 * s + 1) % 4];
+        ca = mfma4(wa.x, Vr[jb][0], ca);
+        cb = mfma4(wb.x, Vr[jb][0], cb);
+        ca = mfma4(wa.y, Vr[jb][1], ca);
+        cb = mfma4(wb.y, Vr[jb][1], cb);
+        ca = mfma4(wa.z, Vr[jb][2], ca);
+        cb = mfma4(wb.z, Vr[jb][2], cb);
+        ca = mfma4(wa.w, Vr[jb][3], ca);
+        cb = mfma4(wb.w, Vr[jb][3], cb);
+        step_tail(std::integral_constant<int, s>{});
+      });
+      qa = ca;
+      qb = cb;
+    });
+  };
+  // G2(k): A Z_k, chains of blocks (2p, 2p+1) over kb = 0..NB-1.  Pair 0 runs the rows of
+  // G1(k)'s last pair (none in the prologue); pair p > 0 runs those of pair p-1.
+  auto g2_pass = [&](auto PRO_, int k, const LayerP& P, const OutR& O, rsrc_t rzo) {
+    constexpr bool PRO = decltype(PRO_)::value;
+    const int gi = 2 * k + 2;
+    mw.reset();
+    bw.reset();
+    if constexpr (PRO) ew.reset();
+    static_for<MB / 2>([&](auto P_) {
+      constexpr int p = decltype(P_)::value;
+      f32x4 ca = zero4, cb = zero4;
+      if constexpr (p > 0) {
+        take_elem();
+        load_x(p - 1);
+      }
+      prefetch_elem(k, PRO);
+      static_for<NB>([&](auto K_) {
+        constexpr int kb = decltype(K_)::value;
+        constexpr int s = p * NB + kb;
+        step_head(std::integral_constant<int, s>{}, gi);
+        static_for<8>([&](auto I_) {
+          constexpr int i = decltype(I_)::value;
+          constexpr int h = i / 4, r = i % 4;
+          if constexpr (rows_at(kb, NB, i)) {
+            if constexpr (p == 0) {
+              if constexpr (!PRO) epi1_row(P, rzo, k, NB - 2 + h, r, h ? qb : qa);
+            } else {
+              epi2_row(P, O, k, PRO, 2 * p - 2 + h, h, r, h ? qb : qa, h ? xb : xa);
+            }
+          }
+        });
+        const f32x4 wa = fr[(2 * s) % 4], wb = fr[(2 * s + 1) % 4];
+        ca = mfma4(wa.x, Zr[kb][0], ca);
+        cb = mfma4(wb.x, Zr[kb][0], cb);
+        ca = mfma4(wa.y, Zr[kb][1], ca);
+        cb = mfma4(wb.y, Zr[kb][1], cb);
+        ca = mfma4(wa.z, Zr[kb][2], ca);
+        cb = mfma4(wb.z, Zr[kb][2], cb);
+        ca = mfma4(wa.w, Zr[kb][3], ca);
+        cb = mfma4(wb.w, Zr[kb][3], cb);
+        step_tail(std::integral_constant<int, s>{});
+      });
+      qa = ca;
+      qb = cb;
+    });
+  };
+
+  // ---------------------------------------------------------------- prologue + K layers
+  // G2(-1) [A Z0 - X -> T0, Var_0], then per layer G1(k) [Z_k], G2(k) [E_k, L_k, T_k+1, Var_k+1]
+  const rsrc_t none = mkrsrc(nullptr, 0u);
+  LayerP Pp = layer_params(-1);
+  OutR Op{none, none,
+          mkrsrc(a.keep_all ? a.To : nullptr, (a.keep_all && a.To) ? mbytes : 0u)};
+  g2_pass(std::true_type{}, -1, Pp, Op, none);
+  for (int k = 0; k < K; ++k) {
     const bool st = a.keep_all || k == K - 1;
     const int ko = a.keep_all ? k : 0;
     const LayerP P = layer_params(k);
-    const LayerP Pp = layer_params(k - 1);
-    // outputs of layer k (Z, E, L) and T[k+1]; num_records 0 = not stored
-    const rsrc_t rzo = mkrsrc(a.Zo + (int64_t)ko * n * a.ldo, st && k >= 0 ? zbytes : 0u);
-    const OutR O{mkrsrc(a.Eo + (int64_t)ko * m * a.ldo, st && k >= 0 ? mbytes : 0u),
-                 mkrsrc(a.Lo + (int64_t)ko * m * a.ldo, st && k >= 0 ? mbytes : 0u),
+    // outputs of layer k; num_records 0 = not stored
+    const rsrc_t rzo = mkrsrc(a.Zo + (int64_t)ko * n * a.ldo, st ? zbytes : 0u);
+    g1_pass(k, P, rzo, Pp, Op);
+    const OutR O{mkrsrc(a.Eo + (int64_t)ko * m * a.ldo, st ? mbytes : 0u),
+                 mkrsrc(a.Lo + (int64_t)ko * m * a.ldo, st ? mbytes : 0u),
                  mkrsrc(a.To ? a.To + (int64_t)(a.keep_all ? k + 1 : 0) * m * a.ldo : nullptr,
                         (a.To && st) ? mbytes : 0u)};
-    // outputs of layer k-1 (its last G2 block's epilogue runs inside this layer's G1)
-    const bool stp = a.keep_all || k - 1 == K - 1;
-    const int kop = a.keep_all ? k - 1 : 0;
-    const OutR Op{mkrsrc(a.Eo + (int64_t)kop * m * a.ldo, stp && k - 1 >= 0 ? mbytes : 0u),
-                  mkrsrc(a.Lo + (int64_t)kop * m * a.ldo, stp && k - 1 >= 0 ? mbytes : 0u),
-                  mkrsrc(a.To ? a.To + (int64_t)(a.keep_all ? k : 0) * m * a.ldo : nullptr,
-                         (a.To && stp) ? mbytes : 0u)};
-    const float* wk = a.Wp + (int64_t)(k < 0 ? 0 : k) * wl;
-
-    // ---- G1(k): U[b] = sum_jb Wp_k[b][jb] * Var[jb]
-    if (k >= 0) {
-      zw.cur = oo;
-      // layer k+1's row table -> buffer (k+1)%3.  Its previous content (layer k-2) was last
-      // read in G1(k-1)'s deferred epilogue, several ring barriers ago; its readers (G2(k)
-      // epilogues, layer k+1) all come after G1(k)'s first barrier.
-      if (k + 1 < K) row_tab_load(k + 1, (k + 1) % 3);
-      static_for<NB>([&](auto B_) {
-        constexpr int b = decltype(B_)::value;
-        f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-        static_for<MB>([&](auto J_) {
-          constexpr int jb = decltype(J_)::value;
-          constexpr int fi = b * MB + jb, fc = fi % CF;
-          if constexpr (fc == 0) {
-            constexpr int ch = fi / CF;
-            acquire(ch + 1 < NCH ? wk + (int64_t)(ch + 1) * CF * kFrag : a.Ap);
-            static_for<D>([&](auto Dd) {
-              constexpr int d = decltype(Dd)::value;
-              if constexpr (fc + d < CF) fr[(fi + d) % NBUF] = frag(fc + d);
-            });
-          }
-          if constexpr (fc + D < CF) fr[(fi + D) % NBUF] = frag(fc + D);
-          static_for<4>([&](auto R_) {
-            constexpr int r = decltype(R_)::value;
-            if constexpr ((r * MB) / 4 == jb) {
-              if constexpr (b == 0) {  // last G2 block of the previous phase
-                if constexpr (r == 0) xpend = xs[(w * MB + MB - 1) * 64 + lane];
-                epi2_row(Pp, Op, k - 1, MB - 1, r, q0, q1, xpend);
-                if constexpr (r == 3) flush_loss(k - 1);
-              } else {
-                epi1_row(P, rzo, k, b - 1, r, q0, q1);
-              }
-            }
-          });
-          const f32x4 wv = fr[fi % NBUF];
-          c0 = mfma4(wv.x, Vr[jb][0], c0);
-          c1 = mfma4(wv.y, Vr[jb][1], c1);
-          c0 = mfma4(wv.z, Vr[jb][2], c0);
-          c1 = mfma4(wv.w, Vr[jb][3], c1);
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr (fc == CF - 1) cur ^= 1;
-        });
-        q0 = c0;
-        q1 = c1;
-      });
-    }
-    // ---- G2(k): P[b] = sum_kb Ap[b][kb] * Z[kb]
-    const float* next_base = (k + 1 < K) ? a.Wp + (int64_t)(k + 1) * wl : a.Ap;
-    mw.cur = oo;
-    bw.cur = ob;
-    static_for<MB>([&](auto B_) {
-      constexpr int b = decltype(B_)::value;
-      f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-      static_for<NB>([&](auto K_) {
-        constexpr int kb = decltype(K_)::value;
-        constexpr int fi = b * NB + kb, fc = fi % CF;
-        if constexpr (fc == 0) {
-          constexpr int ch = fi / CF;
-          acquire(ch + 1 < NCH ? a.Ap + (int64_t)(ch + 1) * CF * kFrag : next_base);
-          static_for<D>([&](auto Dd) {
-            constexpr int d = decltype(Dd)::value;
-            if constexpr (fc + d < CF) fr[(fi + d) % NBUF] = frag(fc + d);
-          });
-        }
-        if constexpr (fc + D < CF) fr[(fi + D) % NBUF] = frag(fc + D);
-        if constexpr (kb == 0) prefetch_elem(k, b);
-        static_for<4>([&](auto R_) {
-          constexpr int r = decltype(R_)::value;
-          if constexpr ((r * NB) / 4 == kb) {
-            if constexpr (b == 0) {  // last G1 block of this layer
-              if (k >= 0) epi1_row(P, rzo, k, NB - 1, r, q0, q1);
-            } else {
-              if constexpr (r == 0) xpend = xs[(w * MB + b - 1) * 64 + lane];
-              epi2_row(P, O, k, b - 1, r, q0, q1, xpend);
-            }
-          }
-        });
-        const f32x4 wv = fr[fi % NBUF];
-        c0 = mfma4(wv.x, Zr[kb][0], c0);
-        c1 = mfma4(wv.y, Zr[kb][1], c1);
-        c0 = mfma4(wv.z, Zr[kb][2], c0);
-        c1 = mfma4(wv.w, Zr[kb][3], c1);
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (fc == CF - 1) cur ^= 1;
-      });
-      q0 = c0;
-      q1 = c1;
-    });
+    g2_pass(std::false_type{}, k, P, O, rzo);
+    Pp = P;
+    Op = O;
   }
-  {
-    const LayerP P = layer_params(K - 1);
-    const int ko = a.keep_all ? K - 1 : 0;
-    const OutR O{mkrsrc(a.Eo + (int64_t)ko * m * a.ldo, mbytes),
-                 mkrsrc(a.Lo + (int64_t)ko * m * a.ldo, mbytes),
-                 mkrsrc(a.To ? a.To + (int64_t)(a.keep_all ? K : 0) * m * a.ldo : nullptr,
-                        a.To ? mbytes : 0u)};
-    xpend = xs[(w * MB + MB - 1) * 64 + lane];
+  // epilogue of the last G2 pair of layer K-1
+  take_elem();
+  load_x(MB / 2 - 1);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) epi2_row(P, O, K - 1, MB - 1, r, q0, q1, xpend);
-    flush_loss(K - 1);
-  }
+  for (int i = 0; i < 8; ++i)
+    epi2_row(Pp, Op, K - 1, false, MB - 2 + i / 4, i / 4, i % 4, i < 4 ? qa : qb,
+             i < 4 ? xa : xb);
+  flush_loss(K - 1);
+  // drain: the ring's last LDS-DMA must land before the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 
@@ -442,9 +527,9 @@ hipError_t dispatch_variant(int variant, const FusedArgs& a, int grid, hipStream
 hipError_t launch_fused_shape(int shape, int variant, const FusedArgs& a, int grid,
                               hipStream_t s) {
   switch (shape) {
-    case 0: return dispatch_variant<16, 32>(variant, a, grid, s);
-    case 1: return dispatch_variant<64, 256>(variant, a, grid, s);
-    case 2: return dispatch_variant<256, 512>(variant, a, grid, s);
+    case 0: return dispatch_variant<kShapeMP[0], kShapeNP[0]>(variant, a, grid, s);
+    case 1: return dispatch_variant<kShapeMP[1], kShapeNP[1]>(variant, a, grid, s);
+    case 2: return dispatch_variant<kShapeMP[2], kShapeNP[2]>(variant, a, grid, s);
   }
   return hipErrorInvalidValue;
 }

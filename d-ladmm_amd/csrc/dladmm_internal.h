@@ -16,8 +16,8 @@ struct FusedArgs {
   const float* Z0; int64_t ldz0;
   const float* E0; int64_t lde0;
   const float* L0; int64_t ldl0;
-  const float* Ap;   // packed A   [MB][NB] fragments
-  const float* Wp;   // packed W_k [K][NB][MB] fragments
+  const float* Ap;   // packed A          [MB/2][NB][2] fragments (pair order)
+  const float* Wp;   // packed -s1_k W_k  [K][NB/2][MB][2] fragments
   const float* scal; // [K][8]
   const float* rowp; int64_t rstride;  // [K][8][rstride]
   int64_t ldb;
@@ -30,7 +30,7 @@ struct FusedArgs {
 
 // Register-resident instantiations of the fused kernel, by index: (MP, NP).
 constexpr int kNumShapes = 3;
-constexpr int kShapeMP[kNumShapes] = {16, 64, 256};
+constexpr int kShapeMP[kNumShapes] = {32, 64, 256};
 constexpr int kShapeNP[kNumShapes] = {32, 256, 512};
 
 hipError_t launch_fused_shape(int shape, int variant, const FusedArgs& a, int grid,

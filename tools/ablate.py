@@ -1,0 +1,39 @@
+"""Build timing-experiment variants of the fused kernel (never shipped; results are WRONG by design).
+
+    python tools/ablate.py name=-DFLAG=1[,-DOTHER=2] ...
+
+Each variant recompiles dladmm_fused.hip with the extra flags and links it with the regular
+capi/layered objects into d-ladmm_amd/lib/abl/<name>/libdladmm_hip.so.  Time one with
+    DLADMM_LIB=d-ladmm_amd/lib/abl/<name>/libdladmm_hip.so python bench.py --no-cpu-baseline
+Knobs: DLADMM_ABLATE (1 = no weight stream, 2 = no epilogue), DLADMM_SYNC_MODE, DLADMM_CHUNK.
+"""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "d-ladmm_amd"))
+import build as B  # noqa: E402
+
+
+def one(spec):
+    name, _, flags = spec.partition("=")
+    flags = [f for f in flags.split(",") if f]
+    out = os.path.join(B.HERE, "lib", "abl", name)
+    os.makedirs(out, exist_ok=True)
+    obj = os.path.join(out, "fused.o")
+    cc = B.hipcc()
+    subprocess.run([cc] + B.FLAGS + flags + ["-c", os.path.join(B.CSRC, "dladmm_fused.hip"), "-o", obj],
+                   check=True)
+    others = [os.path.join(B.OBJ, u.replace(".hip", ".o")) for u in B.UNITS if u != "dladmm_fused.hip"]
+    subprocess.run([cc, "-shared", "-fPIC", f"--offload-arch={B.ARCH}", "-o",
+                    os.path.join(out, "libdladmm_hip.so"), obj] + others, check=True)
+    return name
+
+
+if __name__ == "__main__":
+    B.build()
+    with ThreadPoolExecutor(max_workers=4) as ex:
+        for n in ex.map(one, sys.argv[1:]):
+            print("built", n)
