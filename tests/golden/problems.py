@@ -167,3 +167,57 @@ def build_problem(defn: dict):
                          perturb=d.get("perturb", 0.0), wscale=d.get("wscale"),
                          negtheta=d.get("negtheta", False))
     return inp, sd
+
+
+# ---------------------------------------------------------------- backward
+# Fixtures for the gradient oracle: name -> forward fixture it reuses + the loss it differentiates.
+# The loss is the reference training loss (L1L1 main_syn_l1l1_scalar.py:283-298, LASSO
+# main_syn_lasso_scalar.py:270-285, decay 0.6**epoch at epoch 1 for k < K-1) PLUS seeded random
+# linear terms sum_k <Gz_k,Z_k> + <Ge_k,E_k> + <Gl_k,L_k> (+ sum_j <Gt_j,T_j> for the variants
+# that return T), so every adjoint path of the forward (Z, E, L and T outputs) is exercised --
+# main_lena.py:219-227's dual-gap loss reads E and L as well.
+GRAD_FIXTURES = {
+    "grad_v1_small": dict(base="v1_small_pert", loss="l1l1"),
+    "grad_v2_small": dict(base="v2_small_pert", loss="l1l1"),
+    "grad_v3_small": dict(base="v3_small_pert", loss="l1l1"),
+    "grad_v4_small": dict(base="v4_small_pert", loss="l1l1"),
+    "grad_v4_negtheta": dict(base="v4_small_negtheta", loss="l1l1"),
+    "grad_v5_small": dict(base="v5_small_pert", loss="l1l1"),
+    "grad_v6_small": dict(base="v6_small_pert", loss="lasso"),
+    "grad_v4_ragged": dict(base="v4_ragged", loss="l1l1"),
+    "grad_v2_ragged": dict(base="v2_ragged", loss="l1l1"),
+    # BASELINE config-2 shape (m=256, n=512) at depth 5 (keeps each fixture ~2.5 MB)
+    "grad_v4_med": dict(base="v4_med_pert", loss="l1l1", K=5),
+    "grad_v6_med": dict(base="v6_med", loss="lasso", K=5),
+    "grad_v1_med": dict(base="v1_med_w04", loss="l1l1", K=5),
+    "grad_v3_med": dict(base="v3_med_pert", loss="l1l1", K=5),
+}
+GRAD_ALPHA = 0.001
+GRAD_EPOCH = 1
+GRAD_SCALE = 1e-2  # magnitude of the random linear terms
+
+
+def grad_defn(gdef: dict) -> dict:
+    """Problem definition of a gradient fixture: its base forward fixture, optionally at a
+    smaller depth K (the parameters are then regenerated for that depth)."""
+    d = dict(FIXTURES[gdef["base"]])
+    if "K" in gdef:
+        d["K"] = gdef["K"]
+    return d
+
+
+def loss_coeffs(K: int):
+    """decay = 0.6**epoch if k < layers-1 else 1.0  (main_syn_l1l1_scalar.py:296)."""
+    return [0.6 ** GRAD_EPOCH if k < K - 1 else 1.0 for k in range(K)]
+
+
+def make_upstream(defn: dict, returns_t: bool):
+    """Seeded random cotangents of the forward outputs (fp32): Gz [K,n,B], Ge/Gl [K,m,B] and,
+    if the variant returns T, Gt [K+1,m,B]."""
+    m, n, B, K = defn["m"], defn["n"], defn["B"], defn["K"]
+    rng = np.random.default_rng(defn["seed"] + 104729)
+    g = lambda *s: (GRAD_SCALE * rng.standard_normal(s)).astype(np.float32)  # noqa: E731
+    out = dict(Gz=g(K, n, B), Ge=g(K, m, B), Gl=g(K, m, B))
+    if returns_t:
+        out["Gt"] = g(K + 1, m, B)
+    return out
