@@ -25,7 +25,8 @@ P_BETA1, P_BETA2, P_BETA3, P_SS2, P_SS2B, P_THETA_E, P_THETA_Z, P_S1 = range(8)
 
 # every symbol include/dladmm.h declares (checked by tests/test_capi.py)
 EXPORTED = ("dladmm_abi_version", "dladmm_fwd_workspace_bytes", "dladmm_fwd_path",
-            "dladmm_fwd_f32", "dladmm_error_string")
+            "dladmm_fwd_f32", "dladmm_bwd_workspace_bytes", "dladmm_bwd_f32",
+            "dladmm_error_string")
 
 _fp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -56,6 +57,18 @@ class FwdDesc(ctypes.Structure):
     ]
 
 
+class BwdDesc(ctypes.Structure):
+    """Mirror of `struct dladmm_bwd_desc` (include/dladmm.h)."""
+    _fields_ = [
+        ("fwd", FwdDesc),
+        ("gZ", _fp), ("gE", _fp), ("gL", _fp), ("gT", _fp), ("ld_g", _i64),
+        ("gW", _fp), ("ld_gw", _i64),
+        ("g_scalar", _fp), ("g_row", _fp),
+        ("g_beta1_elem", ctypes.POINTER(_fp)), ("g_beta2_elem", ctypes.POINTER(_fp)),
+        ("workspace", _fp), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
 _LIB = None
 
 
@@ -78,6 +91,10 @@ def lib():
     L.dladmm_fwd_path.argtypes = [ctypes.POINTER(FwdDesc)]
     L.dladmm_fwd_f32.restype = ctypes.c_int
     L.dladmm_fwd_f32.argtypes = [ctypes.POINTER(FwdDesc), ctypes.c_void_p]
+    L.dladmm_bwd_workspace_bytes.restype = ctypes.c_size_t
+    L.dladmm_bwd_workspace_bytes.argtypes = [ctypes.POINTER(BwdDesc)]
+    L.dladmm_bwd_f32.restype = ctypes.c_int
+    L.dladmm_bwd_f32.argtypes = [ctypes.POINTER(BwdDesc), ctypes.c_void_p]
     L.dladmm_error_string.restype = ctypes.c_char_p
     L.dladmm_error_string.argtypes = [ctypes.c_int]
     if L.dladmm_abi_version() != ABI_VERSION:

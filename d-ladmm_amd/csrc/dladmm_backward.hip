@@ -1,0 +1,395 @@
+// dladmm_backward.hip -- MI355X (gfx950) backward of the K-layer D-LADMM forward (SURVEY.md
+// section 8 row f1): the vector-Jacobian product torch autograd computes when the reference
+// training loops call total_loss.backward() (main_lena.py:229, main_syn_l1l1_scalar.py:298,
+// main_syn_lasso_scalar.py:285) through DLADMMNet.forward.
+//
+// One reverse sweep over the layers, three GEMM kernels per layer whose epilogues carry the whole
+// elementwise adjoint algebra (derivation: oracle/dladmm_oracle_grad.py, which restates it in
+// numpy and is pinned against the reference's autograd gradients):
+//   BK1(k)  P = A Z_k                   (m rows, contraction n)  recompute E_k, T_{k+1};
+//           adjoints of L_k, T_{k+1}, E_k -> gP, adjoint of E_{k-1}, partial adjoint of L_{k-1},
+//           Var_k = L_{k-1} + b1 T_k (operand of BK2/wgrad); grads of b3, b2, ss2, ss2b, theta_e
+//   BK2(k)  R = A^T gP, q = M_k Var_k    (n rows, contraction m, two GEMMs)  recompute U_k;
+//           gU = (adj Z_k + R) * S'(U_k) = adjoint of Z_{k-1}; grads of theta_z, s1
+//   BK3(k)  gVar = M_k^T gU              (m rows, contraction n)  adjoint of L_{k-1} += gVar,
+//           adjoint of T_k = b1 gVar; grad of b1
+//   WG(k)   gM_k = gU Var_k^T            (n x m, contraction over the batch: split-K + fixed-order
+//           reduction, so it is deterministic); gW_k = -s1 gM_k
+// where M_k = -s1 W_k is the forward's packed weight.  P and q are recomputed with the exact
+// fragment packing / accumulation order of the forward kernel that produced the saved outputs,
+// so the shrink masks S'(.) are those of the forward, bit for bit.
+// Parameter gradients of broadcast parameters are reduced per wave (scalars: over the wave; per
+// row: over the wave's 16 columns) into partial buffers and summed in fp64 in a fixed order.
+#include "dladmm_common.h"
+#include "dladmm_internal.h"
+#include "dladmm_slice.h"
+
+namespace dladmm {
+
+// (dS/dx, dS/dth) of S(x, th) = relu(x - th) - relu(-1.0*x - th) (main_lena.py:52-53) under
+// torch's relu' = [v > 0]: dS/dx = [x-th > 0] + [-x-th > 0], dS/dth = [-x-th > 0] - [x-th > 0].
+struct SD { float dx, dth; };
+__device__ __forceinline__ SD shrink_d(float x, float th) {
+  const float a = (x - th) > 0.0f ? 1.0f : 0.0f;
+  const float b = (-x - th) > 0.0f ? 1.0f : 0.0f;
+  return SD{a + b, b - a};
+}
+
+// sum over the 16 lanes that share lane>>4 (the 16 batch columns of one row)
+__device__ __forceinline__ float col16_sum(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int EMODE, int PKIND, int PH, int NW, int SB>
+__global__ __launch_bounds__(NW * 64, 1) void bwd_kernel(const BwdArgs a) {
+  __shared__ f32x4 ring[2 * kSliceCF * 64];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  const int64_t col = (int64_t)blockIdx.x * (16 * NW) + w * 16 + (lane & 15);
+  const bool cv = col < a.B;
+  const int64_t colc = cv ? col : 0;
+  const int ib0 = blockIdx.y * SB;
+  const int k = a.k;
+
+  f32x4 acc[SB];
+  slice_gemm<NW, SB>(ring, a.Wp, a.MBp, ib0, a.KB, a.S, a.ldS, a.Krows, colc, cv, acc);
+  f32x4 acc2[PH == 2 ? SB : 1];
+  if constexpr (PH == 2)
+    slice_gemm<NW, SB>(ring, a.Wp2, a.MBp, ib0, a.KB, a.S2, a.ldS2, a.Krows, colc, cv, acc2);
+
+  cfloat_p sp = (cfloat_p)a.scal + k * DLADMM_NSCALAR;
+  const float* rp = a.rowp ? a.rowp + (int64_t)k * 8 * a.rstride : nullptr;
+  auto pm = [&](int slot, int rowc) -> float {  // scalar or per-row parameter of layer k
+    if constexpr (PKIND == PK_ROW) return rp[(int64_t)slot * a.rstride + rowc];
+    else return sp[slot];
+  };
+  auto up = [&](const float* gp, int rowc) -> float {  // upstream cotangent (NULL = 0)
+    return gp ? gp[(int64_t)rowc * a.ldg + colc] : 0.0f;
+  };
+  const int64_t ldw = a.ldw;  // row stride of the adjoint / operand workspaces
+
+  // per-slot partial sums: scalar kind over the whole wave, row kind per row (col16_sum)
+  float ps[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ps[i] = 0.0f;
+  const int cg = blockIdx.x * NW + w;  // column group (wave) index
+  auto row_flush = [&](int row, bool rok, const float (&v)[8], unsigned mask) {
+    if constexpr (PKIND == PK_ROW) {
+#pragma unroll
+      for (int sl = 0; sl < 8; ++sl) {
+        if (!(mask & (1u << sl))) continue;
+        const float s = col16_sum(v[sl]);
+        if ((lane & 15) == 0 && rok)
+          a.part[((int64_t)sl * a.rstride + row) * a.ncg + cg] = s;
+      }
+    }
+  };
+
+  static_for<SB>([&](auto I_) {
+    constexpr int i = decltype(I_)::value;
+    static_for<4>([&](auto R_) {
+      constexpr int r = decltype(R_)::value;
+      const int row = 16 * (ib0 + i) + 4 * g + r;
+      float pv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if constexpr (PH == 1) {
+        // ---------------- BK1: rows of m.  acc = P = A Z_k
+        const bool rok = row < a.m;
+        const bool ok = cv && rok;
+        const int rowc = rok ? row : 0;
+        const int64_t o = (int64_t)rowc * ldw + colc;
+        const float P = acc[i][r];
+        const float x = a.X[(int64_t)rowc * a.ldx + colc];
+        const float ep = a.Ep[(int64_t)rowc * a.ldep + colc];
+        const float lp = a.Lp[(int64_t)rowc * a.ldlp + colc];
+        const float tk = a.Tk[(int64_t)rowc * a.ldt + colc];
+        float b1, b2 = 0.f, b3;
+        if constexpr (PKIND == PK_ELEM) {
+          b1 = a.b1e[(int64_t)rowc * a.ldb + colc];
+          b2 = a.b2e[(int64_t)rowc * a.ldb + colc];
+          b3 = b1;  // main_lena.py:85,89: beta1 serves Var and L
+        } else {
+          b1 = pm(DLADMM_P_BETA1, rowc);
+          b3 = pm(DLADMM_P_BETA3, rowc);
+          if constexpr (EMODE != EM_LASSO) b2 = pm(DLADMM_P_BETA2, rowc);
+        }
+        // incoming adjoints of L_k, T_{k+1}, E_k
+        const float aL = a.AL[o] + up(a.gL, rowc);
+        const float aT = a.AT[o] + up(a.gT, rowc);
+        const float aE = a.AE[o] + up(a.gE, rowc);
+        // recompute the forward's E_k and T_{k+1} (same expressions as the forward kernels)
+        float e, gP, gEp = 0.f, gLp;
+        float t;
+        if constexpr (EMODE == EM_V1) {
+          const float u = (x - P) - b2 * lp;                                  // main_lena.py:87
+          const float the = pm(DLADMM_P_THETA_E, rowc);
+          e = shrink(u, the);
+          t = (P + e) - x;
+          const float gTn = aT + b3 * aL;
+          pv[DLADMM_P_BETA3] = aL * t;
+          const float gEt = aE + gTn;
+          const SD d = shrink_d(u, the);
+          const float gEh = gEt * d.dx;
+          pv[DLADMM_P_THETA_E] = gEt * d.dth;
+          gP = gTn - gEh;
+          pv[DLADMM_P_BETA2] = -gEh * lp;
+          gLp = aL - b2 * gEh;
+        } else if constexpr (EMODE == EM_VVAR) {
+          const float ss2 = pm(DLADMM_P_SS2, rowc), the = pm(DLADMM_P_THETA_E, rowc);
+          const float r0 = (P + ep) - x;
+          const float vv = lp + b2 * r0;                                      // scalar.py:114
+          const float eh = ep - ss2 * vv;                                     // scalar.py:115
+          e = shrink(eh, the);
+          t = (P + e) - x;
+          const float gTn = aT + b3 * aL;
+          pv[DLADMM_P_BETA3] = aL * t;
+          const float gEt = aE + gTn;
+          const SD d = shrink_d(eh, the);
+          const float gEh = gEt * d.dx;
+          pv[DLADMM_P_THETA_E] = gEt * d.dth;
+          const float gVV = -ss2 * gEh;
+          pv[DLADMM_P_SS2] = -gEh * vv;
+          gLp = aL + gVV;
+          pv[DLADMM_P_BETA2] = gVV * r0;
+          gP = gTn + b2 * gVV;
+          gEp = gEh + b2 * gVV;
+        } else {
+          const float ss2 = pm(DLADMM_P_SS2, rowc), ss2b = pm(DLADMM_P_SS2B, rowc);
+          e = ss2 * (x - P) - ss2b * lp;                                      // lasso.py:102-103
+          t = (P + e) - x;
+          const float gTn = aT + b3 * aL;
+          pv[DLADMM_P_BETA3] = aL * t;
+          const float gEt = aE + gTn;
+          pv[DLADMM_P_SS2] = gEt * (x - P);
+          gP = gTn - ss2 * gEt;
+          pv[DLADMM_P_SS2B] = -gEt * lp;
+          gLp = aL - ss2b * gEt;
+        }
+        (void)e;
+        if (ok) {
+          a.GP[o] = gP;
+          a.AE[o] = gEp;
+          a.AL[o] = gLp;
+          a.VAR[o] = lp + b1 * tk;  // Var_k = L_{k-1} + b1 T_k (main_lena.py:71,85)
+          if constexpr (PKIND == PK_ELEM) {
+            a.gb1e[(int64_t)row * a.ldb + col] = pv[DLADMM_P_BETA3];  // BK3 adds gVar*T_k
+            a.gb2e[(int64_t)row * a.ldb + col] = pv[DLADMM_P_BETA2];
+          }
+        }
+        if (!ok) {
+#pragma unroll
+          for (int sl = 0; sl < 8; ++sl) pv[sl] = 0.f;
+        }
+        row_flush(row, rok, pv, (1u << DLADMM_P_BETA3) | (1u << DLADMM_P_BETA2) |
+                                    (1u << DLADMM_P_THETA_E) | (1u << DLADMM_P_SS2) |
+                                    (1u << DLADMM_P_SS2B));
+      } else if constexpr (PH == 2) {
+        // ---------------- BK2: rows of n.  acc = R = A^T gP, acc2 = q = M_k Var_k
+        const bool rok = row < a.n;
+        const bool ok = cv && rok;
+        const int rowc = rok ? row : 0;
+        const int64_t o = (int64_t)rowc * ldw + colc;
+        const float R = acc[i][r];
+        const float q = acc2[i][r];
+        const float zp = a.Zp[(int64_t)rowc * a.ldzp + colc];
+        float s1 = 1.0f;
+        if constexpr (PKIND == PK_SCALAR) s1 = sp[DLADMM_P_S1];
+        // U exactly as the forward kernel that produced the saved outputs formed it
+        const float U = a.ufused ? zp + q : zp - ((PKIND == PK_SCALAR) ? s1 * q : q);
+        const float thz = pm(DLADMM_P_THETA_Z, rowc);
+        const float gZt = (a.AZ[o] + up(a.gZ, rowc)) + R;
+        const SD d = shrink_d(U, thz);
+        const float gU = gZt * d.dx;
+        pv[DLADMM_P_THETA_Z] = gZt * d.dth;
+        if constexpr (PKIND == PK_SCALAR) {
+          // dU/ds1 = -W Var:  fused packing q = -s1 W Var, per-layer packing q = W Var
+          const float wv = a.ufused ? (s1 != 0.0f ? -q / s1 : 0.0f) : q;
+          pv[DLADMM_P_S1] = -gU * wv;
+        }
+        if (ok) a.AZ[o] = gU;  // adjoint of Z_{k-1}; also BK3's operand and wgrad's gM rows
+        if (!ok) {
+#pragma unroll
+          for (int sl = 0; sl < 8; ++sl) pv[sl] = 0.f;
+        }
+        row_flush(row, rok, pv, 1u << DLADMM_P_THETA_Z);
+      } else {
+        // ---------------- BK3: rows of m.  acc = gVar = M_k^T gU
+        const bool rok = row < a.m;
+        const bool ok = cv && rok;
+        const int rowc = rok ? row : 0;
+        const int64_t o = (int64_t)rowc * ldw + colc;
+        const float gVar = acc[i][r];
+        const float tk = a.Tk[(int64_t)rowc * a.ldt + colc];
+        float b1;
+        if constexpr (PKIND == PK_ELEM) b1 = a.b1e[(int64_t)rowc * a.ldb + colc];
+        else b1 = pm(DLADMM_P_BETA1, rowc);
+        pv[DLADMM_P_BETA1] = gVar * tk;
+        if (ok) {
+          a.AL[o] = a.AL[o] + gVar;
+          a.AT[o] = b1 * gVar;  // adjoint of T_k (main_lena.py:85)
+          if constexpr (PKIND == PK_ELEM)
+            a.gb1e[(int64_t)row * a.ldb + col] = a.gb1e[(int64_t)row * a.ldb + col] + pv[DLADMM_P_BETA1];
+        }
+        if (!ok) pv[DLADMM_P_BETA1] = 0.f;
+        row_flush(row, rok, pv, 1u << DLADMM_P_BETA1);
+      }
+#pragma unroll
+      for (int sl = 0; sl < 8; ++sl) ps[sl] += pv[sl];
+    });
+  });
+  if constexpr (PKIND == PK_SCALAR) {
+    const int slot = blockIdx.y * gridDim.x * NW + cg;
+    auto flush = [&](int sl) {
+      const float s = wave_sum(ps[sl]);
+      if (lane == 0) a.part[(int64_t)sl * a.nslots + slot] = s;
+    };
+    if constexpr (PH == 1) {
+      flush(DLADMM_P_BETA3);
+      if constexpr (EMODE == EM_VVAR) { flush(DLADMM_P_BETA2); flush(DLADMM_P_SS2); flush(DLADMM_P_THETA_E); }
+      if constexpr (EMODE == EM_V1) { flush(DLADMM_P_BETA2); flush(DLADMM_P_THETA_E); }
+      if constexpr (EMODE == EM_LASSO) { flush(DLADMM_P_SS2); flush(DLADMM_P_SS2B); }
+    } else if constexpr (PH == 2) {
+      flush(DLADMM_P_THETA_Z);
+      flush(DLADMM_P_S1);
+    } else {
+      flush(DLADMM_P_BETA1);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------ weight gradient
+// part[c][i][j] = sum_{b in chunk c} G[i][b] * V[j][b]   (G: n x ld, V: m x ld; both zero-padded
+// to whole 16-row blocks and whole 16-column steps, so no masks).  One workgroup = 4 waves in a
+// 2 x 2 grid over a 128 x 128 output tile; a wave keeps 4 x 4 16x16 accumulators.  Per 16-column
+// step a lane loads, for each of its 4 row blocks of G and of V, the float4 at
+// (row 16a + (l & 15), columns 16s + 4(l >> 4) .. +3) and issues, per block pair, 4 MFMAs whose
+// k-index is the batch column 16s + 4(l >> 4) + q -- the same permutation for both operands, so
+// the contraction is exact.  Operands are software-pipelined one step ahead.
+__global__ __launch_bounds__(256, 1) void wgrad_kernel(const WgradArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int tiles_m = a.MBp16 / 8;  // 128-column tiles (of V rows)
+  const int tile = blockIdx.x;
+  const int ti = tile / tiles_m, tj = tile % tiles_m;
+  const int i0 = ti * 128 + (w >> 1) * 64;  // G rows of this wave
+  const int j0 = tj * 128 + (w & 1) * 64;   // V rows of this wave
+  const int64_t b0 = (int64_t)blockIdx.y * a.chunk;
+  int64_t b1 = b0 + a.chunk;
+  if (b1 > a.Bpad) b1 = a.Bpad;
+  const int steps = b1 > b0 ? (int)((b1 - b0) / 16) : 0;
+  const int r = lane & 15, g = lane >> 4;
+  const bool wok = i0 < a.NBp16 * 16 && j0 < a.MBp16 * 16;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const float* Gp = a.G + (int64_t)(i0 + r) * a.ld + b0 + 4 * g;
+  const float* Vp = a.V + (int64_t)(j0 + r) * a.ld + b0 + 4 * g;
+  const int64_t rs16 = 16 * a.ld;
+  auto ld4 = [&](const float* p) -> f32x4 { return *reinterpret_cast<const f32x4*>(p); };
+  f32x4 ga[4], va[4], gn[4], vn[4];
+  if (wok && steps > 0) {
+#pragma unroll
+    for (int x = 0; x < 4; ++x) { ga[x] = ld4(Gp + x * rs16); va[x] = ld4(Vp + x * rs16); }
+  }
+  for (int s = 0; wok && s < steps; ++s) {
+    if (s + 1 < steps) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        gn[x] = ld4(Gp + x * rs16 + 16 * (s + 1));
+        vn[x] = ld4(Vp + x * rs16 + 16 * (s + 1));
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = mfma4(ga[x][q], va[y][q], acc[x][y]);
+#pragma unroll
+    for (int x = 0; x < 4; ++x) { ga[x] = gn[x]; va[x] = vn[x]; }
+  }
+  if (!wok) return;
+  // C/D layout: lane holds column (l & 15) = V row j, rows 4g + r' = G rows
+  float* out = a.part + (int64_t)blockIdx.y * a.n * a.m;
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = i0 + 16 * x + 4 * g + q;
+        const int j = j0 + 16 * y + r;
+        if (i < a.n && j < a.m) out[(int64_t)i * a.m + j] = acc[x][y][q];
+      }
+}
+
+// gW[i][j] (+)= scale * sum_c part[c][i][j], c in fixed order; scale = -s1_k (or -1)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* part, int nchunks,
+                                                           int64_t nm, const float* scal, int k,
+                                                           int accumulate, float* gW,
+                                                           int64_t ldgw, int m) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= nm) return;
+  float s = 0.0f;
+  for (int c = 0; c < nchunks; ++c) s += part[(int64_t)c * nm + e];
+  const float scale = -(scal ? scal[k * DLADMM_NSCALAR + DLADMM_P_S1] : 1.0f);
+  const int64_t i = e / m, j = e % m;
+  float* dst = gW + i * ldgw + j;
+  *dst = accumulate ? *dst + scale * s : scale * s;
+}
+
+// ------------------------------------------------------------------------ dispatch
+template <int EM, int PK, int PH>
+hipError_t launch_bwd_v(const BwdArgs& a, dim3 grid, int sb, hipStream_t s) {
+  constexpr int NW = kBwdWaves;
+  // 16 output blocks per slice: with 32 the epilogue's operand loads spill (PH 1, scalar kind)
+  if (sb != 16) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((bwd_kernel<EM, PK, PH, NW, 16>), grid, dim3(NW * 64), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int PH>
+hipError_t launch_bwd_ph(int variant, const BwdArgs& a, dim3 grid, int sb, hipStream_t s) {
+  switch (variant) {
+    case DLADMM_V1_LENA: return launch_bwd_v<EM_V1, PK_ELEM, PH>(a, grid, sb, s);
+    case DLADMM_V2_LTHETA: return launch_bwd_v<EM_V1, PK_ROW, PH>(a, grid, sb, s);
+    case DLADMM_V3_FULL: return launch_bwd_v<EM_VVAR, PK_ROW, PH>(a, grid, sb, s);
+    case DLADMM_V4_SCALAR:
+    case DLADMM_V5_TIED: return launch_bwd_v<EM_VVAR, PK_SCALAR, PH>(a, grid, sb, s);
+    case DLADMM_V6_LASSO: return launch_bwd_v<EM_LASSO, PK_SCALAR, PH>(a, grid, sb, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_bwd(int phase, int variant, const BwdArgs& a, dim3 grid, int sb,
+                      hipStream_t s) {
+  switch (phase) {
+    case 1: return launch_bwd_ph<1>(variant, a, grid, sb, s);
+    case 2: return launch_bwd_ph<2>(variant, a, grid, sb, s);
+    case 3: return launch_bwd_ph<3>(variant, a, grid, sb, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_wgrad(const WgradArgs& a, int tiles, hipStream_t s) {
+  hipLaunchKernelGGL(wgrad_kernel, dim3(tiles, a.nchunks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_wgrad_reduce(const float* part, int nchunks, int n, int m, const float* scal,
+                               int k, int accumulate, float* gW, int64_t ldgw, hipStream_t s) {
+  const int64_t nm = (int64_t)n * m;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((nm + 255) / 256)), dim3(256), 0, s,
+                     part, nchunks, nm, scal, k, accumulate, gW, ldgw, m);
+  return hipGetLastError();
+}
+
+}  // namespace dladmm

@@ -18,6 +18,8 @@ struct PackArgs {
   float* dst;
   float sign;          // every element is multiplied by sign * (scal ? scal[t][S1] : 1)
   const float* scal;   // device [T][DLADMM_NSCALAR] (V4-V6 s1) or null
+  int trans;           // 1: pack the transpose (element (row, c) = src[c][row])
+  int t0;              // scal row of source t is t0 + t
 };
 
 // fragment (ib, jb) of source t: dst[..][lane][q] = src_t[16 ib + (lane & 15)][16 jb + 4 (lane >> 4) + q]
@@ -31,14 +33,16 @@ __global__ __launch_bounds__(256) void pack_frags_kernel(const PackArgs p) {
   if (p.order == 0) { ib = (int)(fr / p.CB); jb = (int)(fr % p.CB); }
   else if (p.order == 1) { ib = (int)(fr % p.RB); jb = (int)(fr / p.RB); }
   else { const int64_t q = fr >> 1; jb = (int)(q % p.CB); ib = 2 * (int)(q / p.CB) + (int)(fr & 1); }
-  const float f = p.sign * (p.scal ? p.scal[t * DLADMM_NSCALAR + DLADMM_P_S1] : 1.0f);
+  const float f = p.sign * (p.scal ? p.scal[(p.t0 + t) * DLADMM_NSCALAR + DLADMM_P_S1] : 1.0f);
   const int row = 16 * ib + (lane & 15);
   const int c0 = 16 * jb + 4 * (lane >> 4);
   const float* s = p.src[t];
   f32x4 v;
 #pragma unroll
   for (int q = 0; q < 4; ++q)
-    v[q] = (row < p.R && c0 + q < p.C) ? f * s[(int64_t)row * p.ld + c0 + q] : 0.0f;
+    v[q] = (row < p.R && c0 + q < p.C)
+               ? f * (p.trans ? s[(int64_t)(c0 + q) * p.ld + row] : s[(int64_t)row * p.ld + c0 + q])
+               : 0.0f;
   reinterpret_cast<f32x4*>(p.dst)[((int64_t)t * p.RB * p.CB + fr) * 64 + lane] = v;
 }
 
@@ -175,8 +179,9 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
 // ---- pack helpers
 inline hipError_t pack(const float* const* srcs, int T, int R, int C, int64_t ld, int RB, int CB,
                        int order, float* dst, hipStream_t s, float sign = 1.0f,
-                       const float* scal = nullptr) {
+                       const float* scal = nullptr, int trans = 0, int t0 = 0) {
   PackArgs pa{};
+  pa.trans = trans; pa.t0 = t0;
   for (int t = 0; t < T; ++t) pa.src[t] = srcs[t];
   pa.R = R; pa.C = C; pa.RB = RB; pa.CB = CB; pa.order = order; pa.ld = ld; pa.dst = dst;
   pa.sign = sign; pa.scal = scal;
@@ -310,6 +315,197 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
   return 0;
 }
 
+// ======================================================================== backward driver
+struct BwdPlan {
+  Plan fwd;                       // the forward's plan (which kernel formed U)
+  int MB, NB, SBm, MBpm, NBpn, slices_m, slices_n, gx;
+  int64_t Bpad, Rn, Rm;           // padded batch; padded rows of the gU / Var buffers
+  int nslots, ncg;
+  int wtiles, nchunks; int64_t chunk;
+  size_t off_a1, off_at, off_m, off_mt, off_az, off_ae, off_al, off_at_, off_gp, off_var,
+      off_part, off_wpart, total;
+};
+
+inline int validate_bwd(const dladmm_bwd_desc* d) {
+  if (!d) return DLADMM_E_NULL;
+  if (int e = validate(&d->fwd)) return e;
+  const dladmm_fwd_desc& f = d->fwd;
+  if (!f.keep_all || !f.T) return DLADMM_E_UNSUPPORTED;
+  if (!d->gW) return DLADMM_E_NULL;
+  if (d->ld_gw < f.m) return DLADMM_E_SHAPE;
+  if ((d->gZ || d->gE || d->gL || d->gT) && d->ld_g < f.batch) return DLADMM_E_SHAPE;
+  const int v = f.variant;
+  if (v >= DLADMM_V4_SCALAR && !d->g_scalar) return DLADMM_E_NULL;
+  if ((v == DLADMM_V2_LTHETA || v == DLADMM_V3_FULL) && !d->g_row) return DLADMM_E_NULL;
+  if (v == DLADMM_V1_LENA) {
+    if (!d->g_beta1_elem || !d->g_beta2_elem) return DLADMM_E_NULL;
+    for (int k = 0; k < f.layers; ++k)
+      if (!d->g_beta1_elem[k] || !d->g_beta2_elem[k]) return DLADMM_E_NULL;
+  }
+  return 0;
+}
+
+inline int64_t round_up(int64_t x, int64_t q) { return (x + q - 1) / q * q; }
+
+inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
+  *p = BwdPlan{};
+  const dladmm_fwd_desc& f = d->fwd;
+  if (int e = make_plan(&f, &p->fwd)) return e;
+  const int m = f.m, n = f.n;
+  const int64_t B = f.batch;
+  p->MB = ceil_div(m, 16);
+  p->NB = ceil_div(n, 16);
+  p->SBm = 16;                          // BK1 / BK3 output rows: m (SB = 32 spills registers)
+  p->MBpm = ceil_div(p->MB, p->SBm) * p->SBm;
+  p->NBpn = ceil_div(p->NB, 16) * 16;   // BK2 output rows: n (two accumulator sets: 16 blocks)
+  p->slices_m = p->MBpm / p->SBm;
+  p->slices_n = p->NBpn / 16;
+  p->gx = ceil_div(f.batch, kBwdCols);
+  p->Bpad = round_up(B, 16);
+  p->Rn = round_up(n, 128);
+  p->Rm = round_up(m, 128);
+  p->ncg = p->gx * kBwdWaves;
+  p->nslots = p->ncg * (p->slices_m > p->slices_n ? p->slices_m : p->slices_n);
+  const int64_t rs = f.row_stride > 0 ? f.row_stride : 1;
+  const int64_t part_floats = 8 * (p->nslots > rs * p->ncg ? (int64_t)p->nslots : rs * p->ncg);
+  p->wtiles = (int)((p->Rn / 128) * (p->Rm / 128));
+  const int64_t steps = p->Bpad / 16;
+  int64_t nch = (512 + p->wtiles - 1) / p->wtiles;
+  if (nch > steps) nch = steps;
+  if (nch < 1) nch = 1;
+  p->chunk = ceil_div((int)steps, (int)nch) * 16;
+  p->nchunks = (int)((p->Bpad + p->chunk - 1) / p->chunk);
+  const size_t fb = (size_t)kFrag * sizeof(float);
+  const size_t colb = (size_t)p->Bpad * sizeof(float);
+  size_t o = 0;
+  p->off_a1 = o; o += align256(fb * p->NB * p->MBpm);     // A      [NB][MBpm]   (BK1)
+  p->off_at = o; o += align256(fb * p->MB * p->NBpn);     // A^T    [MB][NBpn]   (BK2)
+  p->off_m = o; o += align256(fb * p->MB * p->NBpn);      // M_k    [MB][NBpn]   (BK2)
+  p->off_mt = o; o += align256(fb * p->NB * p->MBpm);     // M_k^T  [NB][MBpm]   (BK3)
+  p->off_az = o; o += align256(colb * p->Rn);
+  p->off_ae = o; o += align256(colb * m);
+  p->off_al = o; o += align256(colb * m);
+  p->off_at_ = o; o += align256(colb * m);
+  p->off_gp = o; o += align256(colb * m);
+  p->off_var = o; o += align256(colb * p->Rm);
+  p->off_part = o; o += align256(sizeof(float) * part_floats);
+  p->off_wpart = o; o += align256(sizeof(float) * (size_t)p->nchunks * n * m);
+  p->total = o;
+  return 0;
+}
+
+inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStream_t s) {
+  const dladmm_fwd_desc& f = d->fwd;
+  const int K = f.layers, m = f.m, n = f.n;
+  const int64_t B = f.batch, ldo = f.ld_out, ldw = p.Bpad;
+  const int v = f.variant;
+  const bool has_s1 = v >= DLADMM_V4_SCALAR;
+  const bool tied = v == DLADMM_V5_TIED;
+  const bool ufused = p.fwd.path == 1;
+  const bool rowk = v == DLADMM_V2_LTHETA || v == DLADMM_V3_FULL;
+  float* A1 = (float*)(ws + p.off_a1);
+  float* At = (float*)(ws + p.off_at);
+  float* Mp = (float*)(ws + p.off_m);
+  float* Mt = (float*)(ws + p.off_mt);
+  float* AZ = (float*)(ws + p.off_az);
+  float* AE = (float*)(ws + p.off_ae);
+  float* AL = (float*)(ws + p.off_al);
+  float* AT = (float*)(ws + p.off_at_);
+  float* GP = (float*)(ws + p.off_gp);
+  float* VAR = (float*)(ws + p.off_var);
+  float* part = (float*)(ws + p.off_part);
+  float* wpart = (float*)(ws + p.off_wpart);
+  // adjoints start at zero; the padded rows / columns of gU and Var stay zero (wgrad reads them)
+  if (hipError_t e = hipMemsetAsync(ws + p.off_az, 0, p.off_part - p.off_az, s)) return (int)e;
+  if (tied) {
+    if (hipError_t e = hipMemset2DAsync(d->gW, d->ld_gw * sizeof(float), 0, m * sizeof(float), n, s))
+      return (int)e;
+  }
+  const float* asrc[1] = {f.A};
+  // BK1 operand: A (rows m, contraction n); BK2 operand: A^T (rows n, contraction m)
+  if (hipError_t e = pack(asrc, 1, m, n, f.ld_a, p.MBpm, p.NB, 1, A1, s)) return (int)e;
+  if (hipError_t e = pack(asrc, 1, n, m, f.ld_a, p.NBpn, p.MB, 1, At, s, 1.0f, nullptr, 1))
+    return (int)e;
+  const int64_t zl = (int64_t)n * ldo, ml = (int64_t)m * ldo;
+  const int64_t gzl = (int64_t)n * d->ld_g, gml = (int64_t)m * d->ld_g;
+  BwdArgs a{};
+  a.m = m; a.n = n; a.B = (int)B; a.K = K;
+  a.ufused = ufused ? 1 : 0;
+  a.nslots = p.nslots; a.ncg = p.ncg;
+  a.X = f.X; a.ldx = f.ld_x;
+  a.ldg = d->ld_g;
+  a.AZ = AZ; a.AE = AE; a.AL = AL; a.AT = AT; a.GP = GP; a.VAR = VAR; a.ldw = ldw;
+  a.scal = f.scalar_params;
+  a.rowp = f.row_params; a.rstride = f.row_stride;
+  a.ldb = f.ld_beta;
+  a.part = part;
+  const dim3 gm(p.gx, p.slices_m), gn(p.gx, p.slices_n);
+  const size_t part_bytes = p.off_wpart - p.off_part;
+  for (int k = K - 1; k >= 0; --k) {
+    // M_k exactly as the forward packed it (fused: -s1 W_k; per-layer: W_k), and (-s1 W_k)^T
+    const float* wsrc[1] = {f.W[k]};
+    if (hipError_t e = pack(wsrc, 1, n, m, f.ld_w, p.NBpn, p.MB, 1, Mp, s, ufused ? -1.0f : 1.0f,
+                            (ufused && has_s1) ? f.scalar_params : nullptr, 0, k))
+      return (int)e;
+    if (hipError_t e = pack(wsrc, 1, m, n, f.ld_w, p.MBpm, p.NB, 1, Mt, s, -1.0f,
+                            has_s1 ? f.scalar_params : nullptr, 1, k))
+      return (int)e;
+    if (hipError_t e = hipMemsetAsync(part, 0, part_bytes, s)) return (int)e;
+    a.k = k;
+    a.Ep = k ? f.E + (k - 1) * ml : f.E0; a.ldep = k ? ldo : f.ld_e0;
+    a.Lp = k ? f.L + (k - 1) * ml : f.L0; a.ldlp = k ? ldo : f.ld_l0;
+    a.Zp = k ? f.Z + (k - 1) * zl : f.Z0; a.ldzp = k ? ldo : f.ld_z0;
+    a.Tk = f.T + k * ml; a.ldt = ldo;
+    a.gZ = d->gZ ? d->gZ + k * gzl : nullptr;
+    a.gE = d->gE ? d->gE + k * gml : nullptr;
+    a.gL = d->gL ? d->gL + k * gml : nullptr;
+    a.gT = d->gT ? d->gT + (k + 1) * gml : nullptr;
+    if (v == DLADMM_V1_LENA) {
+      a.b1e = f.beta1_elem[k]; a.b2e = f.beta2_elem[k];
+      a.gb1e = d->g_beta1_elem[k]; a.gb2e = d->g_beta2_elem[k];
+    }
+    // BK1: P = A Z_k
+    BwdArgs b1 = a;
+    b1.KB = p.NB; b1.MBp = p.MBpm; b1.Krows = n; b1.Wp = A1;
+    b1.S = f.Z + k * zl; b1.ldS = ldo;
+    if (hipError_t e = launch_bwd(1, v, b1, gm, p.SBm, s)) return (int)e;
+    // BK2: R = A^T gP, q = M_k Var_k
+    BwdArgs b2 = a;
+    b2.KB = p.MB; b2.MBp = p.NBpn; b2.Krows = m;
+    b2.Wp = At; b2.S = GP; b2.ldS = ldw;
+    b2.Wp2 = Mp; b2.S2 = VAR; b2.ldS2 = ldw;
+    if (hipError_t e = launch_bwd(2, v, b2, gn, 16, s)) return (int)e;
+    // BK3: gVar = M_k^T gU
+    BwdArgs b3 = a;
+    b3.KB = p.NB; b3.MBp = p.MBpm; b3.Krows = n; b3.Wp = Mt;
+    b3.S = AZ; b3.ldS = ldw;
+    if (hipError_t e = launch_bwd(3, v, b3, gm, p.SBm, s)) return (int)e;
+    // weight gradient gW_k = -s1 * gU Var_k^T (split-K over the batch, fixed-order reduction)
+    WgradArgs wa{};
+    wa.G = AZ; wa.V = VAR; wa.ld = ldw; wa.n = n; wa.m = m;
+    wa.NBp16 = (int)(p.Rn / 16); wa.MBp16 = (int)(p.Rm / 16);
+    wa.Bpad = p.Bpad; wa.chunk = p.chunk; wa.nchunks = p.nchunks; wa.part = wpart;
+    if (hipError_t e = launch_wgrad(wa, p.wtiles, s)) return (int)e;
+    float* gWk = tied ? d->gW : d->gW + (int64_t)k * n * d->ld_gw;
+    if (hipError_t e = launch_wgrad_reduce(wpart, p.nchunks, n, m,
+                                           has_s1 ? f.scalar_params : nullptr, k, tied ? 1 : 0,
+                                           gWk, d->ld_gw, s))
+      return (int)e;
+    // parameter slots: fixed-order fp64 sums of the per-wave partials
+    if (v >= DLADMM_V4_SCALAR) {
+      hipLaunchKernelGGL(loss_reduce_kernel, dim3(DLADMM_NSCALAR), dim3(256), 0, s,
+                         (const float*)part, p.nslots, d->g_scalar + (int64_t)k * DLADMM_NSCALAR);
+      if (hipError_t e = hipGetLastError()) return (int)e;
+    } else if (rowk) {
+      hipLaunchKernelGGL(loss_reduce_kernel, dim3((unsigned)(DLADMM_NSCALAR * f.row_stride)),
+                         dim3(256), 0, s, (const float*)part, p.ncg,
+                         d->g_row + (int64_t)k * DLADMM_NSCALAR * f.row_stride);
+      if (hipError_t e = hipGetLastError()) return (int)e;
+    }
+  }
+  return 0;
+}
+
 }  // namespace dladmm
 
 extern "C" {
@@ -350,6 +546,24 @@ int dladmm_fwd_f32(const dladmm_fwd_desc* d, void* stream) {
     if (hipError_t e = hipGetLastError()) return (int)e;
   }
   return 0;
+}
+
+size_t dladmm_bwd_workspace_bytes(const dladmm_bwd_desc* d) {
+  using namespace dladmm;
+  if (validate_bwd(d)) return 0;
+  BwdPlan p;
+  if (make_bwd_plan(d, &p)) return 0;
+  return p.total;
+}
+
+int dladmm_bwd_f32(const dladmm_bwd_desc* d, void* stream) {
+  using namespace dladmm;
+  if (int e = validate_bwd(d)) return e;
+  BwdPlan p;
+  if (int e = make_bwd_plan(d, &p)) return e;
+  if (!d->workspace || d->workspace_bytes < p.total) return DLADMM_E_WORKSPACE;
+  if (((uintptr_t)d->workspace) & 255) return DLADMM_E_ALIGN;
+  return run_bwd(d, p, (char*)d->workspace, (hipStream_t)stream);
 }
 
 const char* dladmm_error_string(int code) {

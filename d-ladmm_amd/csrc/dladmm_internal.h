@@ -70,3 +70,48 @@ hipError_t launch_layer(int phase, int variant, const LayerArgs& a, dim3 grid, i
                         hipStream_t s);
 
 }  // namespace dladmm
+
+namespace dladmm {
+
+// ---- backward (dladmm_backward.hip)
+// 4 waves per workgroup = 1 wave per SIMD: the epilogues' adjoint algebra needs the full
+// 512-register budget next to 64-128 accumulator registers.
+constexpr int kBwdWaves = 4;
+constexpr int kBwdCols = 16 * kBwdWaves;
+struct BwdArgs {
+  int m, n, B, K, k;
+  int KB, MBp, Krows;         // slice GEMM geometry (BK2: both GEMMs share it)
+  int ufused;                 // 1: forward formed U = Z_{k-1} + (-s1 W_k) Var; 0: Z - s1 (W Var)
+  int nslots, ncg;            // scalar partial slots per param slot; column groups (row kind)
+  const float* Wp; const float* S; int64_t ldS;     // GEMM 1: packed operand, B operand
+  const float* Wp2; const float* S2; int64_t ldS2;  // GEMM 2 (BK2 only)
+  const float* X; int64_t ldx;
+  const float* Ep; int64_t ldep;   // E_{k-1}
+  const float* Lp; int64_t ldlp;   // L_{k-1}
+  const float* Zp; int64_t ldzp;   // Z_{k-1}
+  const float* Tk; int64_t ldt;    // T_k
+  const float* gZ; const float* gE; const float* gL; const float* gT; int64_t ldg;  // upstream
+  float* AZ; float* AE; float* AL; float* AT; float* GP; float* VAR; int64_t ldw;   // workspace
+  const float* scal;
+  const float* rowp; int64_t rstride;
+  const float* b1e; const float* b2e; int64_t ldb;  // V1 betas of layer k
+  float* gb1e; float* gb2e;                          // V1 beta grads of layer k
+  float* part;
+};
+
+struct WgradArgs {
+  const float* G; const float* V; int64_t ld;  // gU (NR x ld), Var (MR x ld), zero-padded
+  int n, m;                                    // valid rows of G / V
+  int NBp16, MBp16;                            // padded rows / 16 (multiples of 8)
+  int64_t Bpad, chunk;                         // padded batch; columns per split-K chunk
+  int nchunks;
+  float* part;                                 // [nchunks][n][m]
+};
+
+hipError_t launch_bwd(int phase, int variant, const BwdArgs& a, dim3 grid, int sb,
+                      hipStream_t s);
+hipError_t launch_wgrad(const WgradArgs& a, int tiles, hipStream_t s);
+hipError_t launch_wgrad_reduce(const float* part, int nchunks, int n, int m, const float* scal,
+                               int k, int accumulate, float* gW, int64_t ldgw, hipStream_t s);
+
+}  // namespace dladmm

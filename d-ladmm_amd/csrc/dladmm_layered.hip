@@ -17,113 +17,26 @@
 // by LDS-DMA, shared by the NW waves.  Code size is one k-block of MFMAs, not a whole layer.
 #include "dladmm_common.h"
 #include "dladmm_internal.h"
+#include "dladmm_slice.h"
 
 namespace dladmm {
 
-// B operand of one k-block for this lane: rows 16kb + 4g + q (q = 0..3) of column col of
-// S[Krows][ld]; rows >= Krows (padding) and invalid columns read 0.  Branch-free: the address is
-// clamped, the value selected.
-__device__ __forceinline__ f32x4 load_bfrag(const float* S, int64_t ld, int Krows, int kb, int g,
-                                            int64_t colc, bool cv) {
-  f32x4 v;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int row = 16 * kb + 4 * g + q;
-    const bool ok = cv && row < Krows;
-    const float x = S[(int64_t)(ok ? row : 0) * ld + colc];
-    v[q] = ok ? x : 0.0f;
-  }
-  return v;
-}
-
 template <int EMODE, int PKIND, int PH, int NW, int SB>
 __global__ __launch_bounds__(NW * 64, 1) void layer_kernel(const LayerArgs a) {
-  constexpr int CF = 16;             // fragments per ring chunk (16 KiB)
-  constexpr int NCI = SB / CF;       // chunks per k-block
-  constexpr int D = 2;               // fragment read-ahead
-  constexpr int NBUF = D + 2;        // a step consumes a PAIR of fragments: D + 2 in rotation
-  static_assert(SB % CF == 0, "slice must be whole chunks");
-  __shared__ f32x4 ring[2 * CF * 64];
+  __shared__ f32x4 ring[2 * kSliceCF * 64];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int j = lane & 15, g = lane >> 4;
-  const int64_t col = (int64_t)blockIdx.x * (16 * NW) + w * 16 + j;
+  const int g = lane >> 4;
+  const int64_t col = (int64_t)blockIdx.x * (16 * NW) + w * 16 + (lane & 15);
   const bool cv = col < a.B;
   const int64_t colc = cv ? col : 0;
-  const int slice = blockIdx.y;
-  const int ib0 = slice * SB;  // first output block of this slice
-  const int KB = a.KB;
+  const int ib0 = blockIdx.y * SB;  // first output block of this slice
   const int k = a.k;
 
-  // ---- LDS ring of packed fragments: chunk (kb, c) = Wp[kb][ib0 + 16c .. + 16)
-  auto chunk_src = [&](int kb, int c) -> const float* {
-    return a.Wp + ((int64_t)kb * a.MBp + ib0 + c * CF) * kFrag;
-  };
-  auto issue = [&](const float* src, int slot) {
-    uint64_t sb = (uint64_t)src;
-    asm volatile("" : "+s"(sb));
-    const float* base = (const float*)sb;
-    f32x4* dst = ring + slot * (CF * 64);
-#pragma unroll
-    for (int i = 0; i < (CF + NW - 1) / NW; ++i) {
-      const int f = i * NW + w;
-      if (CF % NW == 0 || f < CF) glds16(base + f * kFrag, lane * 16, dst + f * 64);
-    }
-  };
-
   f32x4 acc[SB];
-#pragma unroll
-  for (int i = 0; i < SB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  issue(chunk_src(0, 0), 0);
-  f32x4 bn1 = load_bfrag(a.S, a.ldS, a.Krows, 0, g, colc, cv);
-  f32x4 bn2 = load_bfrag(a.S, a.ldS, a.Krows, 1, g, colc, cv);
-  f32x4 fr[NBUF];
-  int chunk_id = 0;  // running chunk index (slot = chunk_id & 1)
-
-  for (int kb = 0; kb < KB; ++kb) {
-    const f32x4 bcur = bn1;
-    bn1 = bn2;
-    bn2 = load_bfrag(a.S, a.ldS, a.Krows, kb + 2, g, colc, cv);
-    static_for<NCI>([&](auto C_) {
-      constexpr int c = decltype(C_)::value;
-      const int slot = chunk_id & 1;
-      ring_barrier();
-      {  // prefetch the next chunk (past the end: re-read chunk 0, never consumed)
-        const int nc = c + 1 < NCI ? c + 1 : 0;
-        const int nkb = c + 1 < NCI ? kb : (kb + 1 < KB ? kb + 1 : 0);
-        issue(chunk_src(nkb, nc), slot ^ 1);
-      }
-      const f32x4* rs = ring + slot * (CF * 64);
-      static_for<D>([&](auto Dd) {
-        constexpr int d = decltype(Dd)::value;
-        fr[d % NBUF] = rs[d * 64 + lane];
-      });
-      // pairs of output blocks: 8 MFMAs alternating two independent accumulators
-      static_for<CF / 2>([&](auto P_) {
-        constexpr int p = decltype(P_)::value;
-        constexpr int f0 = 2 * p, f1 = 2 * p + 1;
-        if constexpr (f0 + D < CF) fr[(f0 + D) % NBUF] = rs[(f0 + D) * 64 + lane];
-        if constexpr (f1 + D < CF) fr[(f1 + D) % NBUF] = rs[(f1 + D) * 64 + lane];
-        const f32x4 w0 = fr[f0 % NBUF], w1 = fr[f1 % NBUF];
-        f32x4& a0 = acc[c * CF + f0];
-        f32x4& a1 = acc[c * CF + f1];
-        a0 = mfma4(w0.x, bcur.x, a0);
-        a1 = mfma4(w1.x, bcur.x, a1);
-        a0 = mfma4(w0.y, bcur.y, a0);
-        a1 = mfma4(w1.y, bcur.y, a1);
-        a0 = mfma4(w0.z, bcur.z, a0);
-        a1 = mfma4(w1.z, bcur.z, a1);
-        a0 = mfma4(w0.w, bcur.w, a0);
-        a1 = mfma4(w1.w, bcur.w, a1);
-        __builtin_amdgcn_sched_barrier(0);
-      });
-      ++chunk_id;
-    });
-  }
-  ring_barrier();  // drain the speculative prefetch before the workgroup exits
+  slice_gemm<NW, SB>(ring, a.Wp, a.MBp, ib0, a.KB, a.S, a.ldS, a.Krows, colc, cv, acc);
 
   // ---------------------------------------------------------------- epilogue
   const bool lasso = a.loss_kind == DLADMM_LOSS_LASSO;

@@ -14,8 +14,13 @@ each script):
 Constructor signature `(m, n, d, batch_size, A, Z0, E0, L0, layers)`, `state_dict` keys and
 shapes, `name()` and the forward return arity all follow the reference, so a reference
 checkpoint (e.g. DLADMMNet.pth.tar, 45 keys for V1 at layers=15) loads with
-`load_state_dict(..., strict=True)` unchanged.  `forward` is inference-only: with autograd
-recording and parameters that require grad it raises (backward is future work).
+`load_state_dict(..., strict=True)` unchanged.
+
+`forward` is differentiable: with autograd recording and parameters that require grad it runs as
+the torch.autograd.Function `_DLADMMFunction`, whose backward is the HIP reverse sweep
+(ops.dladmm_backward -> dladmm_bwd_f32), so `total_loss.backward(); optimizer.step()` trains the
+module exactly as the reference training loops do (main_syn_l1l1_scalar.py:269-299).  Without
+grad it runs the inference path (no T saved for V1-V3, nothing kept for backward).
 """
 from __future__ import annotations
 
@@ -26,7 +31,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .ops import dladmm_forward
+from .ops import ForwardResult, dladmm_backward, dladmm_forward
 
 
 def _dev(t: torch.Tensor) -> torch.Tensor:
@@ -90,16 +95,13 @@ class _DLADMMBase(nn.Module):
     def _tables(self, dev) -> dict:  # pragma: no cover - per variant
         raise NotImplementedError
 
-    def _check_grad(self):
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise RuntimeError(
-                "dladmm: the fused HIP forward is inference-only (no backward yet); call it "
-                "under torch.no_grad() / torch.inference_mode() or set requires_grad_(False)")
+    def _needs_grad(self) -> bool:
+        return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
 
     def run(self, x: torch.Tensor, keep_all: bool = True, loss_kind: int = 0,
             kernel_events=None):
-        """Fused forward returning the raw ops.ForwardResult (stacked [K, rows, B] outputs)."""
-        self._check_grad()
+        """Fused forward returning the raw ops.ForwardResult (stacked [K, rows, B] outputs).
+        Not differentiable (it is the inference path; `forward` is the differentiable one)."""
         with torch.no_grad():
             dev = self.A.device
             return dladmm_forward(
@@ -108,14 +110,50 @@ class _DLADMMBase(nn.Module):
                 loss_kind=loss_kind, kernel_events=kernel_events, **self._tables(dev))
 
     def forward(self, x):
-        r = self.run(x)
         K = self.layers
-        Z = [r.Z[k] for k in range(K)]
-        E = [r.E[k] for k in range(K)]
-        L = [r.L[k] for k in range(K)]
+        if self._needs_grad():
+            if x.requires_grad:
+                raise RuntimeError("dladmm: gradients w.r.t. the input X are not supported (the "
+                                   "reference trains the parameters only)")
+            params = list(self.parameters())
+            Zs, Es, Ls, Ts = _DLADMMFunction.apply(self, x, *params)
+        else:
+            r = self.run(x)
+            Zs, Es, Ls, Ts = r.Z, r.E, r.L, r.T
+        Z = [Zs[k] for k in range(K)]
+        E = [Es[k] for k in range(K)]
+        L = [Ls[k] for k in range(K)]
         if self.RETURNS_T:
-            return Z, E, L, [r.T[k] for k in range(K + 1)]
+            return Z, E, L, [Ts[k] for k in range(K + 1)]
         return Z, E, L
+
+    # --- backward: map the C ABI's gradient tables onto the reference parameters ------------
+    # GRAD_SLOTS: ParameterList name -> (kind, slots summed).  kind 'scalar' reads g_scalar,
+    # 'row' reads g_row (theta_z rows = d, else m), 'elem1'/'elem2' the V1 per-sample betas.
+    GRAD_SLOTS: dict = {}
+
+    def _param_grads(self, res) -> dict:
+        K = self.layers
+        out = {}
+        for name, (kind, slots) in self.GRAD_SLOTS.items():
+            for k in range(K):
+                key = f"{name}.{k}"
+                if kind == "scalar":
+                    g = sum(res.g_scalar[k, s] for s in slots).reshape(1, 1)
+                elif kind == "row":
+                    rows = self.d if slots[0] == _lib.P_THETA_Z else self.m
+                    g = sum(res.g_row[k, s, :rows] for s in slots).reshape(rows, 1)
+                elif kind == "elem1":
+                    g = res.g_beta1[k]
+                else:
+                    g = res.g_beta2[k]
+                out[key] = g.to(torch.float32)
+        if isinstance(self.fc, nn.Linear):
+            out["fc.weight"] = res.gW[0]
+        else:
+            for k in range(K):
+                out[f"fc.{k}.weight"] = res.gW[k]
+        return out
 
     def layer_objectives(self, x, alpha: float, kind: str = "l1l1", kernel_events=None):
         """Forward + the per-layer objective of the reference training loop, fused in-kernel:
@@ -126,6 +164,41 @@ class _DLADMMBase(nn.Module):
         r = self.run(x, loss_kind=lk, kernel_events=kernel_events)
         obj = (alpha * r.loss_sums[:, 0] + r.loss_sums[:, 1]) / x.shape[1]
         return r, obj
+
+
+class _DLADMMFunction(torch.autograd.Function):
+    """The K-layer forward as one differentiable op: forward = dladmm_fwd_f32 with every layer
+    (and T) saved, backward = dladmm_bwd_f32 (the HIP reverse sweep).  Inputs: the module, X and
+    the module's parameters in `parameters()` order; outputs: stacked Z [K,n,B], E, L [K,m,B],
+    T [K+1,m,B]."""
+
+    @staticmethod
+    def forward(ctx, mod, x, *params):
+        dev = mod.A.device
+        tables = mod._tables(dev)
+        W = [w.detach() for w in mod._weights()]
+        r = dladmm_forward(mod.VARIANT, x, mod.A, W, mod.Z0, mod.E0, mod.L0, keep_all=True,
+                           want_T=True, **tables)
+        ctx.mod = mod
+        ctx.tables = tables
+        ctx.W = W
+        ctx.save_for_backward(x, r.Z, r.E, r.L, r.T)
+        if not mod.RETURNS_T:
+            ctx.mark_non_differentiable(r.T)
+        return r.Z, r.E, r.L, r.T
+
+    @staticmethod
+    def backward(ctx, gZ, gE, gL, gT):
+        x, Z, E, L, T = ctx.saved_tensors
+        mod = ctx.mod
+        c = lambda g: None if g is None else g.contiguous()  # noqa: E731
+        saved = ForwardResult(Z, E, L, T, None)
+        res = dladmm_backward(mod.VARIANT, x, mod.A, ctx.W, mod.Z0, mod.E0, mod.L0, saved,
+                              c(gZ), c(gE), c(gL), c(gT) if mod.RETURNS_T else None,
+                              tied=isinstance(mod.fc, nn.Linear), **ctx.tables)
+        grads = mod._param_grads(res)
+        names = [n for n, _ in mod.named_parameters()]
+        return (None, None) + tuple(grads.get(n) for n in names)
 
 
 def _stack_scalar(pl) -> torch.Tensor:
@@ -156,6 +229,7 @@ def _row_table(K, R, dev, m, n, **cols) -> torch.Tensor:
 class DLADMMNet(_DLADMMBase):
     """V1, main_lena.py:16-102 (also main_syn_l1l1.py, main_syn_gt.py)."""
     VARIANT = _lib.V1_LENA
+    GRAD_SLOTS = {"beta1": ("elem1", ()), "beta2": ("elem2", ())}
 
     def _register_params(self):
         # main_lena.py:30-41: beta1/beta2 (m, batch_size) per layer; thresholds are plain tensors
@@ -181,6 +255,11 @@ class DLADMMNet(_DLADMMBase):
 class DLADMMNetLTheta(_DLADMMBase):
     """V2, main_syn_l1l1_ltheta.py:16-95 (also _bkp, _rw, -dgap, main_syn_gt_ltheta.py)."""
     VARIANT = _lib.V2_LTHETA
+    # beta1 serves both Var and L (main_syn_l1l1_ltheta.py:74,80): its grad sums slots b1 + b3
+    GRAD_SLOTS = {"beta1": ("row", (_lib.P_BETA1, _lib.P_BETA3)),
+                  "beta2": ("row", (_lib.P_BETA2,)),
+                  "active_para": ("row", (_lib.P_THETA_Z,)),
+                  "active_para1": ("row", (_lib.P_THETA_E,))}
 
     def _register_params(self):
         # main_syn_l1l1_ltheta.py:30-43
@@ -201,6 +280,10 @@ class DLADMMNetFull(_DLADMMBase):
     """V3, main_syn_l1l1_full.py:16-96 (also main_syn_l1l1-sl2_full.py)."""
     VARIANT = _lib.V3_FULL
     WSCALE = 0.4
+    GRAD_SLOTS = {"beta1": ("row", (_lib.P_BETA1,)), "beta2": ("row", (_lib.P_BETA2,)),
+                  "beta3": ("row", (_lib.P_BETA3,)), "ss2": ("row", (_lib.P_SS2,)),
+                  "active_para": ("row", (_lib.P_THETA_Z,)),
+                  "active_para1": ("row", (_lib.P_THETA_E,))}
 
     def _register_params(self):
         # main_syn_l1l1_full.py:29-44
@@ -223,6 +306,10 @@ class DLADMMNetScalar(_DLADMMBase):
     RETURNS_T = True
     WSCALE = 0.4
     NAME = "DLADMMNet_scalar"
+    GRAD_SLOTS = {"beta1": ("scalar", (_lib.P_BETA1,)), "beta2": ("scalar", (_lib.P_BETA2,)),
+                  "beta3": ("scalar", (_lib.P_BETA3,)), "ss2": ("scalar", (_lib.P_SS2,)),
+                  "active_para": ("scalar", (_lib.P_THETA_Z,)),
+                  "active_para1": ("scalar", (_lib.P_THETA_E,))}
 
     def __init__(self, m, n, d, batch_size, A, Z0, E0, L0, layers):
         super().__init__(m, n, d, batch_size, A, Z0, E0, L0, layers)
@@ -252,6 +339,7 @@ class DLADMMNetScalarTied(DLADMMNetScalar):
     """V5, main_syn_l1l1_scalar_tied.py:34-104: one shared fc scaled by ss1[k]."""
     VARIANT = _lib.V5_TIED
     NAME = "DLADMMNet_scalar_tied"
+    GRAD_SLOTS = dict(DLADMMNetScalar.GRAD_SLOTS, ss1=("scalar", (_lib.P_S1,)))
 
     def _register_params(self):
         # main_syn_l1l1_scalar_tied.py:50-66 (registration order = state_dict order)
@@ -277,6 +365,9 @@ class DLADMMNetLasso(DLADMMNetScalar):
     """V6, main_syn_lasso_scalar.py:17-118: E = ss2_1*(X - A Z) - ss2_2*L."""
     VARIANT = _lib.V6_LASSO
     NAME = "DLADMMNet"
+    GRAD_SLOTS = {"beta1": ("scalar", (_lib.P_BETA1,)), "beta3": ("scalar", (_lib.P_BETA3,)),
+                  "ss2_1": ("scalar", (_lib.P_SS2,)), "ss2_2": ("scalar", (_lib.P_SS2B,)),
+                  "active_para": ("scalar", (_lib.P_THETA_Z,))}
 
     def _register_params(self):
         # main_syn_lasso_scalar.py:33-50

@@ -38,23 +38,10 @@ def _f32_dev(t: torch.Tensor, name: str) -> torch.Tensor:
     return t
 
 
-def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[torch.Tensor],
-                   Z0: torch.Tensor, E0: torch.Tensor, L0: torch.Tensor, *,
-                   scalar_params: Optional[torch.Tensor] = None,
-                   row_params: Optional[torch.Tensor] = None,
-                   beta1_elem: Sequence[torch.Tensor] = (),
-                   beta2_elem: Sequence[torch.Tensor] = (),
-                   keep_all: bool = True, want_T: bool = True, loss_kind: int = 0,
-                   out: Optional[ForwardResult] = None,
-                   kernel_events: Optional[tuple] = None) -> ForwardResult:
-    """Run the whole K-layer forward of `variant` (dladmm_variant) on X's device.
-
-    X: (m, B); A: (m, n); W: K tensors (n, m) (fc[k].weight; V5 passes the shared one K times);
-    Z0: (n, B); E0, L0: (m, B).  scalar_params: (K, 8) device fp32 (V1, V4-V6);
-    row_params: (K, 8, max(m, n)) (V2, V3); beta{1,2}_elem: K tensors (m, B) (V1).
-    Returns views-ready stacked outputs and, if loss_kind, the per-layer (sum|Z|, fit) sums.
-    """
-    L = _lib.lib()
+def _fill_fwd_desc(d, variant, X, A, W, Z0, E0, L0, scalar_params, row_params, beta1_elem,
+                   beta2_elem, keep_all, loss_kind, out):
+    """Validate the forward's tensors and fill the C descriptor `d` (a FwdDesc, possibly embedded
+    in a BwdDesc).  Returns the ctypes arrays that must outlive the call."""
     X = _f32_dev(X, "X")
     A = _f32_dev(A, "A")
     Z0, E0, L0 = _f32_dev(Z0, "Z0"), _f32_dev(E0, "E0"), _f32_dev(L0, "L0")
@@ -76,18 +63,6 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
         if tuple(w.shape) != (n, m) or w.stride(0) != ldw:
             raise RuntimeError(f"dladmm: fc[{k}].weight must be ({n}, {m}) with a common stride")
     dev = X.device
-
-    Kout = K if keep_all else 1
-    if out is None:
-        Zo = torch.empty((Kout, n, B), device=dev, dtype=torch.float32)
-        Eo = torch.empty((Kout, m, B), device=dev, dtype=torch.float32)
-        Lo = torch.empty((Kout, m, B), device=dev, dtype=torch.float32)
-        To = (torch.empty((Kout + 1 if keep_all else 1, m, B), device=dev, dtype=torch.float32)
-              if want_T else None)
-        ls = torch.empty((K, 2), device=dev, dtype=torch.float64) if loss_kind else None
-        out = ForwardResult(Zo, Eo, Lo, To, ls)
-
-    d = _lib.FwdDesc()
     d.abi_version = _lib.ABI_VERSION
     d.variant, d.m, d.n, d.batch, d.layers = variant, m, n, B, K
     d.keep_all, d.loss_kind = int(bool(keep_all)), int(loss_kind)
@@ -98,7 +73,7 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
     d.L0, d.ld_l0 = L0.data_ptr(), L0.stride(0)
     warr = _lib.ptr_array([w.data_ptr() for w in Ws])
     d.W, d.ld_w = ctypes.cast(warr, ctypes.POINTER(ctypes.c_void_p)), ldw
-    keep = [warr]
+    keep = [warr, Ws]
     if scalar_params is not None:
         sp = scalar_params
         if sp.device != dev or sp.dtype != torch.float32 or tuple(sp.shape) != (K, _lib.NSCALAR) \
@@ -130,6 +105,45 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
     d.T = out.T.data_ptr() if out.T is not None else None
     d.ld_out = B
     d.loss_sums = out.loss_sums.data_ptr() if out.loss_sums is not None else None
+    return keep
+
+
+def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[torch.Tensor],
+                   Z0: torch.Tensor, E0: torch.Tensor, L0: torch.Tensor, *,
+                   scalar_params: Optional[torch.Tensor] = None,
+                   row_params: Optional[torch.Tensor] = None,
+                   beta1_elem: Sequence[torch.Tensor] = (),
+                   beta2_elem: Sequence[torch.Tensor] = (),
+                   keep_all: bool = True, want_T: bool = True, loss_kind: int = 0,
+                   out: Optional[ForwardResult] = None,
+                   kernel_events: Optional[tuple] = None) -> ForwardResult:
+    """Run the whole K-layer forward of `variant` (dladmm_variant) on X's device.
+
+    X: (m, B); A: (m, n); W: K tensors (n, m) (fc[k].weight; V5 passes the shared one K times);
+    Z0: (n, B); E0, L0: (m, B).  scalar_params: (K, 8) device fp32 (V1, V4-V6);
+    row_params: (K, 8, max(m, n)) (V2, V3); beta{1,2}_elem: K tensors (m, B) (V1).
+    Returns views-ready stacked outputs and, if loss_kind, the per-layer (sum|Z|, fit) sums.
+    """
+    L = _lib.lib()
+    _f32_dev(X, "X")
+    _f32_dev(A, "A")
+    m, B = X.shape
+    n = A.shape[1]
+    K = len(W)
+    dev = X.device
+    Kout = K if keep_all else 1
+    if out is None:
+        Zo = torch.empty((Kout, n, B), device=dev, dtype=torch.float32)
+        Eo = torch.empty((Kout, m, B), device=dev, dtype=torch.float32)
+        Lo = torch.empty((Kout, m, B), device=dev, dtype=torch.float32)
+        To = (torch.empty((Kout + 1 if keep_all else 1, m, B), device=dev, dtype=torch.float32)
+              if want_T else None)
+        ls = torch.empty((K, 2), device=dev, dtype=torch.float64) if loss_kind else None
+        out = ForwardResult(Zo, Eo, Lo, To, ls)
+
+    d = _lib.FwdDesc()
+    keep = _fill_fwd_desc(d, variant, X, A, W, Z0, E0, L0, scalar_params, row_params, beta1_elem,
+                          beta2_elem, keep_all, loss_kind, out)
     if kernel_events is not None:  # (torch.cuda.Event, torch.cuda.Event) around the fused kernel
         d.ev_kernel_start = kernel_events[0].cuda_event
         d.ev_kernel_stop = kernel_events[1].cuda_event
@@ -144,6 +158,80 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
     _lib.check(L.dladmm_fwd_f32(ctypes.byref(d), ctypes.c_void_p(stream)))
     del keep
     return out
+
+
+@dataclass
+class BackwardResult:
+    gW: torch.Tensor                  # [K, n, m] (V5 tied: [1, n, m])
+    g_scalar: Optional[torch.Tensor]  # [K, 8] fp64 (V4-V6)
+    g_row: Optional[torch.Tensor]     # [K, 8, R] fp64 (V2, V3)
+    g_beta1: List[torch.Tensor]       # V1: K tensors (m, B)
+    g_beta2: List[torch.Tensor]
+
+
+def dladmm_backward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[torch.Tensor],
+                    Z0: torch.Tensor, E0: torch.Tensor, L0: torch.Tensor, saved: ForwardResult,
+                    gZ: Optional[torch.Tensor] = None, gE: Optional[torch.Tensor] = None,
+                    gL: Optional[torch.Tensor] = None, gT: Optional[torch.Tensor] = None, *,
+                    scalar_params: Optional[torch.Tensor] = None,
+                    row_params: Optional[torch.Tensor] = None,
+                    beta1_elem: Sequence[torch.Tensor] = (),
+                    beta2_elem: Sequence[torch.Tensor] = (),
+                    tied: bool = False) -> BackwardResult:
+    """Gradients of sum_k <gZ_k,Z_k> + <gE_k,E_k> + <gL_k,L_k> + sum_j <gT_j,T_j> w.r.t. the
+    parameters of the forward that produced `saved` (a keep_all ForwardResult with T), via
+    `dladmm_bwd_f32` (include/dladmm.h).  Cotangents are stacked like the outputs ([K|K+1, rows,
+    B]); None = zero.  This is the backward of the reference's `total_loss.backward()` through
+    DLADMMNet.forward (main_syn_l1l1_scalar.py:298)."""
+    L = _lib.lib()
+    if saved.T is None or saved.Z.shape[0] != len(W):
+        raise ValueError("dladmm: backward needs the keep_all forward outputs including T")
+    m, B = X.shape
+    n = A.shape[1]
+    K = len(W)
+    dev = X.device
+    d = _lib.BwdDesc()
+    keep = _fill_fwd_desc(d.fwd, variant, X, A, W, Z0, E0, L0, scalar_params, row_params,
+                          beta1_elem, beta2_elem, True, 0, saved)
+    shapes = {"gZ": (K, n, B), "gE": (K, m, B), "gL": (K, m, B), "gT": (K + 1, m, B)}
+    for nm, g in (("gZ", gZ), ("gE", gE), ("gL", gL), ("gT", gT)):
+        if g is None:
+            continue
+        if tuple(g.shape) != shapes[nm] or not g.is_contiguous() or g.dtype != torch.float32 \
+                or g.device != dev:
+            raise ValueError(f"dladmm: {nm} must be a contiguous fp32 {shapes[nm]} device tensor")
+        setattr(d, nm, g.data_ptr())
+        keep.append(g)
+    d.ld_g = B
+    gWo = torch.empty((1 if tied else K, n, m), device=dev, dtype=torch.float32)
+    d.gW, d.ld_gw = gWo.data_ptr(), m
+    g_scalar = g_row = None
+    g1, g2 = [], []
+    if variant >= _lib.V4_SCALAR:
+        g_scalar = torch.zeros((K, _lib.NSCALAR), device=dev, dtype=torch.float64)
+        d.g_scalar = g_scalar.data_ptr()
+    elif variant in (_lib.V2_LTHETA, _lib.V3_FULL):
+        g_row = torch.zeros((K, _lib.NSCALAR, d.fwd.row_stride), device=dev, dtype=torch.float64)
+        d.g_row = g_row.data_ptr()
+    else:
+        g1 = [torch.empty((m, B), device=dev, dtype=torch.float32) for _ in range(K)]
+        g2 = [torch.empty((m, B), device=dev, dtype=torch.float32) for _ in range(K)]
+        if d.fwd.ld_beta != B:
+            raise ValueError("dladmm: V1 backward needs contiguous (m, B) betas")
+        a1 = _lib.ptr_array([t.data_ptr() for t in g1])
+        a2 = _lib.ptr_array([t.data_ptr() for t in g2])
+        keep += [a1, a2]
+        d.g_beta1_elem = ctypes.cast(a1, ctypes.POINTER(ctypes.c_void_p))
+        d.g_beta2_elem = ctypes.cast(a2, ctypes.POINTER(ctypes.c_void_p))
+    wsb = L.dladmm_bwd_workspace_bytes(ctypes.byref(d))
+    if wsb == 0:
+        raise ValueError("dladmm: invalid backward descriptor")
+    ws = _workspace(dev, wsb)
+    d.workspace, d.workspace_bytes = ws.data_ptr(), wsb
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _lib.check(L.dladmm_bwd_f32(ctypes.byref(d), ctypes.c_void_p(stream)))
+    del keep
+    return BackwardResult(gWo, g_scalar, g_row, g1, g2)
 
 
 _WS = {}

@@ -147,6 +147,50 @@ int dladmm_fwd_path(const dladmm_fwd_desc* d);
 /* Enqueue the whole K-layer forward on `stream` (hipStream_t). */
 int dladmm_fwd_f32(const dladmm_fwd_desc* d, void* stream);
 
+/*
+ * Backward: the vector-Jacobian product of one forward call.
+ *
+ * The reference trains by `total_loss.backward()` through DLADMMNet.forward
+ * (main_lena.py:229, main_syn_l1l1_scalar.py:298, main_syn_lasso_scalar.py:285); torch autograd
+ * then produces .grad for every parameter.  dladmm_bwd_f32() produces the same gradients from
+ * the saved forward outputs and the upstream cotangents of those outputs:
+ *   grad of  sum_k <gZ_k, Z_k> + <gE_k, E_k> + <gL_k, L_k> + sum_j <gT_j, T_j>
+ * with respect to W_k (fc[k].weight), every per-layer parameter slot and, for V1, the
+ * per-sample betas.  There are no gradients for X, A, Z0, E0, L0 (plain tensors in the
+ * reference, never parameters).
+ *
+ * `fwd` must describe the forward call whose outputs are differentiated, run with keep_all = 1
+ * and T != NULL (all K layers of Z/E/L and T[0..K] saved; V1-V3 keep T internally).  Its
+ * workspace fields are ignored.  Upstream cotangents may be NULL (= zero) and share one row
+ * stride ld_g; gT has K+1 layers (gT_0 reaches no parameter and is never read).
+ */
+typedef struct dladmm_bwd_desc {
+  dladmm_fwd_desc fwd;
+
+  const float* gZ;  /* [K][n][ld_g] or NULL */
+  const float* gE;  /* [K][m][ld_g] or NULL */
+  const float* gL;  /* [K][m][ld_g] or NULL */
+  const float* gT;  /* [K+1][m][ld_g] or NULL */
+  int64_t ld_g;
+
+  /* outputs (device) */
+  float* gW; int64_t ld_gw;   /* [K][n][ld_gw] (V5 tied: ONE n x m block, summed over layers) */
+  double* g_scalar;           /* V4-V6: [K][DLADMM_NSCALAR] per-slot grads (slots the variant
+                                 does not use are 0; V1: unused) */
+  double* g_row;              /* V2/V3: [K][DLADMM_NSCALAR][fwd.row_stride] per-row grads */
+  float* const* g_beta1_elem; /* V1: host arrays of K device pointers, (m x fwd.ld_beta) each: */
+  float* const* g_beta2_elem; /*     grads of the per-sample beta1[k] / beta2[k]              */
+
+  void* workspace; size_t workspace_bytes;
+} dladmm_bwd_desc;
+
+/* Workspace the backward needs for this descriptor (0 on an invalid descriptor). */
+size_t dladmm_bwd_workspace_bytes(const dladmm_bwd_desc* d);
+
+/* Enqueue the whole reverse sweep on `stream` (hipStream_t).  Deterministic: every reduction
+   (parameter slots, per-row params, weight gradients) is summed in a fixed order. */
+int dladmm_bwd_f32(const dladmm_bwd_desc* d, void* stream);
+
 /* Text for a return code of this library (DLADMM_E_* or hipError_t). */
 const char* dladmm_error_string(int code);
 

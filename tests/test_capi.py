@@ -70,3 +70,37 @@ def test_large_shapes_take_the_per_layer_path(dl):
                      ld_z0=65536, ld_e0=65536, ld_l0=65536, ld_out=65536)
     assert L.dladmm_fwd_path(ctypes.byref(d)) == 2
     assert L.dladmm_fwd_workspace_bytes(ctypes.byref(d)) > 15 * 2048 * 512 * 4
+
+
+def _bdesc(dl, **kw):
+    d, keep = _desc(dl)
+    b = dl._lib.BwdDesc()
+    b.fwd = d
+    fake = 1 << 40
+    b.gW, b.ld_gw = fake, 256
+    b.g_scalar = fake
+    b.gZ, b.ld_g = fake, 1000
+    for k, v in kw.items():
+        setattr(b, k, v)
+    return b, keep
+
+
+def test_backward_workspace_and_validation(dl):
+    L = dl._lib.lib()
+    b, _keep = _bdesc(dl)
+    ws = L.dladmm_bwd_workspace_bytes(ctypes.byref(b))
+    # adjoint buffers (5 x m + padded n, padded m rows of padded batch) + packed A, A^T, M, M^T
+    assert ws >= (5 * 256 + 512 + 256) * 1008 * 4 + 4 * 256 * 512 * 4
+    assert ws % 256 == 0
+    for field, value, code in (("gW", None, -5), ("g_scalar", None, -5), ("ld_g", 10, -3),
+                               ("ld_gw", 100, -3)):
+        bb, _k2 = _bdesc(dl, **{field: value})
+        assert L.dladmm_bwd_workspace_bytes(ctypes.byref(bb)) == 0
+        assert L.dladmm_bwd_f32(ctypes.byref(bb), None) == code, field
+    # the forward must have saved every layer and T
+    bb, _k3 = _bdesc(dl)
+    bb.fwd.keep_all = 0
+    assert L.dladmm_bwd_f32(ctypes.byref(bb), None) == -7
+    bb.fwd.keep_all = 1
+    bb.fwd.T = None
+    assert L.dladmm_bwd_f32(ctypes.byref(bb), None) == -7

@@ -1,0 +1,177 @@
+"""Parity of the HIP backward (dladmm_bwd_f32 through the drop-in modules' autograd) with the
+reference's own autograd gradients and with the backward oracle.
+
+* golden gradient fixtures (tests/golden/grad_*.npz): the reference classes' `.grad` after
+  `total_loss.backward()` with the training loss of main_syn_l1l1_scalar.py:283-298 /
+  main_syn_lasso_scalar.py:270-285 plus seeded linear terms on every output -- every variant;
+  the loss is built here with torch ops on the GPU outputs, exactly as the reference loops do;
+* the same through the per-layer kernel path (DLADMM_PATH=layered);
+* the oracle (oracle/dladmm_oracle_grad.py, pinned by those fixtures) at a larger ragged batch;
+* determinism (bitwise) and one full Adam training step.
+
+Tolerance: norm-relative per parameter <= max(GTOL, 3 x the reference's fp32-vs-fp64 gap of that
+gradient).  GTOL = 1e-4: the GPU forward sums its GEMMs in another order than CPU BLAS, and a
+shrink mask that flips on a near-threshold element moves a gradient by more than fp32 rounding
+(the reference's own fp64 twin shows the same effect: its gap column).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+import problems as P
+
+pytestmark = pytest.mark.gpu
+
+GTOL = 1e-4
+
+
+def nrel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    nb = np.linalg.norm(b)
+    return float(np.linalg.norm(a - b) / nb) if nb > 0 else float(np.linalg.norm(a))
+
+
+def make_train_net(dl, variant, inp, sd, K):
+    m, n = inp["A"].shape
+    B = inp["X"].shape[1]
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+    net = dl.VARIANTS[variant](m=m, n=0, d=n, batch_size=B, A=t(inp["A"]), Z0=t(inp["Z0"]),
+                               E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K)
+    net.load_state_dict({k: t(v) for k, v in sd.items()}, strict=True)
+    net.requires_grad_(True)
+    return net
+
+
+def total_loss(out, X, A, up, kind, K):
+    """main_syn_l1l1_scalar.py:283-296 (decay 0.6**epoch) + the fixture's linear terms."""
+    Z, E, L = out[0], out[1], out[2]
+    coeffs = P.loss_coeffs(K)
+    alpha = P.GRAD_ALPHA
+    tot = 0
+    for k in range(K):
+        if kind == "l1l1":
+            lk = alpha * torch.sum(torch.abs(Z[k]), dim=0).mean() + \
+                torch.sum(torch.abs(X - torch.mm(A, Z[k])), dim=0).mean()
+        else:
+            lk = alpha * torch.sum(torch.abs(Z[k]), dim=0).mean() + \
+                0.5 * torch.sum((X - torch.mm(A, Z[k])) ** 2.0, dim=0).mean()
+        tot = tot + lk * coeffs[k]
+    c = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    for k in range(K):
+        tot = tot + (c(up["Gz"][k]) * Z[k]).sum() + (c(up["Ge"][k]) * E[k]).sum() + \
+            (c(up["Gl"][k]) * L[k]).sum()
+    if "Gt" in up:
+        for j in range(K + 1):
+            tot = tot + (c(up["Gt"][j]) * out[3][j]).sum()
+    return tot
+
+
+def run_grads(dl, name):
+    g, meta = load_golden(name)
+    d = meta["defn"]
+    inp, sd = P.build_problem(d)
+    up = P.make_upstream(d, P.VARIANT_SPECS[d["variant"]]["ret_t"])
+    net = make_train_net(dl, d["variant"], inp, sd, d["K"])
+    X = torch.from_numpy(inp["X"]).cuda()
+    A = torch.from_numpy(inp["A"]).cuda()
+    out = net(X)
+    loss = total_loss(out, X, A, up, meta["gdef"]["loss"], d["K"])
+    loss.backward()
+    torch.cuda.synchronize()
+    return g, meta, net, float(loss.detach())
+
+
+def check_against_golden(g, meta, net):
+    got = {k: p.grad for k, p in net.named_parameters()}
+    worst = {}
+    for key in meta["keys"]:
+        assert got[key] is not None, key
+        ref = g["g:" + key]
+        e = nrel(got[key].detach().cpu().numpy(), ref)
+        tol = max(GTOL, 3.0 * float(g["gap:" + key]))
+        worst[key] = e
+        assert e <= tol, (key, e, tol)
+    return worst
+
+
+@pytest.mark.parametrize("name", sorted(P.GRAD_FIXTURES))
+def test_grads_match_reference_autograd(name, dl):
+    g, meta, net, loss = run_grads(dl, name)
+    np.testing.assert_allclose(loss, g["loss"][0], rtol=1e-4)
+    check_against_golden(g, meta, net)
+
+
+@pytest.mark.parametrize("name", ["grad_v4_med", "grad_v6_med", "grad_v1_med", "grad_v3_med",
+                                  "grad_v5_small", "grad_v2_ragged"])
+def test_grads_layered_path(name, dl, monkeypatch):
+    """Forward and backward both on the per-layer kernels (the path of m > 256 / n > 512)."""
+    monkeypatch.setenv("DLADMM_PATH", "layered")
+    g, meta, net, _ = run_grads(dl, name)
+    check_against_golden(g, meta, net)
+
+
+def test_grads_deterministic(dl):
+    a = run_grads(dl, "grad_v4_med")[2]
+    b = run_grads(dl, "grad_v4_med")[2]
+    for (ka, pa), (kb, pb) in zip(a.named_parameters(), b.named_parameters()):
+        assert torch.equal(pa.grad, pb.grad), ka
+
+
+@pytest.mark.parametrize("variant", ["v4", "v2"])
+def test_grads_match_oracle_larger_batch(variant, dl):
+    """B = 333 (ragged, 6 column tiles) at m=250, n=500 against the backward oracle."""
+    from oracle import dladmm_oracle as fwd
+    from oracle import dladmm_oracle_grad as og
+    m, n, B, K = 250, 500, 333, 4
+    d = dict(variant=variant, m=m, n=n, B=B, K=K, seed=9100, perturb=0.1, wscale=0.4)
+    inp, sd = P.build_problem(d)
+    up = P.make_upstream(d, P.VARIANT_SPECS[variant]["ret_t"])
+    net = make_train_net(dl, variant, inp, sd, K)
+    X = torch.from_numpy(inp["X"]).cuda()
+    A = torch.from_numpy(inp["A"]).cuda()
+    loss = total_loss(net(X), X, A, up, "l1l1", K)
+    loss.backward()
+    ref = {}
+    for dt in (np.float32, np.float64):
+        o = fwd.forward(variant, inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd, K,
+                        dtype=dt)
+        gz = og.train_loss_grads(o["Z"], inp["X"], inp["A"], P.GRAD_ALPHA, P.loss_coeffs(K),
+                                 "l1l1", dtype=dt)
+        gz = [a + b for a, b in zip(gz, up["Gz"])]
+        ref[dt] = og.vjp(variant, inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd, K,
+                         gZ=gz, gE=list(up["Ge"]), gL=list(up["Gl"]),
+                         gT=list(up["Gt"]) if "Gt" in up else None, dtype=dt)
+    for key, p in net.named_parameters():
+        # against the fp64 oracle, within the fp32 oracle's own distance from it
+        gap = nrel(ref[np.float32][key], ref[np.float64][key])
+        e = nrel(p.grad.cpu().numpy(), ref[np.float64][key])
+        assert e <= max(GTOL, 3.0 * gap), (key, e, gap)
+
+
+def test_adam_training_step(dl):
+    """One reference training step (main_syn_l1l1_scalar.py:269-299: zero_grad, forward, loss,
+    backward, Adam step) moves the parameters exactly as the same step driven by the oracle's
+    gradients."""
+    name = "grad_v4_small"
+    g, meta = load_golden(name)
+    d = meta["defn"]
+    inp, sd = P.build_problem(d)
+    up = P.make_upstream(d, True)
+    net = make_train_net(dl, "v4", inp, sd, d["K"])
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3)
+    opt.zero_grad()
+    X = torch.from_numpy(inp["X"]).cuda()
+    A = torch.from_numpy(inp["A"]).cuda()
+    total_loss(net(X), X, A, up, "l1l1", d["K"]).backward()
+    opt.step()
+    # the same Adam step on CPU parameters whose .grad is the reference autograd gradient
+    ref = {k: torch.nn.Parameter(torch.from_numpy(v.copy())) for k, v in sd.items()}
+    opt2 = torch.optim.Adam(list(ref.values()), lr=1e-3)
+    for k, p in ref.items():
+        p.grad = torch.from_numpy(g["g:" + k])
+    opt2.step()
+    for k, p in net.named_parameters():
+        np.testing.assert_allclose(p.detach().cpu().numpy(), ref[k].detach().numpy(),
+                                   rtol=0, atol=1e-6, err_msg=k)

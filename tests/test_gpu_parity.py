@@ -190,8 +190,8 @@ def test_errors_are_loud(dl):
         with pytest.raises(RuntimeError):   # no CPU fallback
             net(torch.zeros(m, B))
     net.requires_grad_(True)
-    with pytest.raises(RuntimeError):       # inference-only op under autograd
-        net(torch.zeros(m, B, device="cuda"))
+    with pytest.raises(RuntimeError):       # no gradients w.r.t. the input X (reference: data)
+        net(torch.zeros(m, B, device="cuda", requires_grad=True))
 
 
 def test_baseline_size_column_subset_and_fused_loss(dl, oracle):
