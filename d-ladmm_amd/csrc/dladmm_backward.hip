@@ -170,6 +170,14 @@ __global__ __launch_bounds__(NW * 64, 1) void bwd_kernel(const BwdArgs a) {
           gLp = aL - ss2b * gEt;
         }
         (void)e;
+        if (a.loss_kind) {
+          // d/dP of cf_k * fit_k: fit = sum|X - P| (torch sgn(0) = 0) or 0.5 sum (X - P)^2
+          const float cf = ((cfloat_p)a.lcoef)[2 * k + 1];
+          const float res = x - P;
+          const float dfit = a.loss_kind == DLADMM_LOSS_LASSO
+                                 ? res : (res > 0.f ? 1.f : (res < 0.f ? -1.f : 0.f));
+          gP = gP - cf * dfit;
+        }
         if (ok) {
           a.GP[o] = gP;
           a.AE[o] = gEp;
@@ -201,7 +209,13 @@ __global__ __launch_bounds__(NW * 64, 1) void bwd_kernel(const BwdArgs a) {
         // U exactly as the forward kernel that produced the saved outputs formed it
         const float U = a.ufused ? zp + q : zp - ((PKIND == PK_SCALAR) ? s1 * q : q);
         const float thz = pm(DLADMM_P_THETA_Z, rowc);
-        const float gZt = (a.AZ[o] + up(a.gZ, rowc)) + R;
+        float gZt = (a.AZ[o] + up(a.gZ, rowc)) + R;
+        if (a.loss_kind) {
+          // d/dZ_k of cz_k * sum|Z_k|, Z_k = S(U, theta_z) recomputed as the forward formed it
+          const float cz = ((cfloat_p)a.lcoef)[2 * k];
+          const float z = shrink(U, thz);
+          gZt = gZt + cz * (z > 0.f ? 1.f : (z < 0.f ? -1.f : 0.f));
+        }
         const SD d = shrink_d(U, thz);
         const float gU = gZt * d.dx;
         pv[DLADMM_P_THETA_Z] = gZt * d.dth;

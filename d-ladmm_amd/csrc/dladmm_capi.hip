@@ -334,6 +334,8 @@ inline int validate_bwd(const dladmm_bwd_desc* d) {
   if (!d->gW) return DLADMM_E_NULL;
   if (d->ld_gw < f.m) return DLADMM_E_SHAPE;
   if ((d->gZ || d->gE || d->gL || d->gT) && d->ld_g < f.batch) return DLADMM_E_SHAPE;
+  if (d->loss_kind < 0 || d->loss_kind > 2) return DLADMM_E_UNSUPPORTED;
+  if (d->loss_kind && !d->loss_coef) return DLADMM_E_NULL;
   const int v = f.variant;
   if (v >= DLADMM_V4_SCALAR && !d->g_scalar) return DLADMM_E_NULL;
   if ((v == DLADMM_V2_LTHETA || v == DLADMM_V3_FULL) && !d->g_row) return DLADMM_E_NULL;
@@ -427,13 +429,14 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
   if (hipError_t e = pack(asrc, 1, n, m, f.ld_a, p.NBpn, p.MB, 1, At, s, 1.0f, nullptr, 1))
     return (int)e;
   const int64_t zl = (int64_t)n * ldo, ml = (int64_t)m * ldo;
-  const int64_t gzl = (int64_t)n * d->ld_g, gml = (int64_t)m * d->ld_g;
   BwdArgs a{};
   a.m = m; a.n = n; a.B = (int)B; a.K = K;
   a.ufused = ufused ? 1 : 0;
   a.nslots = p.nslots; a.ncg = p.ncg;
   a.X = f.X; a.ldx = f.ld_x;
   a.ldg = d->ld_g;
+  a.loss_kind = d->loss_kind;
+  a.lcoef = d->loss_coef;
   a.AZ = AZ; a.AE = AE; a.AL = AL; a.AT = AT; a.GP = GP; a.VAR = VAR; a.ldw = ldw;
   a.scal = f.scalar_params;
   a.rowp = f.row_params; a.rstride = f.row_stride;
@@ -456,10 +459,10 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
     a.Lp = k ? f.L + (k - 1) * ml : f.L0; a.ldlp = k ? ldo : f.ld_l0;
     a.Zp = k ? f.Z + (k - 1) * zl : f.Z0; a.ldzp = k ? ldo : f.ld_z0;
     a.Tk = f.T + k * ml; a.ldt = ldo;
-    a.gZ = d->gZ ? d->gZ + k * gzl : nullptr;
-    a.gE = d->gE ? d->gE + k * gml : nullptr;
-    a.gL = d->gL ? d->gL + k * gml : nullptr;
-    a.gT = d->gT ? d->gT + (k + 1) * gml : nullptr;
+    a.gZ = d->gZ ? d->gZ[k] : nullptr;
+    a.gE = d->gE ? d->gE[k] : nullptr;
+    a.gL = d->gL ? d->gL[k] : nullptr;
+    a.gT = d->gT ? d->gT[k + 1] : nullptr;
     if (v == DLADMM_V1_LENA) {
       a.b1e = f.beta1_elem[k]; a.b2e = f.beta2_elem[k];
       a.gb1e = d->g_beta1_elem[k]; a.gb2e = d->g_beta2_elem[k];

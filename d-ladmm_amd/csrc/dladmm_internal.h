@@ -91,6 +91,7 @@ struct BwdArgs {
   const float* Zp; int64_t ldzp;   // Z_{k-1}
   const float* Tk; int64_t ldt;    // T_k
   const float* gZ; const float* gE; const float* gL; const float* gT; int64_t ldg;  // upstream
+  int loss_kind; const float* lcoef;  // fused training objective: device [K][2] (cz_k, cf_k)
   float* AZ; float* AE; float* AL; float* AT; float* GP; float* VAR; int64_t ldw;   // workspace
   const float* scal;
   const float* rowp; int64_t rstride;

@@ -115,17 +115,45 @@ class _DLADMMBase(nn.Module):
             if x.requires_grad:
                 raise RuntimeError("dladmm: gradients w.r.t. the input X are not supported (the "
                                    "reference trains the parameters only)")
-            params = list(self.parameters())
-            Zs, Es, Ls, Ts = _DLADMMFunction.apply(self, x, *params)
+            outs = _DLADMMFunction.apply(self, x, *self.parameters())
+            Z, E, L = list(outs[:K]), list(outs[K:2 * K]), list(outs[2 * K:3 * K])
+            T = list(outs[3 * K:])
         else:
             r = self.run(x)
-            Zs, Es, Ls, Ts = r.Z, r.E, r.L, r.T
-        Z = [Zs[k] for k in range(K)]
-        E = [Es[k] for k in range(K)]
-        L = [Ls[k] for k in range(K)]
+            Z = [r.Z[k] for k in range(K)]
+            E = [r.E[k] for k in range(K)]
+            L = [r.L[k] for k in range(K)]
+            T = [r.T[k] for k in range(K + 1)] if self.RETURNS_T else None
         if self.RETURNS_T:
-            return Z, E, L, [Ts[k] for k in range(K + 1)]
+            return Z, E, L, T
         return Z, E, L
+
+    def training_loss(self, x, alpha: float, coeffs=None, kind: str = "l1l1",
+                      batch: Optional[int] = None):
+        """The reference training objective as one fused, differentiable op:
+            total = sum_k coeffs[k] * (alpha * sum(|Z_k|,0).mean() + sum(|X - A Z_k|,0).mean())
+        (main_syn_l1l1_scalar.py:283-296; kind='lasso': 0.5*sum((X - A Z_k)^2,0), lasso
+        :270-283).  coeffs default: all 1; the reference uses decay 0.6**epoch for k < K-1.
+        `batch` = the column count of the mean (default x.shape[1]; the global batch when the
+        columns are sharded over ranks).  Returns (total, per-layer losses [K]); call
+        total.backward() as the reference does.  Mathematically the same gradients as building
+        the loss from forward()'s outputs with torch ops, without the K products A Z_k."""
+        K = self.layers
+        coeffs = [1.0] * K if coeffs is None else [float(c) for c in coeffs]
+        if len(coeffs) != K:
+            raise ValueError(f"dladmm: coeffs must have {K} entries")
+        if kind not in ("l1l1", "lasso"):
+            raise ValueError(f"dladmm: unknown loss kind {kind!r}")
+        denom = float(batch if batch is not None else x.shape[1])
+        if self._needs_grad():
+            if x.requires_grad:
+                raise RuntimeError("dladmm: gradients w.r.t. the input X are not supported")
+            return _DLADMMLossFunction.apply(self, x, coeffs, float(alpha), kind, denom,
+                                             *self.parameters())
+        r, per_layer = self.layer_objectives(x, alpha, kind)
+        per_layer = (per_layer * x.shape[1] / denom)
+        c = torch.as_tensor(coeffs, dtype=torch.float64, device=per_layer.device)
+        return (c * per_layer).sum().to(torch.float32), per_layer.to(torch.float32)
 
     # --- backward: map the C ABI's gradient tables onto the reference parameters ------------
     # GRAD_SLOTS: ParameterList name -> (kind, slots summed).  kind 'scalar' reads g_scalar,
@@ -168,9 +196,12 @@ class _DLADMMBase(nn.Module):
 
 class _DLADMMFunction(torch.autograd.Function):
     """The K-layer forward as one differentiable op: forward = dladmm_fwd_f32 with every layer
-    (and T) saved, backward = dladmm_bwd_f32 (the HIP reverse sweep).  Inputs: the module, X and
-    the module's parameters in `parameters()` order; outputs: stacked Z [K,n,B], E, L [K,m,B],
-    T [K+1,m,B]."""
+    (and T) saved, backward = dladmm_bwd_f32 (the HIP reverse sweep).
+
+    Inputs: the module, X, and the module's parameters in `parameters()` order.  Outputs: the
+    4K+1 per-layer tensors Z_0..Z_{K-1}, E_0.., L_0.., T_0..T_K as SEPARATE outputs (views of one
+    stacked buffer each), so autograd hands back one cotangent per layer -- or None for a layer
+    the loss never reads -- instead of accumulating K zero-filled stacks."""
 
     @staticmethod
     def forward(ctx, mod, x, *params):
@@ -183,22 +214,68 @@ class _DLADMMFunction(torch.autograd.Function):
         ctx.tables = tables
         ctx.W = W
         ctx.save_for_backward(x, r.Z, r.E, r.L, r.T)
+        ctx.set_materialize_grads(False)
+        K = mod.layers
+        outs = tuple(r.Z[k] for k in range(K)) + tuple(r.E[k] for k in range(K)) + \
+            tuple(r.L[k] for k in range(K)) + tuple(r.T[j] for j in range(K + 1))
         if not mod.RETURNS_T:
-            ctx.mark_non_differentiable(r.T)
-        return r.Z, r.E, r.L, r.T
+            ctx.mark_non_differentiable(*outs[3 * K:])
+        return outs
 
     @staticmethod
-    def backward(ctx, gZ, gE, gL, gT):
+    def backward(ctx, *g):
         x, Z, E, L, T = ctx.saved_tensors
         mod = ctx.mod
-        c = lambda g: None if g is None else g.contiguous()  # noqa: E731
+        K = mod.layers
         saved = ForwardResult(Z, E, L, T, None)
         res = dladmm_backward(mod.VARIANT, x, mod.A, ctx.W, mod.Z0, mod.E0, mod.L0, saved,
-                              c(gZ), c(gE), c(gL), c(gT) if mod.RETURNS_T else None,
+                              g[:K], g[K:2 * K], g[2 * K:3 * K],
+                              g[3 * K:] if mod.RETURNS_T else None,
                               tied=isinstance(mod.fc, nn.Linear), **ctx.tables)
         grads = mod._param_grads(res)
         names = [n for n, _ in mod.named_parameters()]
         return (None, None) + tuple(grads.get(n) for n in names)
+
+
+class _DLADMMLossFunction(torch.autograd.Function):
+    """The reference training objective fused into the op (SURVEY.md section 8 rows a11 + f1):
+        total = sum_k coeffs[k] * (alpha * sum(|Z_k|, 0).mean() + sum(|X - A Z_k|, 0).mean())
+    (main_syn_l1l1_scalar.py:283-296; LASSO main_syn_lasso_scalar.py:270-283 with
+    0.5*sum((X - A Z_k)^2, 0)), computed from the forward kernel's per-layer sums and
+    differentiated inside the backward kernels -- the K products A Z_k of the reference loss
+    never run.  Outputs: total (0-dim, differentiable) and the per-layer losses [K]
+    (non-differentiable, for logging as the reference prints loss[k])."""
+
+    @staticmethod
+    def forward(ctx, mod, x, coeffs, alpha, kind, denom, *params):
+        dev = mod.A.device
+        tables = mod._tables(dev)
+        W = [w.detach() for w in mod._weights()]
+        lk = {"l1l1": _lib.LOSS_L1L1, "lasso": _lib.LOSS_LASSO}[kind]
+        r = dladmm_forward(mod.VARIANT, x, mod.A, W, mod.Z0, mod.E0, mod.L0, keep_all=True,
+                           want_T=True, loss_kind=lk, **tables)
+        per_layer = (alpha * r.loss_sums[:, 0] + r.loss_sums[:, 1]) / denom  # fp64 [K]
+        c = torch.as_tensor(coeffs, dtype=torch.float64, device=dev)
+        total = (c * per_layer).sum().to(torch.float32)
+        ctx.mod, ctx.tables, ctx.W, ctx.lk = mod, tables, W, lk
+        # (cz_k, cf_k) per unit upstream gradient
+        ctx.base = torch.stack([c * alpha / denom, c / denom], 1).to(torch.float32)
+        ctx.save_for_backward(x, r.Z, r.E, r.L, r.T)
+        per_layer = per_layer.to(torch.float32)
+        ctx.mark_non_differentiable(per_layer)
+        return total, per_layer
+
+    @staticmethod
+    def backward(ctx, g_total, g_layers):
+        x, Z, E, L, T = ctx.saved_tensors
+        mod = ctx.mod
+        coef = (ctx.base * g_total).contiguous()  # device-side scale, no host sync
+        res = dladmm_backward(mod.VARIANT, x, mod.A, ctx.W, mod.Z0, mod.E0, mod.L0,
+                              ForwardResult(Z, E, L, T, None), loss_kind=ctx.lk, loss_coef=coef,
+                              tied=isinstance(mod.fc, nn.Linear), **ctx.tables)
+        grads = mod._param_grads(res)
+        names = [n for n, _ in mod.named_parameters()]
+        return (None,) * 6 + tuple(grads.get(n) for n in names)
 
 
 def _stack_scalar(pl) -> torch.Tensor:

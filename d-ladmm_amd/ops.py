@@ -171,18 +171,21 @@ class BackwardResult:
 
 def dladmm_backward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[torch.Tensor],
                     Z0: torch.Tensor, E0: torch.Tensor, L0: torch.Tensor, saved: ForwardResult,
-                    gZ: Optional[torch.Tensor] = None, gE: Optional[torch.Tensor] = None,
-                    gL: Optional[torch.Tensor] = None, gT: Optional[torch.Tensor] = None, *,
+                    gZ: Optional[Sequence] = None, gE: Optional[Sequence] = None,
+                    gL: Optional[Sequence] = None, gT: Optional[Sequence] = None, *,
+                    loss_kind: int = 0, loss_coef: Optional[torch.Tensor] = None,
                     scalar_params: Optional[torch.Tensor] = None,
                     row_params: Optional[torch.Tensor] = None,
                     beta1_elem: Sequence[torch.Tensor] = (),
                     beta2_elem: Sequence[torch.Tensor] = (),
                     tied: bool = False) -> BackwardResult:
-    """Gradients of sum_k <gZ_k,Z_k> + <gE_k,E_k> + <gL_k,L_k> + sum_j <gT_j,T_j> w.r.t. the
-    parameters of the forward that produced `saved` (a keep_all ForwardResult with T), via
-    `dladmm_bwd_f32` (include/dladmm.h).  Cotangents are stacked like the outputs ([K|K+1, rows,
-    B]); None = zero.  This is the backward of the reference's `total_loss.backward()` through
-    DLADMMNet.forward (main_syn_l1l1_scalar.py:298)."""
+    """Gradients of sum_k <gZ_k,Z_k> + <gE_k,E_k> + <gL_k,L_k> + sum_j <gT_j,T_j> (+ the fused
+    training objective sum_k cz_k sum|Z_k| + cf_k fit_k when loss_kind, loss_coef = device
+    (K, 2) fp32 (cz_k, cf_k)) w.r.t. the parameters of the forward that produced `saved` (a
+    keep_all ForwardResult with T), via `dladmm_bwd_f32` (include/dladmm.h).  Cotangents are
+    per-layer sequences of (rows, B) tensors (None entries / None = zero).  This is the backward
+    of the reference's `total_loss.backward()` through DLADMMNet.forward
+    (main_syn_l1l1_scalar.py:298)."""
     L = _lib.lib()
     if saved.T is None or saved.Z.shape[0] != len(W):
         raise ValueError("dladmm: backward needs the keep_all forward outputs including T")
@@ -193,16 +196,32 @@ def dladmm_backward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[
     d = _lib.BwdDesc()
     keep = _fill_fwd_desc(d.fwd, variant, X, A, W, Z0, E0, L0, scalar_params, row_params,
                           beta1_elem, beta2_elem, True, 0, saved)
-    shapes = {"gZ": (K, n, B), "gE": (K, m, B), "gL": (K, m, B), "gT": (K + 1, m, B)}
-    for nm, g in (("gZ", gZ), ("gE", gE), ("gL", gL), ("gT", gT)):
-        if g is None:
+    counts = {"gZ": (K, n), "gE": (K, m), "gL": (K, m), "gT": (K + 1, m)}
+    for nm, seq in (("gZ", gZ), ("gE", gE), ("gL", gL), ("gT", gT)):
+        if seq is None or all(g is None for g in seq):
             continue
-        if tuple(g.shape) != shapes[nm] or not g.is_contiguous() or g.dtype != torch.float32 \
-                or g.device != dev:
-            raise ValueError(f"dladmm: {nm} must be a contiguous fp32 {shapes[nm]} device tensor")
-        setattr(d, nm, g.data_ptr())
-        keep.append(g)
+        cnt, rows = counts[nm]
+        if len(seq) != cnt:
+            raise ValueError(f"dladmm: {nm} must have {cnt} entries")
+        ptrs = []
+        for g in seq:
+            if g is None:
+                ptrs.append(None)
+                continue
+            if tuple(g.shape) != (rows, B) or g.dtype != torch.float32 or g.device != dev:
+                raise ValueError(f"dladmm: {nm} entries must be fp32 ({rows}, {B}) device tensors")
+            g = g.contiguous()
+            keep.append(g)
+            ptrs.append(g.data_ptr())
+        arr = _lib.ptr_array(ptrs)
+        keep.append(arr)
+        setattr(d, nm, ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)))
     d.ld_g = B
+    if loss_kind:
+        if loss_coef is None or tuple(loss_coef.shape) != (K, 2) or loss_coef.dtype != \
+                torch.float32 or loss_coef.device != dev or not loss_coef.is_contiguous():
+            raise ValueError("dladmm: loss_coef must be a contiguous fp32 (K, 2) device tensor")
+        d.loss_kind, d.loss_coef = int(loss_kind), loss_coef.data_ptr()
     gWo = torch.empty((1 if tied else K, n, m), device=dev, dtype=torch.float32)
     d.gW, d.ld_gw = gWo.data_ptr(), m
     g_scalar = g_row = None

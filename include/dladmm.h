@@ -161,17 +161,28 @@ int dladmm_fwd_f32(const dladmm_fwd_desc* d, void* stream);
  *
  * `fwd` must describe the forward call whose outputs are differentiated, run with keep_all = 1
  * and T != NULL (all K layers of Z/E/L and T[0..K] saved; V1-V3 keep T internally).  Its
- * workspace fields are ignored.  Upstream cotangents may be NULL (= zero) and share one row
- * stride ld_g; gT has K+1 layers (gT_0 reaches no parameter and is never read).
+ * workspace fields are ignored.
  */
 typedef struct dladmm_bwd_desc {
   dladmm_fwd_desc fwd;
 
-  const float* gZ;  /* [K][n][ld_g] or NULL */
-  const float* gE;  /* [K][m][ld_g] or NULL */
-  const float* gL;  /* [K][m][ld_g] or NULL */
-  const float* gT;  /* [K+1][m][ld_g] or NULL */
+  /* upstream cotangents: HOST arrays of device pointers, one per layer (gT: K+1), each a
+     (rows x ld_g) matrix; a NULL array or a NULL entry is a zero cotangent */
+  const float* const* gZ;  /* K entries, n x ld_g */
+  const float* const* gE;  /* K entries, m x ld_g */
+  const float* const* gL;  /* K entries, m x ld_g */
+  const float* const* gT;  /* K+1 entries, m x ld_g (entry 0 reaches no parameter) */
   int64_t ld_g;
+
+  /* fused training objective (optional): adds the gradient of
+       sum_k  cz_k * sum|Z_k|  +  cf_k * fit_k,   fit = sum|X - A Z_k| (L1L1) or
+                                                     0.5 * sum (X - A Z_k)^2 (LASSO)
+     -- the reference training loss (main_syn_l1l1_scalar.py:283-296, lasso :270-283) with
+     cz_k = decay_k * alpha / B and cf_k = decay_k / B -- without materialising A Z_k.
+     loss_kind = DLADMM_LOSS_NONE disables it; loss_coef: DEVICE array [K][2] = (cz_k, cf_k). */
+  int32_t loss_kind;
+  int32_t pad0;
+  const float* loss_coef;
 
   /* outputs (device) */
   float* gW; int64_t ld_gw;   /* [K][n][ld_gw] (V5 tied: ONE n x m block, summed over layers) */

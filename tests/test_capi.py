@@ -79,10 +79,11 @@ def _bdesc(dl, **kw):
     fake = 1 << 40
     b.gW, b.ld_gw = fake, 256
     b.g_scalar = fake
-    b.gZ, b.ld_g = fake, 1000
+    gz = dl._lib.ptr_array([fake] * 15)
+    b.gZ, b.ld_g = ctypes.cast(gz, ctypes.POINTER(ctypes.c_void_p)), 1000
     for k, v in kw.items():
         setattr(b, k, v)
-    return b, keep
+    return b, (keep, gz)
 
 
 def test_backward_workspace_and_validation(dl):
@@ -93,7 +94,7 @@ def test_backward_workspace_and_validation(dl):
     assert ws >= (5 * 256 + 512 + 256) * 1008 * 4 + 4 * 256 * 512 * 4
     assert ws % 256 == 0
     for field, value, code in (("gW", None, -5), ("g_scalar", None, -5), ("ld_g", 10, -3),
-                               ("ld_gw", 100, -3)):
+                               ("ld_gw", 100, -3), ("loss_kind", 1, -5), ("loss_kind", 5, -7)):
         bb, _k2 = _bdesc(dl, **{field: value})
         assert L.dladmm_bwd_workspace_bytes(ctypes.byref(bb)) == 0
         assert L.dladmm_bwd_f32(ctypes.byref(bb), None) == code, field

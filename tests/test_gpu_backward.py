@@ -175,3 +175,45 @@ def test_adam_training_step(dl):
     for k, p in net.named_parameters():
         np.testing.assert_allclose(p.detach().cpu().numpy(), ref[k].detach().numpy(),
                                    rtol=0, atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("name", ["grad_v4_med", "grad_v6_med", "grad_v1_small", "grad_v2_ragged",
+                                  "grad_v5_small", "grad_v3_small"])
+def test_fused_training_loss(name, dl):
+    """net.training_loss (objective reduced in the forward kernel, its gradient injected in the
+    backward kernels) == the reference loss built from the outputs with torch ops: same value,
+    same gradients (against the oracle's reverse sweep of the same loss)."""
+    from oracle import dladmm_oracle as fwd
+    from oracle import dladmm_oracle_grad as og
+    g, meta = load_golden(name)
+    d = meta["defn"]
+    kind = meta["gdef"]["loss"]
+    K = d["K"]
+    inp, sd = P.build_problem(d)
+    X = torch.from_numpy(inp["X"]).cuda()
+    A = torch.from_numpy(inp["A"]).cuda()
+    coeffs = P.loss_coeffs(K)
+    net = make_train_net(dl, d["variant"], inp, sd, K)
+    total, per_layer = net.training_loss(X, P.GRAD_ALPHA, coeffs, kind)
+    total.backward()
+    net2 = make_train_net(dl, d["variant"], inp, sd, K)
+    ref_total = total_loss(net2(X), X, A, {"Gz": np.zeros((K, 1, 1), np.float32),
+                                          "Ge": np.zeros((K, 1, 1), np.float32),
+                                          "Gl": np.zeros((K, 1, 1), np.float32)}, kind, K)
+    ref_total.backward()
+    np.testing.assert_allclose(float(total), float(ref_total), rtol=1e-5)
+    assert per_layer.shape == (K,)
+    res = {}
+    for dt in (np.float32, np.float64):
+        o = fwd.forward(d["variant"], inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd, K,
+                        dtype=dt)
+        gz = og.train_loss_grads(o["Z"], inp["X"], inp["A"], P.GRAD_ALPHA, coeffs, kind, dtype=dt)
+        res[dt] = og.vjp(d["variant"], inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd,
+                         K, gZ=gz, dtype=dt)
+    p2 = dict(net2.named_parameters())
+    for key, p in net.named_parameters():
+        gap = nrel(res[np.float32][key], res[np.float64][key])
+        e = nrel(p.grad.cpu().numpy(), res[np.float64][key])
+        assert e <= max(GTOL, 3.0 * gap), (key, e, gap)
+        e2 = nrel(p.grad.cpu().numpy(), p2[key].grad.cpu().numpy())
+        assert e2 <= max(GTOL, 3.0 * gap), (key, e2, gap)

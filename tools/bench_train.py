@@ -1,0 +1,110 @@
+"""Training-step benchmark: one reference training step
+(main_syn_l1l1_scalar.py:269-299 -- zero_grad, forward, per-layer L1L1 loss with decay, backward,
+Adam step) of the V4 model on one MI355X, with the forward and backward of the drop-in module
+timed separately by HIP events on the current stream.
+
+    python tools/bench_train.py [--batch B] [--steps K] [--warmup W] [--m 256 --n 512 --layers 15]
+
+Prints one JSON line.  FLOP model per sample: forward (4K+2)mn; backward 10mn per layer (BK1 A Z,
+BK2 A^T gP + M Var, BK3 M^T gU, weight gradient gU Var^T); the loss's own torch.mm(A, Z_k) and its
+backward (4mn per layer, hipBLASLt) are counted separately.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402  (synthetic inputs)
+
+PEAK = 157.3e12
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--m", type=int, default=256)
+    ap.add_argument("--n", type=int, default=512)
+    ap.add_argument("--layers", type=int, default=15)
+    ap.add_argument("--alpha", type=float, default=0.001)
+    ap.add_argument("--fused-loss", action="store_true",
+                    help="net.training_loss (objective fused into the kernels) instead of the "
+                         "reference's torch-op loss over the returned Z_k")
+    a = ap.parse_args()
+    dl = importlib.import_module("d-ladmm_amd")
+    dev = torch.device("cuda", 0)
+    m, n, K, B = a.m, a.n, a.layers, a.batch
+    A, X, Z0, E0, L0 = bench.synth(m, n, B, 0, dev)
+    net = dl.DLADMMNetScalar(m=m, n=0, d=n, batch_size=B, A=A, Z0=Z0, E0=E0, L0=L0, layers=K)
+    opt = torch.optim.Adam(net.parameters(), lr=0.005)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+
+    def step(timed):
+        opt.zero_grad()
+        if timed:
+            ev[0].record()
+        coeffs = [0.6 if k < K - 1 else 1.0 for k in range(K)]
+        if a.fused_loss:
+            tot, _ = net.training_loss(X, a.alpha, coeffs, "l1l1")
+            if timed:
+                ev[1].record()
+                ev[2].record()
+        else:
+            Z, E, L, T = net(X)
+            if timed:
+                ev[1].record()
+            tot = 0
+            for k in range(K):  # main_syn_l1l1_scalar.py:283-296
+                lk = a.alpha * torch.sum(torch.abs(Z[k]), dim=0).mean() + \
+                    torch.sum(torch.abs(X - torch.mm(A, Z[k])), dim=0).mean()
+                tot = tot + lk * coeffs[k]
+            if timed:
+                ev[2].record()
+        tot.backward()
+        if timed:
+            ev[3].record()
+        opt.step()
+        return tot
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    fw, lo, bw, tot_t = [], [], [], []
+    for _ in range(a.steps):
+        t0 = time.perf_counter()
+        loss = step(True)
+        torch.cuda.synchronize()
+        tot_t.append(time.perf_counter() - t0)
+        fw.append(ev[0].elapsed_time(ev[1]))
+        lo.append(ev[1].elapsed_time(ev[2]))
+        bw.append(ev[2].elapsed_time(ev[3]))
+    med = lambda v: float(np.median(v))  # noqa: E731
+    flop_f = (4 * K + 2) * m * n * B
+    flop_b = 10 * K * m * n * B
+    res = {
+        "metric": "training steps/s (V4 forward + L1L1 loss + backward + Adam)",
+        "loss_path": "fused (net.training_loss)" if a.fused_loss else "torch ops on Z_k",
+        "batch": B, "m": m, "n": n, "layers": K,
+        "step_ms": med(tot_t) * 1e3,
+        "samples_per_s": B / med(tot_t),
+        "forward_ms": med(fw), "loss_ms": med(lo), "backward_ms": med(bw),
+        "forward_tflops": flop_f / (med(fw) * 1e-3) / 1e12,
+        "backward_tflops": flop_b / (med(bw) * 1e-3) / 1e12,
+        "backward_frac_fp32_mfma": flop_b / (med(bw) * 1e-3) / PEAK,
+        "loss": float(loss.detach()),
+    }
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
