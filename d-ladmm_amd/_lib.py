@@ -63,7 +63,7 @@ class BwdDesc(ctypes.Structure):
         ("fwd", FwdDesc),
         ("gZ", ctypes.POINTER(_fp)), ("gE", ctypes.POINTER(_fp)), ("gL", ctypes.POINTER(_fp)),
         ("gT", ctypes.POINTER(_fp)), ("ld_g", _i64),
-        ("loss_kind", _i32), ("pad0", _i32), ("loss_coef", _fp),
+        ("loss_kind", _i32), ("gw_sum", _i32), ("loss_coef", _fp),
         ("gW", _fp), ("ld_gw", _i64),
         ("g_scalar", _fp), ("g_row", _fp),
         ("g_beta1_elem", ctypes.POINTER(_fp)), ("g_beta2_elem", ctypes.POINTER(_fp)),

@@ -402,7 +402,7 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
   const int64_t B = f.batch, ldo = f.ld_out, ldw = p.Bpad;
   const int v = f.variant;
   const bool has_s1 = v >= DLADMM_V4_SCALAR;
-  const bool tied = v == DLADMM_V5_TIED;
+  const bool tied = d->gw_sum != 0;
   const bool ufused = p.fwd.path == 1;
   const bool rowk = v == DLADMM_V2_LTHETA || v == DLADMM_V3_FULL;
   float* A1 = (float*)(ws + p.off_a1);

@@ -109,24 +109,40 @@ class _DLADMMBase(nn.Module):
                 self.Z0, self.E0, self.L0, keep_all=keep_all, want_T=self.RETURNS_T,
                 loss_kind=loss_kind, kernel_events=kernel_events, **self._tables(dev))
 
-    def forward(self, x):
-        K = self.layers
+    def _forward_layers(self, x, nl: int):
+        """Run the first `nl` layers; lists Z, E, L (nl entries) and T (nl + 1), differentiable
+        when autograd records and parameters require grad."""
         if self._needs_grad():
             if x.requires_grad:
                 raise RuntimeError("dladmm: gradients w.r.t. the input X are not supported (the "
                                    "reference trains the parameters only)")
-            outs = _DLADMMFunction.apply(self, x, *self.parameters())
-            Z, E, L = list(outs[:K]), list(outs[K:2 * K]), list(outs[2 * K:3 * K])
-            T = list(outs[3 * K:])
-        else:
-            r = self.run(x)
-            Z = [r.Z[k] for k in range(K)]
-            E = [r.E[k] for k in range(K)]
-            L = [r.L[k] for k in range(K)]
-            T = [r.T[k] for k in range(K + 1)] if self.RETURNS_T else None
+            outs = _DLADMMFunction.apply(self, x, nl, *self.parameters())
+            return (list(outs[:nl]), list(outs[nl:2 * nl]), list(outs[2 * nl:3 * nl]),
+                    list(outs[3 * nl:]))
+        with torch.no_grad():
+            tables = _slice_tables(self._tables(self.A.device), nl)
+            r = dladmm_forward(self.VARIANT, x, self.A, [w.detach() for w in self._weights()[:nl]],
+                               self.Z0, self.E0, self.L0, keep_all=True, want_T=self.RETURNS_T,
+                               **tables)
+        T = [r.T[j] for j in range(nl + 1)] if r.T is not None else None
+        return ([r.Z[k] for k in range(nl)], [r.E[k] for k in range(nl)],
+                [r.L[k] for k in range(nl)], T)
+
+    def forward(self, x):
+        Z, E, L, T = self._forward_layers(x, self.layers)
         if self.RETURNS_T:
             return Z, E, L, T
         return Z, E, L
+
+    def layer_objectives(self, x, alpha: float, kind: str = "l1l1", kernel_events=None):
+        """Forward + the per-layer objective of the reference training loop, fused in-kernel:
+        l1l1  alpha*sum(|Z_k|,0).mean() + sum(|X - A Z_k|,0).mean()   main_syn_l1l1_scalar.py:290-294
+        lasso alpha*sum(|Z_k|,0).mean() + 0.5*sum((X-A Z_k)^2,0).mean() main_syn_lasso_scalar.py:276-281
+        Returns (ForwardResult, fp64 tensor [K])."""
+        lk = {"l1l1": _lib.LOSS_L1L1, "lasso": _lib.LOSS_LASSO}[kind]
+        r = self.run(x, loss_kind=lk, kernel_events=kernel_events)
+        obj = (alpha * r.loss_sums[:, 0] + r.loss_sums[:, 1]) / x.shape[1]
+        return r, obj
 
     def training_loss(self, x, alpha: float, coeffs=None, kind: str = "l1l1",
                       batch: Optional[int] = None):
@@ -160,11 +176,16 @@ class _DLADMMBase(nn.Module):
     # 'row' reads g_row (theta_z rows = d, else m), 'elem1'/'elem2' the V1 per-sample betas.
     GRAD_SLOTS: dict = {}
 
-    def _param_grads(self, res) -> dict:
-        K = self.layers
+    def _fc_key(self, k: int) -> str:
+        """state_dict key of the weight layer k uses."""
+        return "fc.weight" if self._shared_weight() else f"fc.{k}.weight"
+
+    def _param_grads(self, res, nl: int) -> dict:
+        """Gradients by state_dict key from a BackwardResult of the first `nl` layers (layers
+        >= nl were not run: their parameters get no gradient, as in the reference)."""
         out = {}
         for name, (kind, slots) in self.GRAD_SLOTS.items():
-            for k in range(K):
+            for k in range(nl):
                 key = f"{name}.{k}"
                 if kind == "scalar":
                     g = sum(res.g_scalar[k, s] for s in slots).reshape(1, 1)
@@ -176,22 +197,21 @@ class _DLADMMBase(nn.Module):
                 else:
                     g = res.g_beta2[k]
                 out[key] = g.to(torch.float32)
-        if isinstance(self.fc, nn.Linear):
-            out["fc.weight"] = res.gW[0]
+        if self._shared_weight():
+            out[self._fc_key(0)] = res.gW[0]
         else:
-            for k in range(K):
-                out[f"fc.{k}.weight"] = res.gW[k]
+            for k in range(nl):
+                key = self._fc_key(k)
+                out[key] = res.gW[k] if key not in out else out[key] + res.gW[k]
         return out
 
-    def layer_objectives(self, x, alpha: float, kind: str = "l1l1", kernel_events=None):
-        """Forward + the per-layer objective of the reference training loop, fused in-kernel:
-        l1l1  alpha*sum(|Z_k|,0).mean() + sum(|X - A Z_k|,0).mean()   main_syn_l1l1_scalar.py:290-294
-        lasso alpha*sum(|Z_k|,0).mean() + 0.5*sum((X-A Z_k)^2,0).mean() main_syn_lasso_scalar.py:276-281
-        Returns (ForwardResult, fp64 tensor [K])."""
-        lk = {"l1l1": _lib.LOSS_L1L1, "lasso": _lib.LOSS_LASSO}[kind]
-        r = self.run(x, loss_kind=lk, kernel_events=kernel_events)
-        obj = (alpha * r.loss_sums[:, 0] + r.loss_sums[:, 1]) / x.shape[1]
-        return r, obj
+    def _shared_weight(self) -> bool:
+        return isinstance(self.fc, nn.Linear)
+
+
+def _slice_tables(tables: dict, nl: int) -> dict:
+    """Per-layer parameter tables of the first nl layers."""
+    return {k: (v[:nl] if v is not None else None) for k, v in tables.items()}
 
 
 class _DLADMMFunction(torch.autograd.Function):
@@ -204,18 +224,19 @@ class _DLADMMFunction(torch.autograd.Function):
     the loss never reads -- instead of accumulating K zero-filled stacks."""
 
     @staticmethod
-    def forward(ctx, mod, x, *params):
+    def forward(ctx, mod, x, nl, *params):
         dev = mod.A.device
-        tables = mod._tables(dev)
-        W = [w.detach() for w in mod._weights()]
+        tables = _slice_tables(mod._tables(dev), nl)
+        W = [w.detach() for w in mod._weights()[:nl]]
         r = dladmm_forward(mod.VARIANT, x, mod.A, W, mod.Z0, mod.E0, mod.L0, keep_all=True,
                            want_T=True, **tables)
         ctx.mod = mod
+        ctx.nl = nl
         ctx.tables = tables
         ctx.W = W
         ctx.save_for_backward(x, r.Z, r.E, r.L, r.T)
         ctx.set_materialize_grads(False)
-        K = mod.layers
+        K = nl
         outs = tuple(r.Z[k] for k in range(K)) + tuple(r.E[k] for k in range(K)) + \
             tuple(r.L[k] for k in range(K)) + tuple(r.T[j] for j in range(K + 1))
         if not mod.RETURNS_T:
@@ -226,15 +247,15 @@ class _DLADMMFunction(torch.autograd.Function):
     def backward(ctx, *g):
         x, Z, E, L, T = ctx.saved_tensors
         mod = ctx.mod
-        K = mod.layers
+        K = ctx.nl
         saved = ForwardResult(Z, E, L, T, None)
         res = dladmm_backward(mod.VARIANT, x, mod.A, ctx.W, mod.Z0, mod.E0, mod.L0, saved,
                               g[:K], g[K:2 * K], g[2 * K:3 * K],
                               g[3 * K:] if mod.RETURNS_T else None,
-                              tied=isinstance(mod.fc, nn.Linear), **ctx.tables)
-        grads = mod._param_grads(res)
+                              tied=mod._shared_weight(), **ctx.tables)
+        grads = mod._param_grads(res, K)
         names = [n for n, _ in mod.named_parameters()]
-        return (None, None) + tuple(grads.get(n) for n in names)
+        return (None, None, None) + tuple(grads.get(n) for n in names)
 
 
 class _DLADMMLossFunction(torch.autograd.Function):
@@ -272,8 +293,8 @@ class _DLADMMLossFunction(torch.autograd.Function):
         coef = (ctx.base * g_total).contiguous()  # device-side scale, no host sync
         res = dladmm_backward(mod.VARIANT, x, mod.A, ctx.W, mod.Z0, mod.E0, mod.L0,
                               ForwardResult(Z, E, L, T, None), loss_kind=ctx.lk, loss_coef=coef,
-                              tied=isinstance(mod.fc, nn.Linear), **ctx.tables)
-        grads = mod._param_grads(res)
+                              tied=mod._shared_weight(), **ctx.tables)
+        grads = mod._param_grads(res, mod.layers)
         names = [n for n, _ in mod.named_parameters()]
         return (None,) * 6 + tuple(grads.get(n) for n in names)
 
@@ -463,9 +484,93 @@ class DLADMMNetLasso(DLADMMNetScalar):
             thz=_stack_scalar(self.active_para), s1=1.0))
 
 
+class DLADMMNetNewS(DLADMMNetScalar):
+    """V7, main_syn_scalar_newS_layerwise.py:34-114: the "new S" layer-wise schedule.
+
+    Its recurrence is V4's with the E/L-step of layer k-1 moved in front of the Z-step of layer
+    k (:82-92): newS Z[k] = V4 Z_k, newS E[k] = V4 E_{k-1} (E[0] = E0), newS L[k] = V4 L_{k-1}
+    (L[0] = L0), with the same parameters and the same floating-point operations.  So it runs
+    as the V4 op over min(K, layers) layers (a schedule flag on the same kernel, SURVEY.md
+    section 8 row f4) and re-indexes the outputs; the last layer's E/L-step, which newS never
+    uses, is computed and discarded.  forward(x, K) returns (Z, E, L), as the reference."""
+    NAME = "DLADMMNet_scalar_newS_layerwise"
+    THZ0 = 0.1   # main_syn_scalar_newS_layerwise.py:63-64
+    THE0 = 0.1
+
+    def _register_params(self):
+        # main_syn_scalar_newS_layerwise.py:51-65
+        for nm in ("beta1", "beta2", "beta3", "ss2"):
+            self._plist(nm, (1, 1), 1.0)
+        self._plist("active_para", (1, 1), self.THZ0)
+        self._plist("active_para1", (1, 1), self.THE0)
+        self.fc = nn.ModuleList([nn.Linear(self.m, self.d, bias=False) for _ in range(self.layers)])
+
+    def forward(self, x, K=None):
+        nl = self.layers if K is None else min(int(K), self.layers)  # :78
+        Z, E, L, _T = self._forward_layers(x, nl)
+        return Z, [self.E0] + E[: nl - 1], [self.L0] + L[: nl - 1]
+
+
+class DLADMMNetTiedNewS(DLADMMNetNewS):
+    """main_syn_scalar_tied_newS_layerwise.py:34-112: newS schedule, one shared fc scaled by
+    ss1[k] (the V5 kernel path)."""
+    VARIANT = _lib.V5_TIED
+    NAME = "DLADMMNet_scalar_tied_newS_layerwise"
+    THZ0 = 0.01
+    THE0 = 0.01
+    GRAD_SLOTS = dict(DLADMMNetScalar.GRAD_SLOTS, ss1=("scalar", (_lib.P_S1,)))
+
+    def _register_params(self):
+        # :51-66 (registration order = state_dict order)
+        for nm in ("beta1", "beta2", "beta3", "ss1", "ss2"):
+            self._plist(nm, (1, 1), 1.0)
+        self._plist("active_para", (1, 1), self.THZ0)
+        self._plist("active_para1", (1, 1), self.THE0)
+        self.fc = nn.Linear(self.m, self.d, bias=False)
+
+    def _weights(self):
+        return [self.fc.weight] * self.layers
+
+    def _tables(self, dev):
+        return DLADMMNetScalarTied._tables(self, dev)
+
+
+class DLADMMNetPTiedNewS(DLADMMNetTiedNewS):
+    """main_syn_scalar_ptied_newS_layerwise.py:34-121: newS schedule with partial weight tying --
+    layers // interval weights, layer k uses fc[k // interval] scaled by ss1[k] (:92).
+    Constructor adds `interval` (:36)."""
+    NAME = "DLADMMNet_scalar_ptied_newS_layerwise"
+
+    def __init__(self, m, n, d, batch_size, A, Z0, E0, L0, layers, interval):
+        self.interval = interval
+        super().__init__(m, n, d, batch_size, A, Z0, E0, L0, layers)
+
+    def _register_params(self):
+        # :51-71: fc (layers // interval Linears) is registered after the ParameterLists
+        for nm in ("beta1", "beta2", "beta3", "ss1", "ss2"):
+            self._plist(nm, (1, 1), 1.0)
+        self._plist("active_para", (1, 1), self.THZ0)
+        self._plist("active_para1", (1, 1), self.THE0)
+        self.fc = nn.ModuleList([nn.Linear(self.m, self.d, bias=False)
+                                 for _ in range(self.layers // self.interval)])
+
+    def _weights(self):
+        return [self.fc[k // self.interval].weight for k in range(self.layers)]
+
+    def _fc_key(self, k):
+        return f"fc.{k // self.interval}.weight"
+
+    def _shared_weight(self):
+        return False
+
+    def name(self):
+        return "DLADMMNet_scalar_ptied{}_newS_layerwise".format(self.interval)  # :124
+
+
 VARIANTS = {
     "v1": DLADMMNet, "v2": DLADMMNetLTheta, "v3": DLADMMNetFull,
     "v4": DLADMMNetScalar, "v5": DLADMMNetScalarTied, "v6": DLADMMNetLasso,
+    "v7": DLADMMNetNewS, "v7t": DLADMMNetTiedNewS, "v7p": DLADMMNetPTiedNewS,
 }
 
 

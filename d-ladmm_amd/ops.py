@@ -224,6 +224,7 @@ def dladmm_backward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[
         d.loss_kind, d.loss_coef = int(loss_kind), loss_coef.data_ptr()
     gWo = torch.empty((1 if tied else K, n, m), device=dev, dtype=torch.float32)
     d.gW, d.ld_gw = gWo.data_ptr(), m
+    d.gw_sum = int(bool(tied))
     g_scalar = g_row = None
     g1, g2 = [], []
     if variant >= _lib.V4_SCALAR:

@@ -181,11 +181,12 @@ typedef struct dladmm_bwd_desc {
      cz_k = decay_k * alpha / B and cf_k = decay_k / B -- without materialising A Z_k.
      loss_kind = DLADMM_LOSS_NONE disables it; loss_coef: DEVICE array [K][2] = (cz_k, cf_k). */
   int32_t loss_kind;
-  int32_t pad0;
+  int32_t gw_sum;             /* 1: every layer shares ONE weight (V5 tied, tied newS): gW is one
+                                 n x m block holding the sum over layers; 0: gW[k] per layer */
   const float* loss_coef;
 
   /* outputs (device) */
-  float* gW; int64_t ld_gw;   /* [K][n][ld_gw] (V5 tied: ONE n x m block, summed over layers) */
+  float* gW; int64_t ld_gw;   /* [K][n][ld_gw], or [1][n][ld_gw] when gw_sum */
   double* g_scalar;           /* V4-V6: [K][DLADMM_NSCALAR] per-slot grads (slots the variant
                                  does not use are 0; V1: unused) */
   double* g_row;              /* V2/V3: [K][DLADMM_NSCALAR][fwd.row_stride] per-row grads */

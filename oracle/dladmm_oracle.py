@@ -30,7 +30,8 @@ V1_THETA_Z = 0.025
 V1_THETA_E = 0.06
 
 # which reference variants return T (main_syn_l1l1_scalar.py:127) and which return (Z, E, L)
-RETURNS_T = {"v1": False, "v2": False, "v3": False, "v4": True, "v5": True, "v6": True}
+RETURNS_T = {"v1": False, "v2": False, "v3": False, "v4": True, "v5": True, "v6": True,
+             "v7": False, "v7t": False, "v7p": False}
 
 
 def self_active(x, theta):
@@ -43,11 +44,45 @@ def _fc(W, Var):
     return (Var.T @ W.T).T
 
 
+def forward_news(variant, X, A, Z0, E0, L0, p, K, dtype):
+    """The "new S" layer-wise schedule, forward(x, K) of main_syn_scalar_newS_layerwise.py:76-99
+    (v7), main_syn_scalar_tied_newS_layerwise.py:76-99 (v7t, shared fc * ss1[k]) and
+    main_syn_scalar_ptied_newS_layerwise.py:84-115 (v7p, fc[k // interval] * ss1[k])."""
+    nfc = sum(1 for k in p if k.startswith("fc.") and k.endswith(".weight") and k != "fc.weight")
+    total = sum(1 for k in p if k.startswith("beta1."))  # the model's layer count
+    interval = max(total // nfc, 1) if variant == "v7p" else 1
+
+    def fcW(k, Var):
+        if variant == "v7":
+            return _fc(p[f"fc.{k}.weight"], Var)
+        W = p["fc.weight"] if variant == "v7t" else p[f"fc.{k // interval}.weight"]
+        return p[f"ss1.{k}"] * _fc(W, Var)
+
+    Z, E, L = [], [], []
+    for k in range(K):
+        if k == 0:
+            E.append(E0)
+            L.append(L0)
+            Tn = A @ Z0 + E0 - X
+            Varn = L0 + p[f"beta1.{k}"] * Tn
+            Z.append(self_active(Z0 - fcW(k, Varn), p[f"active_para.{k}"]))
+        else:
+            VVar = L[-1] + p[f"beta2.{k-1}"] * (A @ Z[-1] + E[-1] - X)
+            E.append(self_active(E[-1] - p[f"ss2.{k-1}"] * VVar, p[f"active_para1.{k-1}"]))
+            Tn = A @ Z[-1] + E[-1] - X
+            L.append(L[-1] + p[f"beta3.{k-1}"] * Tn)
+            Varn = L[-1] + p[f"beta1.{k}"] * Tn
+            Z.append(self_active(Z[-1] - fcW(k, Varn), p[f"active_para.{k}"]))
+    return dict(Z=Z, E=E, L=L)
+
+
 def forward(variant, X, A, Z0, E0, L0, state_dict, layers, dtype=np.float32):
-    """Run the reference forward of `variant` ('v1'..'v6'); returns dict(Z, E, L[, T]) of lists."""
+    """Run the reference forward of `variant` ('v1'..'v7p'); returns dict(Z, E, L[, T]) of lists."""
     c = lambda a: np.asarray(a, dtype=dtype)  # noqa: E731
     X, A, Z0, E0, L0 = c(X), c(A), c(Z0), c(E0), c(L0)
     p = {k: c(v) for k, v in state_dict.items()}
+    if variant in ("v7", "v7t", "v7p"):
+        return forward_news(variant, X, A, Z0, E0, L0, p, layers, dtype)
     T, Z, E, L = [], [], [], []
     for k in range(layers):
         if variant in ("v1", "v2"):

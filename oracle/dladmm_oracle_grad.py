@@ -34,9 +34,19 @@ from .dladmm_oracle import V1_THETA_E, V1_THETA_Z, self_active
 EM_V1, EM_VVAR, EM_LASSO = 0, 1, 2
 
 
-def _layer_params(variant, p, k, dtype):
+def _layer_params(variant, p, k, dtype, interval=1):
     """Per-layer parameters in the normalised form of the fused kernel (include/dladmm.h slots),
-    plus, per slot, the state_dict key it came from (None = not a parameter)."""
+    plus, per slot, the state_dict key it came from (None = not a parameter).  The newS
+    schedules (v7, v7t, v7p) have V4's / V5's per-layer algebra (see vjp)."""
+    if variant == "v7":
+        variant = "v4"
+    if variant == "v7t":
+        variant = "v5"
+    if variant == "v7p":
+        q, keys = _layer_params("v5", dict(p, **{"fc.weight": p[f"fc.{k // interval}.weight"]}),
+                                k, dtype)
+        keys["W"] = f"fc.{k // interval}.weight"
+        return q, keys
     if variant in ("v1", "v2"):
         # main_lena.py:84-89: b1 serves Var and L (beta1), b2 the E-step; V1 thetas are constants
         q = dict(b1=p[f"beta1.{k}"], b2=p[f"beta2.{k}"], b3=p[f"beta1.{k}"],
@@ -97,11 +107,21 @@ def vjp(variant, X, A, Z0, E0, L0, state_dict, layers, gZ=None, gE=None, gL=None
     X, A, Z0, E0, L0 = c(X), c(A), c(Z0), c(E0), c(L0)
     p = {k: c(v) for k, v in state_dict.items()}
     K = layers
+    interval = 1
+    if variant in ("v7", "v7t", "v7p"):
+        # newS (main_syn_scalar_newS_layerwise.py:76-99): Z[k] = V4 Z_k, E[k] = V4 E_{k-1}
+        # (E[0] = E0), L[k] = V4 L_{k-1}; the V4 sweep with the E/L cotangents shifted by one
+        # layer (E[0], L[0] are inputs; V4's last E_{K-1}, L_{K-1}, T_K are never outputs)
+        shift = lambda seq: None if seq is None else [c(g) for g in seq[1:]] + [None]  # noqa
+        gE, gL, gT = shift(gE), shift(gL), None
+        if variant == "v7p":
+            nfc = sum(1 for k in p if k.startswith("fc.") and k.endswith(".weight"))
+            interval = max(sum(1 for k in p if k.startswith("beta1.")) // nfc, 1)
     # ---- forward, keeping every intermediate the reverse sweep needs
     Zs, Es, Ls, Ts, Vs, Us, Ps, Qs, Eh = [Z0], [E0], [L0], [A @ Z0 + E0 - X], [], [], [], [], []
     prm = []
     for k in range(K):
-        q, keys = _layer_params(variant, p, k, dtype)
+        q, keys = _layer_params(variant, p, k, dtype, interval)
         prm.append((q, keys))
         Zp, Ep, Lp = Zs[-1], Es[-1], Ls[-1]
         Var = Lp + q["b1"] * Ts[-1]

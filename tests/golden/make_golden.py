@@ -48,17 +48,18 @@ def load_ref_cls(path: str, name: str = "DLADMMNet"):
     raise RuntimeError(f"class {name} not found in {path}")
 
 
-def run_ref(cls, inp, sd, K, dtype):
+def run_ref(cls, inp, sd, K, dtype, interval=0, fwd_k=False):
     conv = lambda a: torch.from_numpy(np.asarray(a)).to(dtype)  # noqa: E731
     m, n = inp["A"].shape
     B = inp["X"].shape[1]
+    extra = {"interval": interval} if interval else {}
     net = cls(m=m, n=0, d=n, batch_size=B, A=conv(inp["A"]), Z0=conv(inp["Z0"]),
-              E0=conv(inp["E0"]), L0=conv(inp["L0"]), layers=K)
+              E0=conv(inp["E0"]), L0=conv(inp["L0"]), layers=K, **extra)
     net.load_state_dict({k: conv(v) for k, v in sd.items()}, strict=True)
     net = net.to(dtype)
     keys = list(net.state_dict().keys())
     with torch.no_grad():
-        out = net(conv(inp["X"]))
+        out = net(conv(inp["X"]), K) if fwd_k else net(conv(inp["X"]))
     return out, keys
 
 
@@ -88,8 +89,10 @@ def make_one(name, defn, ref_root):
     cls = load_ref_cls(os.path.join(ref_root, problems.VARIANT_SOURCES[variant]))
     inp, sd = problems.build_problem(defn)
     K = defn["K"]
-    out32, keys = run_ref(cls, inp, sd, K, torch.float32)
-    out64, _ = run_ref(cls, inp, sd, K, torch.float64)
+    spec = problems.VARIANT_SPECS[variant]
+    kw = dict(interval=defn.get("interval", 0), fwd_k=spec.get("fwd_k", False))
+    out32, keys = run_ref(cls, inp, sd, K, torch.float32, **kw)
+    out64, _ = run_ref(cls, inp, sd, K, torch.float64, **kw)
     names = ["Z", "E", "L", "T"][: len(out32)]
     rec = {}
     for nm, seq32, seq64 in zip(names, out32, out64):

@@ -31,17 +31,18 @@ from make_golden import load_ref_cls, nrel  # noqa: E402
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def run_grad(cls, inp, sd, up, K, kind, dtype):
+def run_grad(cls, inp, sd, up, K, kind, dtype, interval=0, fwd_k=False):
     conv = lambda a: torch.from_numpy(np.asarray(a)).to(dtype)  # noqa: E731
     m, n = inp["A"].shape
     B = inp["X"].shape[1]
+    extra = {"interval": interval} if interval else {}
     net = cls(m=m, n=0, d=n, batch_size=B, A=conv(inp["A"]), Z0=conv(inp["Z0"]),
-              E0=conv(inp["E0"]), L0=conv(inp["L0"]), layers=K)
+              E0=conv(inp["E0"]), L0=conv(inp["L0"]), layers=K, **extra)
     net.load_state_dict({k: conv(v) for k, v in sd.items()}, strict=True)
     net = net.to(dtype)
     X = conv(inp["X"])
     A = conv(inp["A"])
-    out = net(X)
+    out = net(X, K) if fwd_k else net(X)
     Z, E, L = out[0], out[1], out[2]
     coeffs = problems.loss_coeffs(K)
     total = 0
@@ -55,6 +56,7 @@ def run_grad(cls, inp, sd, up, K, kind, dtype):
                 0.5 * torch.sum((X - torch.mm(A, Z[k])) ** 2.0, dim=0).mean()
         total = total + lk * coeffs[k]
     for k in range(K):
+        # newS: E[0] / L[0] are the inputs E0 / L0 (no parameter reaches them)
         total = total + (conv(up["Gz"][k]) * Z[k]).sum() + (conv(up["Ge"][k]) * E[k]).sum() + \
             (conv(up["Gl"][k]) * L[k]).sum()
     if "Gt" in up:
@@ -76,8 +78,10 @@ def make_one(name, gdef, ref_root):
     inp, sd = problems.build_problem(defn)
     ret_t = problems.VARIANT_SPECS[variant]["ret_t"]
     up = problems.make_upstream(defn, ret_t)
-    g32, l32 = run_grad(cls, inp, sd, up, defn["K"], gdef["loss"], torch.float32)
-    g64, l64 = run_grad(cls, inp, sd, up, defn["K"], gdef["loss"], torch.float64)
+    kw = dict(interval=defn.get("interval", 0),
+              fwd_k=problems.VARIANT_SPECS[variant].get("fwd_k", False))
+    g32, l32 = run_grad(cls, inp, sd, up, defn["K"], gdef["loss"], torch.float32, **kw)
+    g64, l64 = run_grad(cls, inp, sd, up, defn["K"], gdef["loss"], torch.float64, **kw)
     rec = {}
     for k in sd:
         rec["g:" + k] = g32[k].astype(np.float32)

@@ -53,6 +53,20 @@ VARIANT_SPECS = {
     "v6": dict(params=[("beta1", "11", 1.0), ("beta3", "11", 1.0), ("ss2_1", "11", 0.5),
                        ("ss2_2", "11", 0.5), ("active_para", "11", 0.2)],
                fc="per_layer", wscale=0.4, ret_t=True),
+    # V7 newS layer-wise schedule, main_syn_scalar_newS_layerwise.py:51-72; forward(x, K)
+    "v7": dict(params=[("beta1", "11", 1.0), ("beta2", "11", 1.0), ("beta3", "11", 1.0),
+                       ("ss2", "11", 1.0), ("active_para", "11", 0.1), ("active_para1", "11", 0.1)],
+               fc="per_layer", wscale=0.4, ret_t=False, fwd_k=True),
+    # tied newS, main_syn_scalar_tied_newS_layerwise.py:51-72
+    "v7t": dict(params=[("beta1", "11", 1.0), ("beta2", "11", 1.0), ("beta3", "11", 1.0),
+                        ("ss1", "11", 1.0), ("ss2", "11", 1.0), ("active_para", "11", 0.01),
+                        ("active_para1", "11", 0.01)],
+                fc="tied", wscale=0.4, ret_t=False, fwd_k=True),
+    # partially tied newS, main_syn_scalar_ptied_newS_layerwise.py:51-78 (ctor arg interval)
+    "v7p": dict(params=[("beta1", "11", 1.0), ("beta2", "11", 1.0), ("beta3", "11", 1.0),
+                        ("ss1", "11", 1.0), ("ss2", "11", 1.0), ("active_para", "11", 0.01),
+                        ("active_para1", "11", 0.01)],
+                fc="ptied", wscale=0.4, ret_t=False, fwd_k=True),
 }
 
 # Reference source file each variant's class is taken from (fixture generation only).
@@ -63,6 +77,9 @@ VARIANT_SOURCES = {
     "v4": "main_syn_l1l1_scalar.py",
     "v5": "main_syn_l1l1_scalar_tied.py",
     "v6": "main_syn_lasso_scalar.py",
+    "v7": "main_syn_scalar_newS_layerwise.py",
+    "v7t": "main_syn_scalar_tied_newS_layerwise.py",
+    "v7p": "main_syn_scalar_ptied_newS_layerwise.py",
 }
 
 
@@ -93,7 +110,7 @@ def make_inputs(m: int, n: int, B: int, seed: int, p: float = 0.1, sigma: float 
 
 def make_state_dict(variant: str, m: int, n: int, B: int, K: int, A: np.ndarray, seed: int,
                     perturb: float = 0.0, wscale: float | None = None,
-                    negtheta: bool = False) -> "OrderedDict[str, np.ndarray]":
+                    negtheta: bool = False, interval: int = 1) -> "OrderedDict[str, np.ndarray]":
     """state_dict (reference key names and shapes) at the reference init, optionally perturbed.
 
     perturb > 0 multiplies every entry of every non-weight param by (1 + perturb * U(-1, 1)).
@@ -118,6 +135,10 @@ def make_state_dict(variant: str, m: int, n: int, B: int, K: int, A: np.ndarray,
         for k in range(K):
             w = (At + 1e-3 * rng.standard_normal(At.shape)) * s
             sd[f"fc.{k}.weight"] = w.astype(np.float32)
+    elif spec["fc"] == "ptied":
+        for i in range(K // interval):
+            w = (At + 1e-3 * rng.standard_normal(At.shape)) * s
+            sd[f"fc.{i}.weight"] = w.astype(np.float32)
     else:
         w = (At + 1e-3 * rng.standard_normal(At.shape)) * s
         sd["fc.weight"] = w.astype(np.float32)
@@ -156,7 +177,18 @@ FIXTURES = {
     "v3_med_pert": dict(variant="v3", m=256, n=512, B=12, K=15, seed=1143, perturb=0.1),
     # BASELINE config 4 shape (LASSO m=512, n=2048, depth 40), few columns
     "v6_cfg4": dict(variant="v6", m=512, n=2048, B=4, K=40, seed=1144),
+    # newS layer-wise schedules
+    "v7_small_pert": dict(variant="v7", m=16, n=32, B=8, K=4, seed=1145, perturb=0.2),
+    "v7t_small_pert": dict(variant="v7t", m=16, n=32, B=8, K=4, seed=1146, perturb=0.2),
+    "v7p_small_pert": dict(variant="v7p", m=16, n=32, B=8, K=6, seed=1147, perturb=0.2,
+                           interval=2),
+    "v7_med": dict(variant="v7", m=250, n=500, B=9, K=8, seed=1148, perturb=0.1),
 }
+
+
+def ctor_extra(defn: dict) -> dict:
+    """Extra constructor arguments of a variant (ptied newS takes `interval`)."""
+    return {"interval": defn["interval"]} if "interval" in defn else {}
 
 
 def build_problem(defn: dict):
@@ -165,7 +197,7 @@ def build_problem(defn: dict):
     inp = make_inputs(d["m"], d["n"], d["B"], d["seed"])
     sd = make_state_dict(d["variant"], d["m"], d["n"], d["B"], d["K"], inp["A"], d["seed"],
                          perturb=d.get("perturb", 0.0), wscale=d.get("wscale"),
-                         negtheta=d.get("negtheta", False))
+                         negtheta=d.get("negtheta", False), interval=d.get("interval", 1))
     return inp, sd
 
 
@@ -186,6 +218,9 @@ GRAD_FIXTURES = {
     "grad_v6_small": dict(base="v6_small_pert", loss="lasso"),
     "grad_v4_ragged": dict(base="v4_ragged", loss="l1l1"),
     "grad_v2_ragged": dict(base="v2_ragged", loss="l1l1"),
+    "grad_v7_small": dict(base="v7_small_pert", loss="l1l1"),
+    "grad_v7t_small": dict(base="v7t_small_pert", loss="l1l1"),
+    "grad_v7p_small": dict(base="v7p_small_pert", loss="l1l1"),
     # BASELINE config-2 shape (m=256, n=512) at depth 5 (keeps each fixture ~2.5 MB)
     "grad_v4_med": dict(base="v4_med_pert", loss="l1l1", K=5),
     "grad_v6_med": dict(base="v6_med", loss="lasso", K=5),

@@ -33,12 +33,12 @@ def nrel(a, b):
     return float(np.linalg.norm(a - b) / nb) if nb > 0 else float(np.linalg.norm(a))
 
 
-def make_train_net(dl, variant, inp, sd, K):
+def make_train_net(dl, variant, inp, sd, K, **extra):
     m, n = inp["A"].shape
     B = inp["X"].shape[1]
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
     net = dl.VARIANTS[variant](m=m, n=0, d=n, batch_size=B, A=t(inp["A"]), Z0=t(inp["Z0"]),
-                               E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K)
+                               E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K, **extra)
     net.load_state_dict({k: t(v) for k, v in sd.items()}, strict=True)
     net.requires_grad_(True)
     return net
@@ -73,7 +73,7 @@ def run_grads(dl, name):
     d = meta["defn"]
     inp, sd = P.build_problem(d)
     up = P.make_upstream(d, P.VARIANT_SPECS[d["variant"]]["ret_t"])
-    net = make_train_net(dl, d["variant"], inp, sd, d["K"])
+    net = make_train_net(dl, d["variant"], inp, sd, d["K"], **P.ctor_extra(d))
     X = torch.from_numpy(inp["X"]).cuda()
     A = torch.from_numpy(inp["A"]).cuda()
     out = net(X)
@@ -193,10 +193,10 @@ def test_fused_training_loss(name, dl):
     X = torch.from_numpy(inp["X"]).cuda()
     A = torch.from_numpy(inp["A"]).cuda()
     coeffs = P.loss_coeffs(K)
-    net = make_train_net(dl, d["variant"], inp, sd, K)
+    net = make_train_net(dl, d["variant"], inp, sd, K, **P.ctor_extra(d))
     total, per_layer = net.training_loss(X, P.GRAD_ALPHA, coeffs, kind)
     total.backward()
-    net2 = make_train_net(dl, d["variant"], inp, sd, K)
+    net2 = make_train_net(dl, d["variant"], inp, sd, K, **P.ctor_extra(d))
     ref_total = total_loss(net2(X), X, A, {"Gz": np.zeros((K, 1, 1), np.float32),
                                           "Ge": np.zeros((K, 1, 1), np.float32),
                                           "Gl": np.zeros((K, 1, 1), np.float32)}, kind, K)

@@ -28,13 +28,13 @@ def nrel(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
-def make_net(dl, variant, inp, sd, K):
+def make_net(dl, variant, inp, sd, K, **extra):
     m, n = inp["A"].shape
     B = inp["X"].shape[1]
     cls = dl.VARIANTS[variant]
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
     net = cls(m=m, n=0, d=n, batch_size=B, A=t(inp["A"]), Z0=t(inp["Z0"]), E0=t(inp["E0"]),
-              L0=t(inp["L0"]), layers=K)
+              L0=t(inp["L0"]), layers=K, **extra)
     net.load_state_dict({k: t(v) for k, v in sd.items()}, strict=True)
     net.requires_grad_(False)
     return net
@@ -45,7 +45,7 @@ def test_matches_reference_golden(name, dl):
     g, meta = load_golden(name)
     d = meta["defn"]
     inp, sd = P.build_problem(d)
-    net = make_net(dl, d["variant"], inp, sd, d["K"])
+    net = make_net(dl, d["variant"], inp, sd, d["K"], **P.ctor_extra(d))
     X = torch.from_numpy(inp["X"]).cuda()
     with torch.no_grad():
         out = net(X)
@@ -263,3 +263,24 @@ def test_forced_per_layer_path_matches_fused(variant, dl, monkeypatch):
             assert nrel(b[k].cpu().numpy(), a[k].cpu().numpy()) <= 2e-6
     assert torch.equal(lean.Z[0], rl.Z[-1]) and torch.equal(lean.L[0], rl.L[-1])
     np.testing.assert_allclose(ol.cpu().numpy(), of.cpu().numpy(), rtol=2e-6)
+
+
+@pytest.mark.parametrize("variant,extra", [("v7", {}), ("v7t", {}), ("v7p", {"interval": 2})])
+def test_news_partial_depth(variant, extra, dl, oracle):
+    """newS forward(x, K) runs min(K, layers) layers (main_syn_scalar_newS_layerwise.py:78)."""
+    d = dict(variant=variant, m=64, n=256, B=40, K=6, seed=7301, perturb=0.2, **extra)
+    inp, sd = P.build_problem(d)
+    net = make_net(dl, variant, inp, sd, 6, **extra)
+    X = torch.from_numpy(inp["X"]).cuda()
+    for K in (1, 4, 9):
+        nl = min(K, 6)
+        with torch.no_grad():
+            Z, E, L = net(X, K)
+        assert len(Z) == len(E) == len(L) == nl
+        ref = oracle.forward(variant, inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd, nl)
+        r64 = oracle.forward(variant, inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd, nl,
+                             dtype=np.float64)
+        for nm, seq in (("Z", Z), ("E", E), ("L", L)):
+            for k in range(nl):
+                tol = max(REL, 3.0 * nrel(ref[nm][k], r64[nm][k]))  # the oracle's own fp32 gap
+                assert nrel(seq[k].cpu().numpy(), r64[nm][k]) <= tol, (nm, K, k)

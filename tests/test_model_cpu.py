@@ -10,11 +10,11 @@ from conftest import GOLDEN, load_golden
 import problems as P
 
 
-def _net(dl, variant, m=16, n=32, B=8, K=3, seed=1):
+def _net(dl, variant, m=16, n=32, B=8, K=3, seed=1, **extra):
     inp = P.make_inputs(m, n, B, seed)
     t = torch.from_numpy
     return dl.VARIANTS[variant](m=m, n=0, d=n, batch_size=B, A=t(inp["A"]), Z0=t(inp["Z0"]),
-                                E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K)
+                                E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K, **extra)
 
 
 @pytest.mark.parametrize("name", sorted(P.FIXTURES))
@@ -22,7 +22,7 @@ def test_state_dict_layout_matches_reference(name, dl):
     """Same keys, order and shapes as the reference class (recorded in each fixture)."""
     g, meta = load_golden(name)
     d = meta["defn"]
-    net = _net(dl, d["variant"], d["m"], d["n"], d["B"], d["K"])
+    net = _net(dl, d["variant"], d["m"], d["n"], d["B"], d["K"], **P.ctor_extra(d))
     sd = net.state_dict()
     assert list(sd.keys()) == meta["keys"]
     _, ref_sd = P.build_problem(d)
@@ -53,6 +53,9 @@ def test_names_and_init(dl):
     assert _net(dl, "v1").name() == "DLADMMNet"
     assert _net(dl, "v4").name() == "DLADMMNet_scalar"
     assert _net(dl, "v5").name() == "DLADMMNet_scalar_tied"
+    assert _net(dl, "v7").name() == "DLADMMNet_scalar_newS_layerwise"
+    assert _net(dl, "v7t").name() == "DLADMMNet_scalar_tied_newS_layerwise"
+    assert _net(dl, "v7p", K=6, interval=3).name() == "DLADMMNet_scalar_ptied3_newS_layerwise"
     net = _net(dl, "v4")
     W = net.fc[0].weight.detach().cpu()
     At = net.A.t().cpu()
