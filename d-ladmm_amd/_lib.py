@@ -12,8 +12,9 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DLADMM_LIB") or os.path.join(HERE, "lib", "libdladmm_hip.so")
 
-ABI_VERSION = 1
-MAX_LAYERS = 64
+ABI_VERSION = 2
+MAX_LAYERS = 65536
+MAX_LAYERS_V1 = 64
 NSCALAR = 8
 
 # enum dladmm_variant
@@ -26,7 +27,9 @@ P_BETA1, P_BETA2, P_BETA3, P_SS2, P_SS2B, P_THETA_E, P_THETA_Z, P_S1 = range(8)
 # every symbol include/dladmm.h declares (checked by tests/test_capi.py)
 EXPORTED = ("dladmm_abi_version", "dladmm_fwd_workspace_bytes", "dladmm_fwd_path",
             "dladmm_fwd_f32", "dladmm_bwd_workspace_bytes", "dladmm_bwd_f32",
-            "dladmm_error_string")
+            "dladmm_safeguard_f32", "dladmm_error_string")
+# enum dladmm_mu_updater
+MU_NONE, MU_EMA, MU_GS, MU_RT = 0, 1, 2, 3
 
 _fp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -71,6 +74,20 @@ class BwdDesc(ctypes.Structure):
     ]
 
 
+class SafeguardDesc(ctypes.Structure):
+    """Mirror of `struct dladmm_safeguard_desc` (include/dladmm.h)."""
+    _fields_ = [
+        ("abi_version", _i32), ("m", _i32), ("n", _i32), ("batch", _i32), ("ld", _i64),
+        ("Zl", _fp), ("El", _fp), ("Ll", _fp), ("Tl", _fp),
+        ("Zk", _fp), ("Ek", _fp), ("Lk", _fp), ("Tk", _fp),
+        ("Es", _fp), ("Ts", _fp), ("Ep", _fp),
+        ("Zo", _fp), ("Eo", _fp), ("Lo", _fp), ("To", _fp),
+        ("mu", _fp), ("norm_out", _fp), ("count", _fp),
+        ("beta", ctypes.c_float), ("c", ctypes.c_float), ("delta", ctypes.c_double),
+        ("updater", _i32), ("mu_param", ctypes.c_float),
+    ]
+
+
 _LIB = None
 
 
@@ -97,6 +114,8 @@ def lib():
     L.dladmm_bwd_workspace_bytes.argtypes = [ctypes.POINTER(BwdDesc)]
     L.dladmm_bwd_f32.restype = ctypes.c_int
     L.dladmm_bwd_f32.argtypes = [ctypes.POINTER(BwdDesc), ctypes.c_void_p]
+    L.dladmm_safeguard_f32.restype = ctypes.c_int
+    L.dladmm_safeguard_f32.argtypes = [ctypes.POINTER(SafeguardDesc), ctypes.c_void_p]
     L.dladmm_error_string.restype = ctypes.c_char_p
     L.dladmm_error_string.argtypes = [ctypes.c_int]
     if L.dladmm_abi_version() != ABI_VERSION:

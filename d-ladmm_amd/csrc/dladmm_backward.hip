@@ -9,15 +9,15 @@
 //   BK1(k)  P = A Z_k                   (m rows, contraction n)  recompute E_k, T_{k+1};
 //           adjoints of L_k, T_{k+1}, E_k -> gP, adjoint of E_{k-1}, partial adjoint of L_{k-1},
 //           Var_k = L_{k-1} + b1 T_k (operand of BK2/wgrad); grads of b3, b2, ss2, ss2b, theta_e
-//   BK2(k)  R = A^T gP, q = M_k Var_k    (n rows, contraction m, two GEMMs)  recompute U_k;
+//   BK2(k)  R = A^T gP, q = W_k Var_k    (n rows, contraction m, two GEMMs)  recompute U_k;
 //           gU = (adj Z_k + R) * S'(U_k) = adjoint of Z_{k-1}; grads of theta_z, s1
 //   BK3(k)  gVar = M_k^T gU              (m rows, contraction n)  adjoint of L_{k-1} += gVar,
 //           adjoint of T_k = b1 gVar; grad of b1
 //   WG(k)   gM_k = gU Var_k^T            (n x m, contraction over the batch: split-K + fixed-order
 //           reduction, so it is deterministic); gW_k = -s1 gM_k
-// where M_k = -s1 W_k is the forward's packed weight.  P and q are recomputed with the exact
-// fragment packing / accumulation order of the forward kernel that produced the saved outputs,
-// so the shrink masks S'(.) are those of the forward, bit for bit.
+// where M_k = -s1 W_k.  P and q are recomputed with the fragment packing / accumulation order of
+// the forward kernels (U = Z_{k-1} - s1 q on both forward paths), so the shrink masks S'(.) are
+// those of the forward, bit for bit.
 // Parameter gradients of broadcast parameters are reduced per wave (scalars: over the wave; per
 // row: over the wave's 16 columns) into partial buffers and summed in fp64 in a fixed order.
 #include "dladmm_common.h"
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(NW * 64, 1) void bwd_kernel(const BwdArgs a) {
                                     (1u << DLADMM_P_THETA_E) | (1u << DLADMM_P_SS2) |
                                     (1u << DLADMM_P_SS2B));
       } else if constexpr (PH == 2) {
-        // ---------------- BK2: rows of n.  acc = R = A^T gP, acc2 = q = M_k Var_k
+        // ---------------- BK2: rows of n.  acc = R = A^T gP, acc2 = q = W_k Var_k
         const bool rok = row < a.n;
         const bool ok = cv && rok;
         const int rowc = rok ? row : 0;
@@ -206,8 +206,8 @@ __global__ __launch_bounds__(NW * 64, 1) void bwd_kernel(const BwdArgs a) {
         const float zp = a.Zp[(int64_t)rowc * a.ldzp + colc];
         float s1 = 1.0f;
         if constexpr (PKIND == PK_SCALAR) s1 = sp[DLADMM_P_S1];
-        // U exactly as the forward kernel that produced the saved outputs formed it
-        const float U = a.ufused ? zp + q : zp - ((PKIND == PK_SCALAR) ? s1 * q : q);
+        // U exactly as the forward kernels formed it: Z_{k-1} - s1 (W_k Var_k)
+        const float U = zp - ((PKIND == PK_SCALAR) ? s1 * q : q);
         const float thz = pm(DLADMM_P_THETA_Z, rowc);
         float gZt = (a.AZ[o] + up(a.gZ, rowc)) + R;
         if (a.loss_kind) {
@@ -220,9 +220,7 @@ __global__ __launch_bounds__(NW * 64, 1) void bwd_kernel(const BwdArgs a) {
         const float gU = gZt * d.dx;
         pv[DLADMM_P_THETA_Z] = gZt * d.dth;
         if constexpr (PKIND == PK_SCALAR) {
-          // dU/ds1 = -W Var:  fused packing q = -s1 W Var, per-layer packing q = W Var
-          const float wv = a.ufused ? (s1 != 0.0f ? -q / s1 : 0.0f) : q;
-          pv[DLADMM_P_S1] = -gU * wv;
+          pv[DLADMM_P_S1] = -gU * q;  // dU/ds1 = -W Var
         }
         if (ok) a.AZ[o] = gU;  // adjoint of Z_{k-1}; also BK3's operand and wgrad's gM rows
         if (!ok) {

@@ -9,8 +9,10 @@
 namespace dladmm {
 
 // ------------------------------------------------------------------------ weight packing
+constexpr int kPackBatch = 64;  // sources per pack launch (the struct is a kernel argument)
+
 struct PackArgs {
-  const float* src[DLADMM_MAX_LAYERS + 1];
+  const float* src[kPackBatch];
   int R, C, RB, CB;  // valid rows/cols of each source; row-blocks (padded) / col-blocks packed
   int order;         // fragment (ib, jb) at: 0 ib*CB + jb; 1 jb*RB + ib (per-layer path);
                      // 2 ((ib/2)*CB + jb)*2 + ib%2 (fused path: output blocks in pairs)
@@ -21,6 +23,7 @@ struct PackArgs {
   int trans;           // 1: pack the transpose (element (row, c) = src[c][row])
   int t0;              // scal row of source t is t0 + t
 };
+static_assert(sizeof(PackArgs) <= 2048, "kernel argument size");
 
 // fragment (ib, jb) of source t: dst[..][lane][q] = src_t[16 ib + (lane & 15)][16 jb + 4 (lane >> 4) + q]
 // (0 outside R x C) -- exactly the A operand of one v_mfma_f32_16x16x4_f32 k-step group
@@ -93,6 +96,7 @@ inline int validate(const dladmm_fwd_desc* d) {
   if (d->variant < DLADMM_V1_LENA || d->variant > DLADMM_V6_LASSO) return DLADMM_E_VARIANT;
   if (d->m < 1 || d->n < 1 || d->batch < 1) return DLADMM_E_SHAPE;
   if (d->layers < 1 || d->layers > DLADMM_MAX_LAYERS) return DLADMM_E_LAYERS;
+  if (d->variant == DLADMM_V1_LENA && d->layers > DLADMM_MAX_LAYERS_V1) return DLADMM_E_LAYERS;
   if (d->loss_kind < 0 || d->loss_kind > 2) return DLADMM_E_UNSUPPORTED;
   if (!d->X || !d->A || !d->Z0 || !d->E0 || !d->L0 || !d->W || !d->Z || !d->E || !d->L)
     return DLADMM_E_NULL;
@@ -128,6 +132,13 @@ inline bool fits_32bit(const dladmm_fwd_desc* d) {
            (d->variant == DLADMM_V1_LENA && mx * d->ld_beta * 4 >= lim));
 }
 
+// every layer uses the same weight tensor (V5 tied, the KM iteration): packed once
+inline bool shared_weight(const dladmm_fwd_desc* d) {
+  for (int k = 1; k < d->layers; ++k)
+    if (d->W[k] != d->W[0]) return false;
+  return true;
+}
+
 inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
   *p = Plan{};
   const int s = pick_shape(d->m, d->n);
@@ -146,7 +157,7 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
     const size_t frag_bytes = (size_t)p->MP * p->NP * sizeof(float);
     p->off_ap = 0;
     p->off_wp = align256(frag_bytes);
-    p->off_loss = p->off_wp + align256(frag_bytes * K);
+    p->off_loss = p->off_wp + align256(frag_bytes * (shared_weight(d) ? 1 : K));
     p->total = p->off_loss + align256((size_t)2 * K * p->nslots * sizeof(float));
     return 0;
   }
@@ -166,7 +177,7 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
   const size_t fb = (size_t)kFrag * sizeof(float);
   p->off_ap = 0;
   p->off_wp = align256(fb * p->KB2 * p->MBp2);
-  p->off_v = p->off_wp + align256(fb * p->KB1 * p->MBp1 * K);
+  p->off_v = p->off_wp + align256(fb * p->KB1 * p->MBp1 * (shared_weight(d) ? 1 : K));
   p->off_zw = p->off_v + align256((size_t)d->m * B * sizeof(float));
   const bool lean = !d->keep_all && K > 1;
   p->off_ew = p->off_zw + (lean ? align256((size_t)d->n * B * sizeof(float)) : 0);
@@ -177,16 +188,23 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
 }
 
 // ---- pack helpers
+// Pack T sources (layer t uses scal row t0 + t) into consecutive [RB*CB] fragment blocks, at
+// most kPackBatch sources per launch.
 inline hipError_t pack(const float* const* srcs, int T, int R, int C, int64_t ld, int RB, int CB,
                        int order, float* dst, hipStream_t s, float sign = 1.0f,
                        const float* scal = nullptr, int trans = 0, int t0 = 0) {
-  PackArgs pa{};
-  pa.trans = trans; pa.t0 = t0;
-  for (int t = 0; t < T; ++t) pa.src[t] = srcs[t];
-  pa.R = R; pa.C = C; pa.RB = RB; pa.CB = CB; pa.order = order; pa.ld = ld; pa.dst = dst;
-  pa.sign = sign; pa.scal = scal;
-  hipLaunchKernelGGL(pack_frags_kernel, dim3((RB * CB + 3) / 4, T), dim3(256), 0, s, pa);
-  return hipGetLastError();
+  for (int b = 0; b < T; b += kPackBatch) {
+    const int nb = T - b < kPackBatch ? T - b : kPackBatch;
+    PackArgs pa{};
+    pa.trans = trans; pa.t0 = t0 + b;
+    for (int t = 0; t < nb; ++t) pa.src[t] = srcs[b + t];
+    pa.R = R; pa.C = C; pa.RB = RB; pa.CB = CB; pa.order = order; pa.ld = ld;
+    pa.dst = dst + (size_t)b * RB * CB * kFrag;
+    pa.sign = sign; pa.scal = scal;
+    hipLaunchKernelGGL(pack_frags_kernel, dim3((RB * CB + 3) / 4, nb), dim3(256), 0, s, pa);
+    if (hipError_t e = hipGetLastError()) return e;
+  }
+  return hipSuccess;
 }
 
 inline int run_fused(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStream_t s) {
@@ -194,13 +212,13 @@ inline int run_fused(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStrea
   float* Wp = (float*)(ws + p.off_wp);
   float* lossp = (float*)(ws + p.off_loss);
   const int MB = p.MP / 16, NB = p.NP / 16;
-  // 1. pack A and every -s1_k W_k into paired MFMA fragment order (zero-padded to MP x NP);
-  //    s1 is ss1[k] for V5 and 1.0 in the V4/V6 tables; V1-V3 have no step size
+  // 1. pack A and every -W_k into paired MFMA fragment order (zero-padded to MP x NP); a weight
+  //    shared by every layer is packed once
   const float* asrc[1] = {d->A};
-  const bool has_s1 = d->variant >= DLADMM_V4_SCALAR;
+  const bool shared = shared_weight(d);
   if (hipError_t e = pack(asrc, 1, d->m, d->n, d->ld_a, MB, NB, 2, Ap, s)) return (int)e;
-  if (hipError_t e = pack(d->W, d->layers, d->n, d->m, d->ld_w, NB, MB, 2, Wp, s, -1.0f,
-                          has_s1 ? d->scalar_params : nullptr))
+  if (hipError_t e = pack(d->W, shared ? 1 : d->layers, d->n, d->m, d->ld_w, NB, MB, 2, Wp, s,
+                          -1.0f))
     return (int)e;
   // 2. the fused K-layer forward
   FusedArgs a{};
@@ -211,6 +229,7 @@ inline int run_fused(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStrea
   a.E0 = d->E0; a.lde0 = d->ld_e0;
   a.L0 = d->L0; a.ldl0 = d->ld_l0;
   a.Ap = Ap; a.Wp = Wp;
+  a.wstep = shared ? 0 : 1;
   a.scal = d->scalar_params;
   a.rowp = d->row_params; a.rstride = d->row_stride;
   a.ldb = d->ld_beta;
@@ -242,7 +261,9 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
   // 1. pack A (rows m, contraction n) and every W_k (rows n, contraction m), k-major
   const float* asrc[1] = {d->A};
   if (hipError_t e = pack(asrc, 1, m, n, d->ld_a, p.MBp2, p.KB2, 1, Ap, s)) return (int)e;
-  if (hipError_t e = pack(d->W, K, n, m, d->ld_w, p.MBp1, p.KB1, 1, Wp, s)) return (int)e;
+  const bool shared = shared_weight(d);
+  if (hipError_t e = pack(d->W, shared ? 1 : K, n, m, d->ld_w, p.MBp1, p.KB1, 1, Wp, s))
+    return (int)e;
   if (d->loss_kind) {
     if (hipError_t e = hipMemsetAsync(lossp, 0, (size_t)2 * K * p.nslots * sizeof(float), s))
       return (int)e;
@@ -290,7 +311,7 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
     const int64_t ldout = (lean && !last) ? B : ldo;
     // G1(k): Z_k = S(Z_{k-1} - s1 * W_k Var_k)
     LayerArgs b = a;
-    b.k = k; b.KB = p.KB1; b.MBp = p.MBp1; b.Krows = m; b.Wp = Wp + k * wl;
+    b.k = k; b.KB = p.KB1; b.MBp = p.MBp1; b.Krows = m; b.Wp = Wp + (shared ? 0 : k * wl);
     b.S = V; b.ldS = B;
     b.Zprev = Zp; b.ldzp = ldzp;
     b.Zo = Zo; b.ldo = ldout;
@@ -403,7 +424,6 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
   const int v = f.variant;
   const bool has_s1 = v >= DLADMM_V4_SCALAR;
   const bool tied = d->gw_sum != 0;
-  const bool ufused = p.fwd.path == 1;
   const bool rowk = v == DLADMM_V2_LTHETA || v == DLADMM_V3_FULL;
   float* A1 = (float*)(ws + p.off_a1);
   float* At = (float*)(ws + p.off_at);
@@ -431,7 +451,6 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
   const int64_t zl = (int64_t)n * ldo, ml = (int64_t)m * ldo;
   BwdArgs a{};
   a.m = m; a.n = n; a.B = (int)B; a.K = K;
-  a.ufused = ufused ? 1 : 0;
   a.nslots = p.nslots; a.ncg = p.ncg;
   a.X = f.X; a.ldx = f.ld_x;
   a.ldg = d->ld_g;
@@ -445,11 +464,10 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
   const dim3 gm(p.gx, p.slices_m), gn(p.gx, p.slices_n);
   const size_t part_bytes = p.off_wpart - p.off_part;
   for (int k = K - 1; k >= 0; --k) {
-    // M_k exactly as the forward packed it (fused: -s1 W_k; per-layer: W_k), and (-s1 W_k)^T
+    // W_k (q = W_k Var_k; both forward paths formed U = Z_{k-1} - s1 q bit for bit) and
+    // (-s1 W_k)^T
     const float* wsrc[1] = {f.W[k]};
-    if (hipError_t e = pack(wsrc, 1, n, m, f.ld_w, p.NBpn, p.MB, 1, Mp, s, ufused ? -1.0f : 1.0f,
-                            (ufused && has_s1) ? f.scalar_params : nullptr, 0, k))
-      return (int)e;
+    if (hipError_t e = pack(wsrc, 1, n, m, f.ld_w, p.NBpn, p.MB, 1, Mp, s)) return (int)e;
     if (hipError_t e = pack(wsrc, 1, m, n, f.ld_w, p.MBpm, p.NB, 1, Mt, s, -1.0f,
                             has_s1 ? f.scalar_params : nullptr, 1, k))
       return (int)e;

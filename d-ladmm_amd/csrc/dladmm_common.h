@@ -14,7 +14,8 @@ namespace dladmm {
 
 
 enum { EM_V1 = 0, EM_VVAR = 1, EM_LASSO = 2 };   // E-step form
-enum { PK_SCALAR = 0, PK_ROW = 1, PK_ELEM = 2 };  // parameter broadcast class
+// parameter broadcast class; PK_S1 = scalar params plus a per-layer step s1 on W Var (V5)
+enum { PK_SCALAR = 0, PK_ROW = 1, PK_ELEM = 2, PK_S1 = 3 };
 
 constexpr int kWaves = 4;
 constexpr int kTileCols = 16 * kWaves;  // batch columns per workgroup

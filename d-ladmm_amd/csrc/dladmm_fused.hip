@@ -14,7 +14,7 @@
 //    lane-local -- no LDS transpose, no HBM round trip for the state;
 //  * two output blocks are computed together (two independent MFMA chains, so neither waits
 //    on the MFMA's dependent-issue latency and no partial sums need combining); W_k is packed
-//    as -s1*W_k so the Z update is one add.  The chains start at zero: starting them at Z or
+//    as -W_k so the Z update is one add (V5 multiplies by its step ss1[k] first).  The chains start at zero: starting them at Z or
 //    -X (saving that add) accumulates every rounding at the state's magnitude and measurably
 //    loses accuracy against the reference on cancelling residuals;
 //  * W_k and A are pre-packed (pack_frags_kernel) into paired fragment order (1 KiB per 16x16
@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   const int64_t wl = (int64_t)F::GF * kFrag;  // floats per packed W_k
   auto gsrc = [&](int gi) -> const float* {
     const int kk = gi >> 1;
-    return ((gi & 1) && kk < K) ? a.Wp + (int64_t)kk * wl : a.Ap;
+    return ((gi & 1) && kk < K) ? a.Wp + (int64_t)(kk * a.wstep) * wl : a.Ap;
   };
   // source of chunk ch (may run past the GEMM) of GEMM gi
   // The GEMM base goes through an opaque statement before the chunk offset is added: otherwise
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   };
   // uniform per-layer scalars (s_load).  k = -1 (prologue) reads layer 0; b1n = beta1 of the
   // layer whose Var the G2 epilogue of layer k produces (k+1, clamped).
-  struct LayerP { float b1n, b2, b3, ss2, ss2b; ShrinkP the, thz; };
+  struct LayerP { float b1n, b2, b3, ss2, ss2b, s1; ShrinkP the, thz; };
   auto layer_params = [&](int k) -> LayerP {
     LayerP p{};
     if constexpr (PKIND != PK_ROW) {
@@ -152,6 +152,7 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
       p.ss2b = sp[DLADMM_P_SS2B];
       p.the = shrink_params(sp[DLADMM_P_THETA_E]);
       p.thz = shrink_params(sp[DLADMM_P_THETA_Z]);
+      if constexpr (PKIND == PK_S1) p.s1 = sp[DLADMM_P_S1];
       p.b1n = ((cfloat_p)a.scal)[kn * DLADMM_NSCALAR + DLADMM_P_BETA1];
     }
     return p;
@@ -201,12 +202,13 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
 
   // ---------------------------------------------------------------- per-row epilogues
   // G1 block b, row r of layer k: Z = S(Z - s1*(W_k Var), theta_z)  main_lena.py:86 / tied :114
-  // (q = -s1 W_k Var: the chain ran on the negated packed weights)
+  // (q = -W_k Var: the chain ran on the negated packed weights, so Z + s1*q is the reference's
+  // Z - ss1*fc(Var) operation for operation; s1 = 1 outside V5)
   auto epi1_row = [&](const LayerP& P, rsrc_t rzo, int k, int b, int r, const f32x4& q) {
 #if DLADMM_ABLATE & 2  // timing experiment: no epilogue work (WRONG results)
     Zr[b][r] = q[r]; pin_agpr(Zr[b][r]); return;
 #endif
-    const float u = Zr[b][r] + q[r];
+    const float u = (PKIND == PK_S1) ? Zr[b][r] + P.s1 * q[r] : Zr[b][r] + q[r];
     float z;
     if constexpr (PKIND == PK_ROW) {
       z = shrink(u, rowp(k, DLADMM_P_THETA_Z, b, r));
@@ -517,8 +519,8 @@ hipError_t dispatch_variant(int variant, const FusedArgs& a, int grid, hipStream
     case DLADMM_V1_LENA: return launch_fused<MP, NP, EM_V1, PK_ELEM>(a, grid, s);
     case DLADMM_V2_LTHETA: return launch_fused<MP, NP, EM_V1, PK_ROW>(a, grid, s);
     case DLADMM_V3_FULL: return launch_fused<MP, NP, EM_VVAR, PK_ROW>(a, grid, s);
-    case DLADMM_V4_SCALAR:
-    case DLADMM_V5_TIED: return launch_fused<MP, NP, EM_VVAR, PK_SCALAR>(a, grid, s);
+    case DLADMM_V4_SCALAR: return launch_fused<MP, NP, EM_VVAR, PK_SCALAR>(a, grid, s);
+    case DLADMM_V5_TIED: return launch_fused<MP, NP, EM_VVAR, PK_S1>(a, grid, s);
     case DLADMM_V6_LASSO: return launch_fused<MP, NP, EM_LASSO, PK_SCALAR>(a, grid, s);
   }
   return hipErrorInvalidValue;

@@ -17,12 +17,14 @@ struct FusedArgs {
   const float* E0; int64_t lde0;
   const float* L0; int64_t ldl0;
   const float* Ap;   // packed A          [MB/2][NB][2] fragments (pair order)
-  const float* Wp;   // packed -s1_k W_k  [K][NB/2][MB][2] fragments
+  const float* Wp;   // packed -W_k  [K][NB/2][MB][2] fragments (V5: s1 applied in the epilogue)
+  int wstep;         // 1: layer k reads packed weight k; 0: every layer reads the one shared weight
+  int pad1;
   const float* scal; // [K][8]
   const float* rowp; int64_t rstride;  // [K][8][rstride]
   int64_t ldb;
-  const float* b1e[DLADMM_MAX_LAYERS];
-  const float* b2e[DLADMM_MAX_LAYERS];
+  const float* b1e[DLADMM_MAX_LAYERS_V1];
+  const float* b2e[DLADMM_MAX_LAYERS_V1];
   float* Zo; float* Eo; float* Lo; float* To; int64_t ldo;
   float* lossp;      // [K][2][nwaves]
 };
@@ -81,7 +83,6 @@ constexpr int kBwdCols = 16 * kBwdWaves;
 struct BwdArgs {
   int m, n, B, K, k;
   int KB, MBp, Krows;         // slice GEMM geometry (BK2: both GEMMs share it)
-  int ufused;                 // 1: forward formed U = Z_{k-1} + (-s1 W_k) Var; 0: Z - s1 (W Var)
   int nslots, ncg;            // scalar partial slots per param slot; column groups (row kind)
   const float* Wp; const float* S; int64_t ldS;     // GEMM 1: packed operand, B operand
   const float* Wp2; const float* S2; int64_t ldS2;  // GEMM 2 (BK2 only)
@@ -111,6 +112,12 @@ struct WgradArgs {
 
 hipError_t launch_bwd(int phase, int variant, const BwdArgs& a, dim3 grid, int sb,
                       hipStream_t s);
+
+// every argument struct travels by value as a kernel argument: keep them small
+static_assert(sizeof(FusedArgs) <= 2048, "kernel argument size");
+static_assert(sizeof(LayerArgs) <= 2048, "kernel argument size");
+static_assert(sizeof(BwdArgs) <= 2048, "kernel argument size");
+static_assert(sizeof(WgradArgs) <= 2048, "kernel argument size");
 hipError_t launch_wgrad(const WgradArgs& a, int tiles, hipStream_t s);
 hipError_t launch_wgrad_reduce(const float* part, int nchunks, int n, int m, const float* scal,
                                int k, int accumulate, float* gW, int64_t ldgw, hipStream_t s);

@@ -54,8 +54,9 @@ def _fill_fwd_desc(d, variant, X, A, W, Z0, E0, L0, scalar_params, row_params, b
         raise RuntimeError(
             "dladmm: Z0/E0/L0 shapes do not broadcast with X: "
             f"Z0 {tuple(Z0.shape)}, E0 {tuple(E0.shape)}, L0 {tuple(L0.shape)}, X {tuple(X.shape)}")
-    if not 1 <= K <= _lib.MAX_LAYERS:
-        raise ValueError(f"dladmm: layers must be in [1, {_lib.MAX_LAYERS}], got {K}")
+    kmax = _lib.MAX_LAYERS_V1 if variant == _lib.V1_LENA else _lib.MAX_LAYERS
+    if not 1 <= K <= kmax:
+        raise ValueError(f"dladmm: layers must be in [1, {kmax}], got {K}")
     Ws = [_f32_dev(w if w.dim() == 2 and w.stride(1) == 1 else w.contiguous(), f"W[{k}]")
           for k, w in enumerate(W)]
     ldw = Ws[0].stride(0)

@@ -29,8 +29,9 @@
 extern "C" {
 #endif
 
-#define DLADMM_ABI_VERSION 1
-#define DLADMM_MAX_LAYERS 64
+#define DLADMM_ABI_VERSION 2
+#define DLADMM_MAX_LAYERS 65536   /* K limit (V4-V6; e.g. the K=2000 KM ground-truth iteration) */
+#define DLADMM_MAX_LAYERS_V1 64   /* V1: per-layer per-sample beta pointer tables */
 
 /* Reference variants (class DLADMMNet of the named reference script). */
 enum dladmm_variant {
@@ -102,7 +103,8 @@ typedef struct dladmm_fwd_desc {
   const float* L0; int64_t ld_l0;  /* m x batch */
 
   /* weights: host array of `layers` device pointers to fc[k].weight (n x m, row stride ld_w).
-     V5 (tied) passes the same pointer `layers` times. */
+     V5 (tied) passes the same pointer `layers` times; when every entry is the same pointer the
+     weight is packed once (any K). */
   const float* const* W; int64_t ld_w;
 
   /* parameters (device), see dladmm_param_slot:
@@ -202,6 +204,45 @@ size_t dladmm_bwd_workspace_bytes(const dladmm_bwd_desc* d);
 /* Enqueue the whole reverse sweep on `stream` (hipStream_t).  Deterministic: every reduction
    (parameter slots, per-row params, weight gradients) is summed in a fixed order. */
 int dladmm_bwd_f32(const dladmm_bwd_desc* d, void* stream);
+
+/*
+ * Safeguard step of learned + safeguarded KM (LSKM):
+ * test_syn_l1l1_scalar.py:227-266 with the mu updaters of mu_updater.py:18-116.
+ * Given, for every batch column, the L2O candidate (Zl, El, Ll, Tl), the classic KM candidate
+ * (Zk, Ek, Lk, Tk) -- both one step from the same state whose E is Ep -- and the KM step taken
+ * from the L2O candidate (Es, Ts), it computes
+ *   |S| = sqrt(sum_i (beta Ts_i)^2 + (c ((Es_i - 2 El_i) + Ep_i))^2),   keep = |S| < (1-delta) mu,
+ * updates mu, writes the selected candidate to (Zo, Eo, Lo, To) and adds the number of
+ * safeguarded (not kept) columns to *count.  All matrices share the row stride ld.
+ * With Zo == NULL it only initialises mu = |S| (mu_0 = |S(Z0, E0, L0, T0, X, E0)|, :190-197;
+ * pass the KM step from the initial state as Es/Ts and E0 as El and Ep).
+ */
+enum dladmm_mu_updater {
+  DLADMM_MU_NONE = 0, /* BlankUpdater: mu = 1e10 after the first step (mu_updater.py:98-110)  */
+  DLADMM_MU_EMA = 1,  /* mu = keep ? p|S| + (1-p) mu : mu                  (:18-32)            */
+  DLADMM_MU_GS = 2,   /* mu = keep ? (1-p) mu : mu                         (:34-52)            */
+  DLADMM_MU_RT = 3    /* mu = keep ? |S| : mu                              (:55-73)            */
+};
+
+typedef struct dladmm_safeguard_desc {
+  int32_t abi_version;
+  int32_t m, n, batch;
+  int64_t ld;
+  const float *Zl, *El, *Ll, *Tl;  /* L2O candidate (Z: n rows, others m rows) */
+  const float *Zk, *Ek, *Lk, *Tk;  /* KM candidate */
+  const float *Es, *Ts;            /* KM step from the L2O candidate */
+  const float* Ep;                 /* E of the state both candidates started from */
+  float *Zo, *Eo, *Lo, *To;        /* selected outputs (may alias neither input) */
+  float* mu;                       /* [batch] in/out */
+  float* norm_out;                 /* [batch] |S| or NULL */
+  int32_t* count;                  /* += safeguarded columns */
+  float beta, c;
+  double delta;
+  int32_t updater;                 /* enum dladmm_mu_updater */
+  float mu_param;
+} dladmm_safeguard_desc;
+
+int dladmm_safeguard_f32(const dladmm_safeguard_desc* d, void* stream);
 
 /* Text for a return code of this library (DLADMM_E_* or hipError_t). */
 const char* dladmm_error_string(int code);

@@ -256,3 +256,29 @@ def make_upstream(defn: dict, returns_t: bool):
     if returns_t:
         out["Gt"] = g(K + 1, m, B)
     return out
+
+
+# ---------------------------------------------------------------- classic KM / LSKM (row f2)
+# name -> test_syn_l1l1_scalar.py configuration: the V4 parameter set of `defn`, the module
+# globals the reference class reads (alpha, delta, mu_k_method, mu_k_param, continued) and the
+# forward arguments (use_learned, use_safeguard, K).
+def _lskm(defn, layers, K, learned, safeguard, continued=False, alpha=0.01, delta=-99.0,
+          mu="None", mu_param=0.0):
+    return dict(defn=defn, layers=layers, K=K, learned=learned, safeguard=safeguard,
+                continued=continued, alpha=alpha, delta=delta, mu=mu, mu_param=mu_param)
+
+
+_LS = dict(variant="v4", m=16, n=32, B=24, K=6, seed=1150, perturb=0.3, wscale=0.8)
+_LM = dict(variant="v4", m=250, n=500, B=10, K=5, seed=1151, perturb=0.2, wscale=0.9)
+LSKM_FIXTURES = {
+    "lskm_km_small": _lskm(_LS, 6, 120, False, False),                  # classic KM only
+    "lskm_km_med": _lskm(_LM, 5, 60, False, False, alpha=0.05),
+    "lskm_l2o_small": _lskm(_LS, 6, 6, True, False),                    # learned only
+    "lskm_sg_none": _lskm(_LS, 6, 6, True, True, delta=0.0),            # safeguard, BlankUpdater
+    "lskm_sg_ema": _lskm(_LS, 6, 6, True, True, delta=0.05, mu="EMA", mu_param=0.5),
+    "lskm_sg_gs": _lskm(_LS, 6, 6, True, True, delta=0.0, mu="GS", mu_param=0.2),
+    "lskm_sg_rt": _lskm(_LS, 6, 6, True, True, delta=0.0, mu="RT"),
+    "lskm_sg_continued": _lskm(_LS, 6, 30, True, True, continued=True, delta=0.0, mu="EMA",
+                               mu_param=0.3),
+    "lskm_sg_med": _lskm(_LM, 5, 5, True, True, delta=0.0, mu="EMA", mu_param=0.5),
+}

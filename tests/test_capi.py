@@ -31,7 +31,7 @@ def _desc(dl, **kw):
         setattr(d, f, fake)
     d.ld_x = d.ld_z0 = d.ld_e0 = d.ld_l0 = d.ld_out = 1000
     d.ld_a, d.ld_w = 512, 256
-    w = dl._lib.ptr_array([fake] * 15)
+    w = dl._lib.ptr_array([fake + 4096 * k for k in range(15)])
     d.W = ctypes.cast(w, ctypes.POINTER(ctypes.c_void_p))
     for k, v in kw.items():
         setattr(d, k, v)
@@ -46,11 +46,15 @@ def test_workspace_and_path(dl):
     # packed A + 15 packed W_k (256 x 512 fp32 each) + per-wave loss partials
     assert ws >= 16 * 256 * 512 * 4 + 2 * 15 * 16 * 4 * 4
     assert ws % 256 == 0
+    # one weight shared by every layer (V5 tied / the KM iteration) is packed once
+    w1 = dl._lib.ptr_array([1 << 40] * 15)
+    d.W = ctypes.cast(w1, ctypes.POINTER(ctypes.c_void_p))
+    assert L.dladmm_fwd_workspace_bytes(ctypes.byref(d)) == ws - 14 * 256 * 512 * 4
 
 
 @pytest.mark.parametrize("field,value,code", [
     ("abi_version", 99, -1), ("variant", 9, -2), ("m", 0, -3), ("batch", 0, -3),
-    ("layers", 0, -4), ("layers", 65, -4), ("X", None, -5), ("ld_x", 10, -3),
+    ("layers", 0, -4), ("layers", 65537, -4), ("X", None, -5), ("ld_x", 10, -3),
     ("loss_kind", 7, -7),
 ])
 def test_validation_codes(dl, field, value, code):

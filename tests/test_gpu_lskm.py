@@ -1,0 +1,66 @@
+"""Classic KM / learned + safeguarded KM on the HIP kernels against
+the reference test-script class (golden fixtures, tests/golden/make_golden_lskm.py) and the
+oracle (oracle/dladmm_oracle_lskm.py) at the K = 2000 ground-truth depth."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+import problems as P
+
+pytestmark = pytest.mark.gpu
+
+
+def nrel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def make(dl, case, inp, sd):
+    m, n = inp["A"].shape
+    B = inp["X"].shape[1]
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+    net = dl.DLADMMNetLSKM(m=m, n=0, d=n, batch_size=B, A=t(inp["A"]), Z0=t(inp["Z0"]),
+                           E0=t(inp["E0"]), L0=t(inp["L0"]), layers=case["layers"],
+                           alpha=case["alpha"], delta=case["delta"], mu_k_method=case["mu"],
+                           mu_k_param=case["mu_param"])
+    net.load_state_dict({k: t(v) for k, v in sd.items()}, strict=True)
+    return net
+
+
+@pytest.mark.parametrize("name", sorted(P.LSKM_FIXTURES))
+def test_lskm_matches_reference(name, dl):
+    g, meta = load_golden(name)
+    case = meta["case"]
+    inp, sd = P.build_problem(case["defn"])
+    net = make(dl, case, inp, sd)
+    X = torch.from_numpy(inp["X"]).cuda()
+    out = net(X, case["learned"], case["safeguard"], case["continued"], K=case["K"])
+    assert len(out) == (5 if case["learned"] and case["safeguard"] else 4)
+    K = case["K"]
+    assert len(out[0]) == K and len(out[3]) == K + 1
+    for i, j in enumerate(g["layers_kept"]):
+        for c, nm in enumerate("ZELT"):
+            got = out[c][j + 1 if nm == "T" else j].cpu().numpy()
+            tol = max(1e-5, 3.0 * float(g["gap_" + nm][i]))
+            assert nrel(got, g[nm][i]) <= tol, (nm, int(j))
+    if "sg_count" in g.files:
+        np.testing.assert_array_equal(out[4], g["sg_count"])
+
+
+def test_km_ground_truth_depth(dl):
+    """K = 2000 KM iterations (the test scripts' ground truth, test_syn_l1l1_scalar.py:478) in
+    one launch with the weight A^T packed once, against the oracle."""
+    from oracle import dladmm_oracle_lskm as ol
+    d = dict(variant="v4", m=64, n=128, B=40, K=3, seed=1160, perturb=0.1)
+    inp, sd = P.build_problem(d)
+    case = dict(layers=3, alpha=0.01, delta=-99.0, mu="None", mu_param=0.0)
+    net = make(dl, case, inp, sd)
+    X = torch.from_numpy(inp["X"]).cuda()
+    Z, E, L, T = net(X, False, False, False, K=2000)
+    ref = ol.lskm_forward(inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd, 3, False,
+                          False, False, 2000, 0.01)
+    for k in (0, 9, 99, 1999):
+        assert nrel(Z[k].cpu().numpy(), ref["Z"][k]) <= 1e-4, k
+        assert nrel(E[k].cpu().numpy(), ref["E"][k]) <= 1e-4, k

@@ -80,16 +80,19 @@ def _oracle_case(oracle, variant, m, n, B, K, seed, perturb=0.1, wscale=None, sd
     ref["Xs"] = inp["X"]
     ref["gap"] = {nm: [nrel(a, b) for a, b in zip(ref[nm], ref64[nm])]
                   for nm in ("Z", "E", "L", "T") if nm in ref}
+    ref["r64"] = ref64
     return inp, sd, ref
 
 
 def _compare(out, ref, tag=""):
-    """Per layer: nrel(gpu, oracle32) <= max(1e-5, 3 x nrel(oracle32, oracle64)).  T (= A Z + E
-    - X, a small residual) is measured against the scale of X."""
+    """Per layer, against the fp64 oracle: nrel(gpu, oracle64) <= max(1e-5, 3 x nrel(oracle32,
+    oracle64)) -- the GPU's fp32 result may be as far from the exact one as the reference's own
+    fp32 evaluation is (it sums its GEMMs in another order).  T (= A Z + E - X, a small residual)
+    is measured against the scale of X."""
     names = ["Z", "E", "L", "T"][: len(out)]
     for nm, seq in zip(names, out):
         for k, t in enumerate(seq):
-            r = np.asarray(ref[nm][k], np.float64)
+            r = np.asarray(ref["r64"][nm][k], np.float64)
             got = t.cpu().numpy().astype(np.float64)
             if nm == "T":
                 e = float(np.linalg.norm(got - r) / max(np.linalg.norm(ref["Xs"]), 1e-30))
