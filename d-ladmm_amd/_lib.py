@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DLADMM_LIB") or os.path.join(HERE, "lib", "libdladmm_hip.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_LAYERS = 65536
 MAX_LAYERS_V1 = 64
 NSCALAR = 8
@@ -27,7 +27,7 @@ P_BETA1, P_BETA2, P_BETA3, P_SS2, P_SS2B, P_THETA_E, P_THETA_Z, P_S1 = range(8)
 # every symbol include/dladmm.h declares (checked by tests/test_capi.py)
 EXPORTED = ("dladmm_abi_version", "dladmm_fwd_workspace_bytes", "dladmm_fwd_path",
             "dladmm_fwd_f32", "dladmm_bwd_workspace_bytes", "dladmm_bwd_f32",
-            "dladmm_safeguard_f32", "dladmm_error_string")
+            "dladmm_safeguard_f32", "dladmm_colobj_f32", "dladmm_error_string")
 # enum dladmm_mu_updater
 MU_NONE, MU_EMA, MU_GS, MU_RT = 0, 1, 2, 3
 
@@ -57,6 +57,7 @@ class FwdDesc(ctypes.Structure):
         ("loss_sums", _fp),
         ("workspace", _fp), ("workspace_bytes", ctypes.c_size_t),
         ("ev_kernel_start", _fp), ("ev_kernel_stop", _fp),
+        ("col_loss", _fp),
     ]
 
 
@@ -88,6 +89,20 @@ class SafeguardDesc(ctypes.Structure):
     ]
 
 
+class ColObjDesc(ctypes.Structure):
+    """Mirror of `struct dladmm_colobj_desc` (include/dladmm.h)."""
+    _fields_ = [
+        ("abi_version", _i32), ("m", _i32), ("n", _i32), ("batch", _i32), ("layers", _i32),
+        ("fit_kind", _i32),
+        ("Z", _fp), ("z_layer_stride", _i64), ("ld_z", _i64),
+        ("E", _fp), ("e_layer_stride", _i64), ("ld_e", _i64),
+        ("T", _fp), ("t_layer_stride", _i64), ("ld_t", _i64),
+        ("Zref", _fp), ("ld_zref", _i64),
+        ("Eref", _fp), ("ld_eref", _i64),
+        ("reg", _fp), ("fit", _fp), ("dz", _fp), ("de", _fp),
+    ]
+
+
 _LIB = None
 
 
@@ -116,6 +131,8 @@ def lib():
     L.dladmm_bwd_f32.argtypes = [ctypes.POINTER(BwdDesc), ctypes.c_void_p]
     L.dladmm_safeguard_f32.restype = ctypes.c_int
     L.dladmm_safeguard_f32.argtypes = [ctypes.POINTER(SafeguardDesc), ctypes.c_void_p]
+    L.dladmm_colobj_f32.restype = ctypes.c_int
+    L.dladmm_colobj_f32.argtypes = [ctypes.POINTER(ColObjDesc), ctypes.c_void_p]
     L.dladmm_error_string.restype = ctypes.c_char_p
     L.dladmm_error_string.argtypes = [ctypes.c_int]
     if L.dladmm_abi_version() != ABI_VERSION:

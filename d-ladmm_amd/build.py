@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 UNITS = ("dladmm_capi.hip", "dladmm_fused.hip", "dladmm_layered.hip", "dladmm_backward.hip",
-         "dladmm_lskm.hip")
+         "dladmm_lskm.hip", "dladmm_eval.hip")
 HEADERS = (os.path.join(ROOT, "include", "dladmm.h"), os.path.join(CSRC, "dladmm_common.h"),
            os.path.join(CSRC, "dladmm_internal.h"), os.path.join(CSRC, "dladmm_slice.h"))
 OUT = os.path.join(HERE, "lib", "libdladmm_hip.so")

@@ -50,6 +50,17 @@ __global__ __launch_bounds__(256) void pack_frags_kernel(const PackArgs p) {
 }
 
 // ------------------------------------------------------------------------ loss reduction
+// per-column objective terms: out[r][b] = sum_s part[r][s][b] over the slices, in order
+__global__ __launch_bounds__(256) void col_loss_kernel(const float* part, int nslice, int ldl,
+                                                       int B, float* out) {
+  const int r = blockIdx.y;
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  float s = 0.0f;
+  for (int sl = 0; sl < nslice; ++sl) s += part[((int64_t)r * nslice + sl) * ldl + b];
+  out[(int64_t)r * B + b] = s;
+}
+
 // sums[i] = sum_w part[i][w] in fp64, fixed order (bitwise reproducible)
 __global__ __launch_bounds__(256) void loss_reduce_kernel(const float* part, int nw, double* sums) {
   __shared__ double red[256];
@@ -86,7 +97,8 @@ struct Plan {
   int shape, MP, NP, tiles;
   // per-layer
   int KB1, KB2, SB1, SB2, MBp1, MBp2, slices1, slices2, gx;
-  int nslots;  // loss partial slots per (layer, term)
+  int nslots;  // loss partials per (layer, term): slices x ldl per-column entries
+  int ldl;     // columns per slice
   size_t off_ap, off_wp, off_v, off_zw, off_ew, off_lw, off_loss, total;
 };
 
@@ -103,6 +115,7 @@ inline int validate(const dladmm_fwd_desc* d) {
   for (int k = 0; k < d->layers; ++k)
     if (!d->W[k]) return DLADMM_E_NULL;
   if (d->loss_kind && !d->loss_sums) return DLADMM_E_NULL;
+  if (d->col_loss && !d->loss_kind) return DLADMM_E_UNSUPPORTED;
   const int v = d->variant;
   if (v == DLADMM_V2_LTHETA || v == DLADMM_V3_FULL) {
     if (!d->row_params) return DLADMM_E_NULL;
@@ -153,7 +166,8 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
     p->MP = kShapeMP[s];
     p->NP = kShapeNP[s];
     p->tiles = ceil_div(d->batch, kTileCols);
-    p->nslots = p->tiles * kWaves;
+    p->ldl = p->tiles * kTileCols;
+    p->nslots = p->ldl;  // one slice
     const size_t frag_bytes = (size_t)p->MP * p->NP * sizeof(float);
     p->off_ap = 0;
     p->off_wp = align256(frag_bytes);
@@ -173,7 +187,8 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
   p->slices1 = p->MBp1 / p->SB1;
   p->slices2 = p->MBp2 / p->SB2;
   p->gx = ceil_div(d->batch, kLayerCols);
-  p->nslots = p->gx * (p->slices1 > p->slices2 ? p->slices1 : p->slices2) * kLayerWaves;
+  p->ldl = p->gx * kLayerCols;
+  p->nslots = p->ldl * (p->slices1 > p->slices2 ? p->slices1 : p->slices2);
   const size_t fb = (size_t)kFrag * sizeof(float);
   p->off_ap = 0;
   p->off_wp = align256(fb * p->KB2 * p->MBp2);
@@ -223,7 +238,7 @@ inline int run_fused(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStrea
   // 2. the fused K-layer forward
   FusedArgs a{};
   a.m = d->m; a.n = d->n; a.B = d->batch; a.K = d->layers;
-  a.keep_all = d->keep_all ? 1 : 0; a.loss_kind = d->loss_kind; a.nwaves = p.nslots;
+  a.keep_all = d->keep_all ? 1 : 0; a.loss_kind = d->loss_kind; a.ldl = p.ldl;
   a.X = d->X; a.ldx = d->ld_x;
   a.Z0 = d->Z0; a.ldz0 = d->ld_z0;
   a.E0 = d->E0; a.lde0 = d->ld_e0;
@@ -273,7 +288,7 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
   const int64_t zl = (int64_t)n * ldo, ml = (int64_t)m * ldo;
   LayerArgs a{};
   a.m = m; a.n = n; a.B = d->batch; a.K = K;
-  a.loss_kind = d->loss_kind; a.nslots = p.nslots;
+  a.loss_kind = d->loss_kind; a.nslots = p.nslots; a.ldl = p.ldl;
   a.X = d->X; a.ldx = d->ld_x;
   a.Vo = V; a.ldv = B;
   a.scal = d->scalar_params;
@@ -560,11 +575,17 @@ int dladmm_fwd_f32(const dladmm_fwd_desc* d, void* stream) {
   char* ws = (char*)d->workspace;
   const int rc = p.path == 1 ? run_fused(d, p, ws, s) : run_layered(d, p, ws, s);
   if (rc) return rc;
-  // per-layer loss sums, fixed-order fp64 reduction of the per-wave partials
+  // per-layer loss sums, fixed-order fp64 reduction of the per-column partials
   if (d->loss_kind) {
     hipLaunchKernelGGL(loss_reduce_kernel, dim3(2 * d->layers), dim3(256), 0, s,
                        (const float*)(ws + p.off_loss), p.nslots, d->loss_sums);
     if (hipError_t e = hipGetLastError()) return (int)e;
+    if (d->col_loss) {
+      hipLaunchKernelGGL(col_loss_kernel, dim3(ceil_div(d->batch, 256), 2 * d->layers),
+                         dim3(256), 0, s, (const float*)(ws + p.off_loss), p.nslots / p.ldl,
+                         p.ldl, d->batch, d->col_loss);
+      if (hipError_t e = hipGetLastError()) return (int)e;
+    }
   }
   return 0;
 }

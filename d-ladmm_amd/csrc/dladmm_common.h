@@ -95,6 +95,13 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
   static_for_impl(fn, std::make_integer_sequence<int, N>{});
 }
 
+// sum over the 4 lane groups that share a batch column (lanes l, l^16, l^32, l^48)
+__device__ __forceinline__ float col_sum(float v) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -284,15 +284,16 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     pin_agpr(Vr[b][r]);
     if (r == 3) mw.next();
   };
-  // per-wave partial objective of layer k (k < 0: just reset the prologue's sums)
+  // per-column objective of layer k (k < 0: just reset the prologue's sums): the column's
+  // rows are spread over the 4 lane groups
   auto flush_loss = [&](int k) {
     if (lossz && k >= 0) {
-      const float rs = wave_sum(regsum);
-      const float fs = lasso ? 0.5f * wave_sum(fit2) : wave_sum(fit1);
-      if (lane == 0) {
-        const int gw = blockIdx.x * kWaves + w;
-        a.lossp[(int64_t)(2 * k + 0) * a.nwaves + gw] = rs;
-        a.lossp[(int64_t)(2 * k + 1) * a.nwaves + gw] = fs;
+      const float rs = col_sum(regsum);
+      const float fs = lasso ? 0.5f * col_sum(fit2) : col_sum(fit1);
+      if (g == 0) {
+        const int64_t c = (int64_t)blockIdx.x * kTileCols + w * 16 + j;
+        a.lossp[(int64_t)(2 * k + 0) * a.ldl + c] = rs;
+        a.lossp[(int64_t)(2 * k + 1) * a.ldl + c] = fs;
       }
     }
     regsum = 0.f;

@@ -10,7 +10,7 @@ namespace dladmm {
 
 struct FusedArgs {
   int m, n, B, K;
-  int keep_all, loss_kind, nwaves;
+  int keep_all, loss_kind, ldl;   // ldl: columns per row of lossp (tiles * 64)
   int pad0;
   const float* X;  int64_t ldx;
   const float* Z0; int64_t ldz0;
@@ -26,7 +26,7 @@ struct FusedArgs {
   const float* b1e[DLADMM_MAX_LAYERS_V1];
   const float* b2e[DLADMM_MAX_LAYERS_V1];
   float* Zo; float* Eo; float* Lo; float* To; int64_t ldo;
-  float* lossp;      // [K][2][nwaves]
+  float* lossp;      // [K][2][ldl] per-column objective terms
 };
 
 
@@ -48,7 +48,8 @@ constexpr int kLayerCols = 16 * kLayerWaves;        // batch columns per workgro
 
 struct LayerArgs {
   int m, n, B, K, k;          // k = layer index; -1 = prologue (T0, Var0)
-  int loss_kind, nslots;      // loss partial slots per (2k+s) row of lossp
+  int loss_kind, nslots;      // lossp row length: slices * ldl (per slice, per column)
+  int ldl;                    // columns per slice row of lossp (gx * 16 * NW)
   int KB;                     // 16-row blocks of the contraction
   int MBp;                    // packed output row-blocks (padded to the slice size)
   int Krows;                  // valid rows of the B operand

@@ -115,11 +115,12 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_kernel(const LayerArgs a) {
     });
   });
   if (a.lossp && k >= 0 && !(PH == 2)) {
-    const float s = wave_sum(lsum);
-    if (lane == 0) {
-      const int slot = (blockIdx.y * gridDim.x + blockIdx.x) * NW + w;
+    // per-column partial over this slice's rows
+    const float s = col_sum(lsum);
+    if (g == 0) {
       const float v = (PH == 1 && lasso) ? 0.5f * s : s;
-      a.lossp[(int64_t)(2 * k + (PH == 0 ? 0 : 1)) * a.nslots + slot] = v;
+      a.lossp[(int64_t)(2 * k + (PH == 0 ? 0 : 1)) * a.nslots + (int64_t)blockIdx.y * a.ldl +
+              (int64_t)blockIdx.x * (16 * NW) + w * 16 + (lane & 15)] = v;
     }
   }
 }

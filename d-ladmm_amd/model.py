@@ -99,7 +99,7 @@ class _DLADMMBase(nn.Module):
         return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
 
     def run(self, x: torch.Tensor, keep_all: bool = True, loss_kind: int = 0,
-            kernel_events=None):
+            kernel_events=None, want_col_loss: bool = False):
         """Fused forward returning the raw ops.ForwardResult (stacked [K, rows, B] outputs).
         Not differentiable (it is the inference path; `forward` is the differentiable one)."""
         with torch.no_grad():
@@ -107,7 +107,8 @@ class _DLADMMBase(nn.Module):
             return dladmm_forward(
                 self.VARIANT, x, self.A, [w.detach() for w in self._weights()],
                 self.Z0, self.E0, self.L0, keep_all=keep_all, want_T=self.RETURNS_T,
-                loss_kind=loss_kind, kernel_events=kernel_events, **self._tables(dev))
+                loss_kind=loss_kind, kernel_events=kernel_events, want_col_loss=want_col_loss,
+                **self._tables(dev))
 
     def _forward_layers(self, x, nl: int):
         """Run the first `nl` layers; lists Z, E, L (nl entries) and T (nl + 1), differentiable
@@ -134,13 +135,15 @@ class _DLADMMBase(nn.Module):
             return Z, E, L, T
         return Z, E, L
 
-    def layer_objectives(self, x, alpha: float, kind: str = "l1l1", kernel_events=None):
+    def layer_objectives(self, x, alpha: float, kind: str = "l1l1", kernel_events=None,
+                         want_col_loss: bool = False):
         """Forward + the per-layer objective of the reference training loop, fused in-kernel:
         l1l1  alpha*sum(|Z_k|,0).mean() + sum(|X - A Z_k|,0).mean()   main_syn_l1l1_scalar.py:290-294
         lasso alpha*sum(|Z_k|,0).mean() + 0.5*sum((X-A Z_k)^2,0).mean() main_syn_lasso_scalar.py:276-281
-        Returns (ForwardResult, fp64 tensor [K])."""
+        Returns (ForwardResult, fp64 tensor [K]); want_col_loss also fills ForwardResult.col_loss
+        [K, 2, B] with the per-column (sum|Z_k|, fit) terms."""
         lk = {"l1l1": _lib.LOSS_L1L1, "lasso": _lib.LOSS_LASSO}[kind]
-        r = self.run(x, loss_kind=lk, kernel_events=kernel_events)
+        r = self.run(x, loss_kind=lk, kernel_events=kernel_events, want_col_loss=want_col_loss)
         obj = (alpha * r.loss_sums[:, 0] + r.loss_sums[:, 1]) / x.shape[1]
         return r, obj
 

@@ -23,6 +23,7 @@ class ForwardResult:
     L: torch.Tensor          # [K | 1, m, B]
     T: Optional[torch.Tensor]  # [K+1 | 1, m, B] or None
     loss_sums: Optional[torch.Tensor]  # [K, 2] fp64: (sum|Z_k|, fit_k)
+    col_loss: Optional[torch.Tensor] = None  # [K, 2, B] fp32 per-column terms (want_col_loss)
 
 
 def _f32_dev(t: torch.Tensor, name: str) -> torch.Tensor:
@@ -117,7 +118,8 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
                    beta2_elem: Sequence[torch.Tensor] = (),
                    keep_all: bool = True, want_T: bool = True, loss_kind: int = 0,
                    out: Optional[ForwardResult] = None,
-                   kernel_events: Optional[tuple] = None) -> ForwardResult:
+                   kernel_events: Optional[tuple] = None,
+                   want_col_loss: bool = False) -> ForwardResult:
     """Run the whole K-layer forward of `variant` (dladmm_variant) on X's device.
 
     X: (m, B); A: (m, n); W: K tensors (n, m) (fc[k].weight; V5 passes the shared one K times);
@@ -145,6 +147,12 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
     d = _lib.FwdDesc()
     keep = _fill_fwd_desc(d, variant, X, A, W, Z0, E0, L0, scalar_params, row_params, beta1_elem,
                           beta2_elem, keep_all, loss_kind, out)
+    if want_col_loss:
+        if not loss_kind:
+            raise ValueError("dladmm: per-column objectives need loss_kind")
+        if out.col_loss is None:
+            out.col_loss = torch.empty((K, 2, B), device=dev, dtype=torch.float32)
+        d.col_loss = out.col_loss.data_ptr()
     if kernel_events is not None:  # (torch.cuda.Event, torch.cuda.Event) around the fused kernel
         d.ev_kernel_start = kernel_events[0].cuda_event
         d.ev_kernel_stop = kernel_events[1].cuda_event

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DLADMM_ABI_VERSION 2
+#define DLADMM_ABI_VERSION 3
 #define DLADMM_MAX_LAYERS 65536   /* K limit (V4-V6; e.g. the K=2000 KM ground-truth iteration) */
 #define DLADMM_MAX_LAYERS_V1 64   /* V1: per-layer per-sample beta pointer tables */
 
@@ -134,6 +134,11 @@ typedef struct dladmm_fwd_desc {
      fused K-layer kernel (NULL = not recorded) */
   void* ev_kernel_start;
   void* ev_kernel_stop;
+
+  /* optional per-column objective terms (device, needs loss_kind): col_loss[(k*2+t)*batch + b]
+     = sum_i |Z_k[i,b]| (t = 0) and the column's fit term (t = 1) -- the per-sample values the
+     reference's evaluation objectives reduce (test_syn_l1l1_scalar.py:460-478). NULL = off. */
+  float* col_loss;
 } dladmm_fwd_desc;
 
 /* ABI version the library was built with. */
@@ -243,6 +248,29 @@ typedef struct dladmm_safeguard_desc {
 } dladmm_safeguard_desc;
 
 int dladmm_safeguard_f32(const dladmm_safeguard_desc* d, void* stream);
+
+/*
+ * Per-column evaluation objectives over saved layers: for every
+ * layer k and batch column b (fp64 sums over the rows)
+ *   reg[k*batch+b] = sum_i |Z_k|,  fit = sum_i |E_k - T_{k+1}| (L1L1) or 0.5 sum (E_k - T_{k+1})^2
+ *   (LASSO) -- i.e. |X - A Z_k| without re-forming A Z_k --, dz = sum_i (Zref - Z_k)^2,
+ *   de = sum_i (Eref - E_k)^2.
+ * The reference test scripts reduce these per-sample values into NMSE, L1L1, Normalized-L1L1,
+ * GT and Normalized-GT (test_syn_l1l1_scalar.py:436-489).  Any output may be NULL.
+ */
+typedef struct dladmm_colobj_desc {
+  int32_t abi_version;
+  int32_t m, n, batch, layers;
+  int32_t fit_kind;                            /* DLADMM_LOSS_L1L1 / DLADMM_LOSS_LASSO */
+  const float* Z; int64_t z_layer_stride; int64_t ld_z;   /* layer k at Z + k*z_layer_stride */
+  const float* E; int64_t e_layer_stride; int64_t ld_e;
+  const float* T; int64_t t_layer_stride; int64_t ld_t;   /* layer k reads T_{k+1} */
+  const float* Zref; int64_t ld_zref;                      /* n x batch or NULL */
+  const float* Eref; int64_t ld_eref;                      /* m x batch or NULL */
+  double* reg; double* fit; double* dz; double* de;        /* [layers][batch] each, or NULL */
+} dladmm_colobj_desc;
+
+int dladmm_colobj_f32(const dladmm_colobj_desc* d, void* stream);
 
 /* Text for a return code of this library (DLADMM_E_* or hipError_t). */
 const char* dladmm_error_string(int code);

@@ -1,0 +1,113 @@
+"""Evaluation objectives: d-ladmm_amd.objectives on the GPU against
+the literal reference formulas (oracle/dladmm_oracle_eval.py) evaluated on the same forward
+outputs, and the fused per-column objective of the forward kernel."""
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+import problems as P
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def case(dl):
+    from oracle import dladmm_oracle_lskm as ol
+    d = dict(variant="v4", m=64, n=128, B=50, K=5, seed=1170, perturb=0.2, wscale=0.9)
+    inp, sd = P.build_problem(d)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+    net = dl.DLADMMNetLSKM(m=64, n=0, d=128, batch_size=50, A=t(inp["A"]), Z0=t(inp["Z0"]),
+                           E0=t(inp["E0"]), L0=t(inp["L0"]), layers=5, alpha=0.01)
+    net.load_state_dict({k: t(v) for k, v in sd.items()})
+    X = t(inp["X"]).cuda()
+    Z, E, L, T = net(X, True, False, False, K=5)
+    Zp, Ep, Lp, Tp = net(X, False, False, False, K=300)   # ground truth (the scripts use 2000)
+    cpu = lambda seq: [s.cpu().numpy() for s in seq]  # noqa: E731
+    return dict(net=net, inp=inp, X=X, out=(Z, E, L, T), gt=(Zp[-1], Ep[-1], Tp[-1]),
+                np=(cpu(Z), cpu(E), cpu(L), cpu(T)), gtnp=(Zp[-1].cpu().numpy(),
+                                                          Ep[-1].cpu().numpy()))
+
+
+def ev(dl, name, K=5, alpha=0.01):
+    obj = importlib.import_module("d-ladmm_amd.objectives")
+    return obj.Evaluator(name, K, alpha, n_test=50)
+
+
+def test_nmse(dl, case):
+    from oracle import dladmm_oracle_eval as oe
+    inp = case["inp"]
+    e = ev(dl, "NMSE")
+    Zl, El = torch.from_numpy(inp["Zstar"]).cuda(), torch.from_numpy(inp["Estar"]).cuda()
+    Z, E, L, T = case["out"]
+    e.add_batch(case["X"], Z, E, Z_label=Zl, E_label=El)
+    rz, re = oe.nmse_terms(case["np"][0], case["np"][1], inp["Zstar"], inp["Estar"])
+    np.testing.assert_allclose(e.acc, rz, rtol=1e-6)
+    np.testing.assert_allclose(e.acc_e, re, rtol=1e-6)
+    got = e.result(inp["Zstar"], inp["Estar"])
+    ref = 10 * np.log10(rz / 50 / ((inp["Zstar"].astype(np.float64) ** 2).sum() / 50) +
+                        re / 50 / ((inp["Estar"].astype(np.float64) ** 2).sum() / 50))
+    np.testing.assert_allclose(got, ref, rtol=1e-6)
+
+
+@pytest.mark.parametrize("name", ["L1L1", "LASSO"])
+def test_l1l1_lasso(dl, case, name):
+    """X - A Z_k read as E_k - T_{k+1}: equal to the literal A @ Z_k form within fp32 rounding."""
+    from oracle import dladmm_oracle_eval as oe
+    inp = case["inp"]
+    Z, E, L, T = case["out"]
+    e = ev(dl, name)
+    e.add_batch(case["X"], Z, E, T=T)
+    fn = oe.l1l1 if name == "L1L1" else oe.lasso
+    np.testing.assert_allclose(e.acc, fn(case["np"][0], inp["X"], inp["A"], 0.01), rtol=2e-5)
+    e2 = ev(dl, "LASSO-ALL")
+    e2.add_batch(case["X"], Z, E, T=T)
+    np.testing.assert_allclose(e2.result(), oe.lasso(case["np"][0], inp["X"], inp["A"], 0.01,
+                                                     per_sample=True), rtol=2e-5)
+
+
+def test_normalized_and_gt(dl, case):
+    from oracle import dladmm_oracle_eval as oe
+    inp = case["inp"]
+    Z, E, L, T = case["out"]
+    Zg, Eg = case["gtnp"]
+    e = ev(dl, "Normalized-L1L1")
+    e.add_batch(case["X"], Z, E, T=T, gt=case["gt"])
+    np.testing.assert_allclose(e.acc, oe.normalized_l1l1(case["np"][0], inp["X"], inp["A"], 0.01,
+                                                         Zg), rtol=1e-4)
+    e = ev(dl, "GT")
+    e.add_batch(case["X"], Z, E, gt=case["gt"])
+    np.testing.assert_allclose(e.acc, oe.gt(case["np"][0], case["np"][1], Zg, Eg), rtol=1e-6)
+    e = ev(dl, "Normalized-GT")
+    e.add_batch(case["X"], Z, E, gt=case["gt"])
+    np.testing.assert_allclose(e.acc, oe.normalized_gt(case["np"][0], case["np"][1], Zg, Eg),
+                               rtol=1e-6)
+
+
+def test_s_l2(dl, case):
+    from oracle import dladmm_oracle_eval as oe
+    inp = case["inp"]
+    Z, E, L, T = case["out"]
+    e = ev(dl, "S-L2")
+    e.add_batch(case["X"], Z, E, L=L, T=T, model=case["net"])
+    ref = oe.s_l2(*case["np"], inp["X"], inp["A"], inp["E0"], 0.01,
+                  float(case["net"].L.reshape(())))
+    np.testing.assert_allclose(e.acc, ref, rtol=1e-4)
+
+
+def test_fused_per_column_objective(dl, case):
+    """The forward kernel's per-column objective terms (loss_kind + col_loss) sum to its per-layer
+    sums and match the literal formula per sample."""
+    from oracle import dladmm_oracle_eval as oe
+    inp = case["inp"]
+    net = case["net"]
+    r, obj = net.layer_objectives(case["X"], 0.01, "l1l1", want_col_loss=True)
+    cl = r.col_loss.double().cpu().numpy()                      # [K, 2, B]
+    np.testing.assert_allclose(cl.sum(2), r.loss_sums.cpu().numpy(), rtol=1e-6)
+    per = 0.01 * cl[:, 0, :] + cl[:, 1, :]
+    Zs = [r.Z[k].cpu().numpy() for k in range(5)]
+    ref = np.stack([0.01 * np.abs(z).sum(0) + np.abs(inp["X"].astype(np.float64) -
+                    inp["A"].astype(np.float64) @ z).sum(0) for z in Zs])
+    np.testing.assert_allclose(per, ref, rtol=2e-5)
+    assert abs(per.sum() - oe.l1l1(Zs, inp["X"], inp["A"], 0.01).sum()) <= 1e-5 * per.sum()
