@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 METRIC = "samples/sec through d=15 D-LADMM forward (m=256,n=512); %HBM-roofline"
 PEAK_F32_MFMA = 157.3e12   # MI355X_MICROARCH.md: fp32 matrix 157.3 TF/s (spec; 155 measured)
 PEAK_HBM = 8.0e12          # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+PEAK_BF16_MFMA = 2.5e15    # MI355X_MICROARCH.md: ~2.5 PF/s dense bf16 MFMA
 
 
 def parse():
@@ -48,6 +49,9 @@ def parse():
                          "(config 4: --m 512 --n 2048 --layers 40)")
     ap.add_argument("--alpha", type=float, default=0.001)
     ap.add_argument("--lean", action="store_true", help="write only the last layer (not default)")
+    ap.add_argument("--precision", default="f32", choices=["f32", "bf16"],
+                    help="bf16 = BASELINE config 5 mode (bf16 MFMA operands, fp32 state): "
+                         "--precision bf16 --m 1024 --n 4096 --batch 16384")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=8192, help="columns of the CPU sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -117,6 +121,7 @@ def main():
     A, X, Z0, E0, L0 = synth(m, n, B, rank, dev)
     cls = {"v4": dl.DLADMMNetScalar, "v6": dl.DLADMMNetLasso}[a.variant]
     net = cls(m=m, n=0, d=n, batch_size=B, A=A, Z0=Z0, E0=E0, L0=L0, layers=K)
+    net.precision = a.precision
     lk = dl._lib.LOSS_L1L1 if a.variant == "v4" else dl._lib.LOSS_LASSO
     net.requires_grad_(False)
     keep_all = not a.lean
@@ -159,14 +164,15 @@ def main():
     obj = obj.cpu().numpy()
 
     if rank == 0:
-        path = "fused" if (m <= 256 and n <= 512 and os.environ.get("DLADMM_PATH", "")[:1] != "l") \
-            else "per-layer"
+        path = "fused" if (m <= 256 and n <= 512 and os.environ.get("DLADMM_PATH", "")[:1] != "l"
+                           and a.precision == "f32") else "per-layer"
+        peak = PEAK_BF16_MFMA if a.precision == "bf16" else PEAK_F32_MFMA
         kname = ("dladmm::fused_kernel (one launch)" if path == "fused" else
                  f"dladmm::layer_kernel x {2 * K + 1} launches (timed together)")
         total = B * world * a.steps
         value = total / elapsed
         flop = (4 * K + 2) * m * n * B                      # per launch (one rank's shard)
-        achieved = flop / kern_avg
+        achieved = flop / kern_avg  # noqa
         # algorithmic HBM bytes per sample (SURVEY 8d, V4 API-parity): inputs X,Z0,E0,L0 +
         # outputs Z,E,L (K layers) + T (K+1); weights (K+1)*m*n*4 per launch
         bytes_io = 4 * ((m + n + 2 * m) + K * (n + 2 * m) + (K + 1) * m) if keep_all else \
@@ -192,7 +198,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32" if a.precision == "f32" else "bf16 operands / f32 state",
             "data": "synthetic (gen_syn_data.py distribution generated on device; reference-init "
                     "V4 parameters, random W = 0.4(A^T + 1e-3 N))",
             "config": {
@@ -208,9 +214,9 @@ def main():
             "roofline": {
                 "bound": "mfma",
                 "achieved": achieved / 1e12,
-                "peak": PEAK_F32_MFMA / 1e12,
+                "peak": peak / 1e12,
                 "unit": "TFLOP/s",
-                "frac": achieved / PEAK_F32_MFMA,
+                "frac": achieved / peak,
                 "traffic": traffic,
                 "kernel": kname,
                 "kernel_ms": kern_avg * 1e3,

@@ -12,7 +12,8 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DLADMM_LIB") or os.path.join(HERE, "lib", "libdladmm_hip.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
+PREC_F32, PREC_BF16 = 0, 1
 MAX_LAYERS = 65536
 MAX_LAYERS_V1 = 64
 NSCALAR = 8
@@ -58,6 +59,7 @@ class FwdDesc(ctypes.Structure):
         ("workspace", _fp), ("workspace_bytes", ctypes.c_size_t),
         ("ev_kernel_start", _fp), ("ev_kernel_stop", _fp),
         ("col_loss", _fp),
+        ("precision", _i32), ("pad1", _i32),
     ]
 
 

@@ -22,6 +22,7 @@ struct PackArgs {
   const float* scal;   // device [T][DLADMM_NSCALAR] (V4-V6 s1) or null
   int trans;           // 1: pack the transpose (element (row, c) = src[c][row])
   int t0;              // scal row of source t is t0 + t
+  int bf16;            // 1: v_mfma_f32_16x16x32_bf16 A fragments (16 x 32, 8 bf16 per lane)
 };
 static_assert(sizeof(PackArgs) <= 2048, "kernel argument size");
 
@@ -38,6 +39,22 @@ __global__ __launch_bounds__(256) void pack_frags_kernel(const PackArgs p) {
   else { const int64_t q = fr >> 1; jb = (int)(q % p.CB); ib = 2 * (int)(q / p.CB) + (int)(fr & 1); }
   const float f = p.sign * (p.scal ? p.scal[(p.t0 + t) * DLADMM_NSCALAR + DLADMM_P_S1] : 1.0f);
   const int row = 16 * ib + (lane & 15);
+  if (p.bf16) {
+    // lane l: M[16 ib + (l & 15)][32 jb + 8 (l >> 4) + j], j = 0..7, rounded to bf16 (RNE)
+    const int c8 = 32 * jb + 8 * (lane >> 4);
+    const float* s8 = p.src[t];
+    bf16x8 v;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float x = (row < p.R && c8 + q < p.C)
+                          ? f * (p.trans ? s8[(int64_t)(c8 + q) * p.ld + row]
+                                         : s8[(int64_t)row * p.ld + c8 + q])
+                          : 0.0f;
+      v[q] = (__bf16)x;
+    }
+    reinterpret_cast<bf16x8*>(p.dst)[((int64_t)t * p.RB * p.CB + fr) * 64 + lane] = v;
+    return;
+  }
   const int c0 = 16 * jb + 4 * (lane >> 4);
   const float* s = p.src[t];
   f32x4 v;
@@ -116,6 +133,8 @@ inline int validate(const dladmm_fwd_desc* d) {
     if (!d->W[k]) return DLADMM_E_NULL;
   if (d->loss_kind && !d->loss_sums) return DLADMM_E_NULL;
   if (d->col_loss && !d->loss_kind) return DLADMM_E_UNSUPPORTED;
+  if (d->precision != DLADMM_PREC_F32 && d->precision != DLADMM_PREC_BF16)
+    return DLADMM_E_UNSUPPORTED;
   const int v = d->variant;
   if (v == DLADMM_V2_LTHETA || v == DLADMM_V3_FULL) {
     if (!d->row_params) return DLADMM_E_NULL;
@@ -160,7 +179,8 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
   // DLADMM_PATH=layered forces the per-layer kernels (tests / A-B measurements)
   const char* force = getenv("DLADMM_PATH");
   const bool force_layered = force && force[0] == 'l';
-  if (s >= 0 && fits_32bit(d) && !force_layered) {
+  const bool bf16 = d->precision == DLADMM_PREC_BF16;
+  if (s >= 0 && fits_32bit(d) && !force_layered && !bf16) {
     p->path = 1;
     p->shape = s;
     p->MP = kShapeMP[s];
@@ -175,13 +195,13 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
     p->total = p->off_loss + align256((size_t)2 * K * p->nslots * sizeof(float));
     return 0;
   }
-  // per-layer path
-  p->path = 2;
+  // per-layer path (path 3: bf16 operands, k-blocks of 32, slices of 32 output blocks)
+  p->path = bf16 ? 3 : 2;
   const int MB = ceil_div(d->m, 16), NB = ceil_div(d->n, 16);
-  p->KB1 = MB;                       // G1 contracts over m
-  p->KB2 = NB;                       // G2 contracts over n
-  p->SB1 = NB >= 32 ? 32 : 16;       // G1 output rows: n
-  p->SB2 = MB >= 32 ? 32 : 16;       // G2 output rows: m
+  p->KB1 = bf16 ? ceil_div(d->m, 32) : MB;  // G1 contracts over m
+  p->KB2 = bf16 ? ceil_div(d->n, 32) : NB;  // G2 contracts over n
+  p->SB1 = (bf16 || NB >= 32) ? 32 : 16;    // G1 output rows: n
+  p->SB2 = (bf16 || MB >= 32) ? 32 : 16;    // G2 output rows: m
   p->MBp1 = ceil_div(NB, p->SB1) * p->SB1;
   p->MBp2 = ceil_div(MB, p->SB2) * p->SB2;
   p->slices1 = p->MBp1 / p->SB1;
@@ -207,7 +227,7 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
 // most kPackBatch sources per launch.
 inline hipError_t pack(const float* const* srcs, int T, int R, int C, int64_t ld, int RB, int CB,
                        int order, float* dst, hipStream_t s, float sign = 1.0f,
-                       const float* scal = nullptr, int trans = 0, int t0 = 0) {
+                       const float* scal = nullptr, int trans = 0, int t0 = 0, int bf16 = 0) {
   for (int b = 0; b < T; b += kPackBatch) {
     const int nb = T - b < kPackBatch ? T - b : kPackBatch;
     PackArgs pa{};
@@ -215,7 +235,7 @@ inline hipError_t pack(const float* const* srcs, int T, int R, int C, int64_t ld
     for (int t = 0; t < nb; ++t) pa.src[t] = srcs[b + t];
     pa.R = R; pa.C = C; pa.RB = RB; pa.CB = CB; pa.order = order; pa.ld = ld;
     pa.dst = dst + (size_t)b * RB * CB * kFrag;
-    pa.sign = sign; pa.scal = scal;
+    pa.sign = sign; pa.scal = scal; pa.bf16 = bf16;
     hipLaunchKernelGGL(pack_frags_kernel, dim3((RB * CB + 3) / 4, nb), dim3(256), 0, s, pa);
     if (hipError_t e = hipGetLastError()) return e;
   }
@@ -273,11 +293,15 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
   float* Lw = (float*)(ws + p.off_lw);
   float* lossp = (float*)(ws + p.off_loss);
   const size_t wl = (size_t)kFrag * p.KB1 * p.MBp1;  // floats per packed W_k
+  const int bf = p.path == 3 ? 1 : 0;
+  const int sb1 = bf ? -32 : p.SB1, sb2 = bf ? -32 : p.SB2;  // launch code: -32 = bf16
   // 1. pack A (rows m, contraction n) and every W_k (rows n, contraction m), k-major
   const float* asrc[1] = {d->A};
-  if (hipError_t e = pack(asrc, 1, m, n, d->ld_a, p.MBp2, p.KB2, 1, Ap, s)) return (int)e;
+  if (hipError_t e = pack(asrc, 1, m, n, d->ld_a, p.MBp2, p.KB2, 1, Ap, s, 1.0f, nullptr, 0, 0, bf))
+    return (int)e;
   const bool shared = shared_weight(d);
-  if (hipError_t e = pack(d->W, shared ? 1 : K, n, m, d->ld_w, p.MBp1, p.KB1, 1, Wp, s))
+  if (hipError_t e = pack(d->W, shared ? 1 : K, n, m, d->ld_w, p.MBp1, p.KB1, 1, Wp, s, 1.0f,
+                          nullptr, 0, 0, bf))
     return (int)e;
   if (d->loss_kind) {
     if (hipError_t e = hipMemsetAsync(lossp, 0, (size_t)2 * K * p.nslots * sizeof(float), s))
@@ -309,7 +333,7 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
     b.ldo = ldo;
     b.To = (d->T && !lean) ? d->T : nullptr;
     b.b1n_e = v1 ? d->beta1_elem[0] : nullptr;
-    if (hipError_t e = launch_layer(2, d->variant, b, g2, p.SB2, s)) return (int)e;
+    if (hipError_t e = launch_layer(2, d->variant, b, g2, sb2, s)) return (int)e;
   }
   for (int k = 0; k < K; ++k) {
     const bool last = k == K - 1;
@@ -330,7 +354,7 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
     b.S = V; b.ldS = B;
     b.Zprev = Zp; b.ldzp = ldzp;
     b.Zo = Zo; b.ldo = ldout;
-    if (hipError_t e = launch_layer(0, d->variant, b, g1, p.SB1, s)) return (int)e;
+    if (hipError_t e = launch_layer(0, d->variant, b, g1, sb1, s)) return (int)e;
     // G2(k): P = A Z_k -> E_k, L_k, T_{k+1}, Var_{k+1}
     LayerArgs c = a;
     c.k = k; c.KB = p.KB2; c.MBp = p.MBp2; c.Krows = n; c.Wp = Ap;
@@ -343,7 +367,7 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
       c.b2e = d->beta2_elem[k];
       c.b1n_e = k + 1 < K ? d->beta1_elem[k + 1] : nullptr;
     }
-    if (hipError_t e = launch_layer(1, d->variant, c, g2, p.SB2, s)) return (int)e;
+    if (hipError_t e = launch_layer(1, d->variant, c, g2, sb2, s)) return (int)e;
   }
   if (d->ev_kernel_stop) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_stop, s)) return (int)e;
@@ -367,6 +391,7 @@ inline int validate_bwd(const dladmm_bwd_desc* d) {
   if (int e = validate(&d->fwd)) return e;
   const dladmm_fwd_desc& f = d->fwd;
   if (!f.keep_all || !f.T) return DLADMM_E_UNSUPPORTED;
+  if (f.precision != DLADMM_PREC_F32) return DLADMM_E_UNSUPPORTED;  // backward is fp32
   if (!d->gW) return DLADMM_E_NULL;
   if (d->ld_gw < f.m) return DLADMM_E_SHAPE;
   if ((d->gZ || d->gE || d->gL || d->gT) && d->ld_g < f.batch) return DLADMM_E_SHAPE;

@@ -9,6 +9,7 @@
 #include "../../include/dladmm.h"
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 namespace dladmm {
 
@@ -44,6 +45,9 @@ __device__ __forceinline__ float shrink_u(float x, ShrinkP p) {
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma_bf16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
 // LDS-DMA of one 1 KiB fragment: lane l copies 16 B from sbase + voff to ldst + 16 l.

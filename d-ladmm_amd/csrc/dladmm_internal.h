@@ -68,7 +68,8 @@ struct LayerArgs {
 };
 
 // phase 0 = G1 (W_k Var -> Z_k), 1 = G2 (A Z_k -> E_k, L_k, T_{k+1}, Var_{k+1}),
-// 2 = prologue G2 (A Z0 -> T_0, Var_0).  sb = output blocks per slice (16 or 32).
+// 2 = prologue G2 (A Z0 -> T_0, Var_0).  sb = output blocks per slice (16 or 32; -32 = 32 with
+// bf16 operands, k-blocks of 32).
 hipError_t launch_layer(int phase, int variant, const LayerArgs& a, dim3 grid, int sb,
                         hipStream_t s);
 

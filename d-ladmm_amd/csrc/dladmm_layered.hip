@@ -21,9 +21,10 @@
 
 namespace dladmm {
 
-template <int EMODE, int PKIND, int PH, int NW, int SB>
+template <int EMODE, int PKIND, int PH, int NW, int SB, int BF16>
 __global__ __launch_bounds__(NW * 64, 1) void layer_kernel(const LayerArgs a) {
-  __shared__ f32x4 ring[2 * kSliceCF * 64];
+  // fp32: 16-fragment chunks; bf16 (BASELINE config 5): one k-block of SB fragments per chunk
+  __shared__ f32x4 ring[2 * (BF16 ? SB : kSliceCF) * 64];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -36,7 +37,10 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_kernel(const LayerArgs a) {
   const int k = a.k;
 
   f32x4 acc[SB];
-  slice_gemm<NW, SB>(ring, a.Wp, a.MBp, ib0, a.KB, a.S, a.ldS, a.Krows, colc, cv, acc);
+  if constexpr (BF16)
+    slice_gemm_bf16<NW, SB>(ring, a.Wp, a.MBp, ib0, a.KB, a.S, a.ldS, a.Krows, colc, cv, acc);
+  else
+    slice_gemm<NW, SB>(ring, a.Wp, a.MBp, ib0, a.KB, a.S, a.ldS, a.Krows, colc, cv, acc);
 
   // ---------------------------------------------------------------- epilogue
   const bool lasso = a.loss_kind == DLADMM_LOSS_LASSO;
@@ -128,10 +132,12 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_kernel(const LayerArgs a) {
 template <int EM, int PK, int PH>
 hipError_t launch_layer_v(const LayerArgs& a, dim3 grid, int sb, hipStream_t s) {
   constexpr int NW = kLayerWaves;
-  if (sb == 32)
-    hipLaunchKernelGGL((layer_kernel<EM, PK, PH, NW, 32>), grid, dim3(NW * 64), 0, s, a);
+  if (sb == -32)  // bf16 operands (config 5)
+    hipLaunchKernelGGL((layer_kernel<EM, PK, PH, NW, 32, 1>), grid, dim3(NW * 64), 0, s, a);
+  else if (sb == 32)
+    hipLaunchKernelGGL((layer_kernel<EM, PK, PH, NW, 32, 0>), grid, dim3(NW * 64), 0, s, a);
   else
-    hipLaunchKernelGGL((layer_kernel<EM, PK, PH, NW, 16>), grid, dim3(NW * 64), 0, s, a);
+    hipLaunchKernelGGL((layer_kernel<EM, PK, PH, NW, 16, 0>), grid, dim3(NW * 64), 0, s, a);
   return hipGetLastError();
 }
 

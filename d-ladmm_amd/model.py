@@ -98,6 +98,10 @@ class _DLADMMBase(nn.Module):
     def _needs_grad(self) -> bool:
         return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
 
+    # GEMM operand precision of forward / run: "f32" (the reference) or "bf16" (BASELINE config
+    # 5: bf16 MFMA operands, fp32 accumulation and fp32 elementwise state; inference only)
+    precision = "f32"
+
     def run(self, x: torch.Tensor, keep_all: bool = True, loss_kind: int = 0,
             kernel_events=None, want_col_loss: bool = False):
         """Fused forward returning the raw ops.ForwardResult (stacked [K, rows, B] outputs).
@@ -108,7 +112,7 @@ class _DLADMMBase(nn.Module):
                 self.VARIANT, x, self.A, [w.detach() for w in self._weights()],
                 self.Z0, self.E0, self.L0, keep_all=keep_all, want_T=self.RETURNS_T,
                 loss_kind=loss_kind, kernel_events=kernel_events, want_col_loss=want_col_loss,
-                **self._tables(dev))
+                precision=self.precision, **self._tables(dev))
 
     def _forward_layers(self, x, nl: int):
         """Run the first `nl` layers; lists Z, E, L (nl entries) and T (nl + 1), differentiable
@@ -117,6 +121,8 @@ class _DLADMMBase(nn.Module):
             if x.requires_grad:
                 raise RuntimeError("dladmm: gradients w.r.t. the input X are not supported (the "
                                    "reference trains the parameters only)")
+            if self.precision != "f32":
+                raise RuntimeError("dladmm: the bf16 operand mode is inference-only")
             outs = _DLADMMFunction.apply(self, x, nl, *self.parameters())
             return (list(outs[:nl]), list(outs[nl:2 * nl]), list(outs[2 * nl:3 * nl]),
                     list(outs[3 * nl:]))
@@ -124,7 +130,7 @@ class _DLADMMBase(nn.Module):
             tables = _slice_tables(self._tables(self.A.device), nl)
             r = dladmm_forward(self.VARIANT, x, self.A, [w.detach() for w in self._weights()[:nl]],
                                self.Z0, self.E0, self.L0, keep_all=True, want_T=self.RETURNS_T,
-                               **tables)
+                               precision=self.precision, **tables)
         T = [r.T[j] for j in range(nl + 1)] if r.T is not None else None
         return ([r.Z[k] for k in range(nl)], [r.E[k] for k in range(nl)],
                 [r.L[k] for k in range(nl)], T)

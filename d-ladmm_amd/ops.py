@@ -119,7 +119,7 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
                    keep_all: bool = True, want_T: bool = True, loss_kind: int = 0,
                    out: Optional[ForwardResult] = None,
                    kernel_events: Optional[tuple] = None,
-                   want_col_loss: bool = False) -> ForwardResult:
+                   want_col_loss: bool = False, precision: str = "f32") -> ForwardResult:
     """Run the whole K-layer forward of `variant` (dladmm_variant) on X's device.
 
     X: (m, B); A: (m, n); W: K tensors (n, m) (fc[k].weight; V5 passes the shared one K times);
@@ -147,6 +147,9 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
     d = _lib.FwdDesc()
     keep = _fill_fwd_desc(d, variant, X, A, W, Z0, E0, L0, scalar_params, row_params, beta1_elem,
                           beta2_elem, keep_all, loss_kind, out)
+    if precision not in ("f32", "bf16"):
+        raise ValueError(f"dladmm: precision must be 'f32' or 'bf16', got {precision!r}")
+    d.precision = _lib.PREC_BF16 if precision == "bf16" else _lib.PREC_F32
     if want_col_loss:
         if not loss_kind:
             raise ValueError("dladmm: per-column objectives need loss_kind")

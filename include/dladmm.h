@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DLADMM_ABI_VERSION 3
+#define DLADMM_ABI_VERSION 4
 #define DLADMM_MAX_LAYERS 65536   /* K limit (V4-V6; e.g. the K=2000 KM ground-truth iteration) */
 #define DLADMM_MAX_LAYERS_V1 64   /* V1: per-layer per-sample beta pointer tables */
 
@@ -139,7 +139,16 @@ typedef struct dladmm_fwd_desc {
      = sum_i |Z_k[i,b]| (t = 0) and the column's fit term (t = 1) -- the per-sample values the
      reference's evaluation objectives reduce (test_syn_l1l1_scalar.py:460-478). NULL = off. */
   float* col_loss;
+
+  /* GEMM operand precision: DLADMM_PREC_F32 (default; the reference's fp32) or DLADMM_PREC_BF16
+     (BASELINE config 5: A, W_k and the state operands Var / Z_k rounded to bf16 for the MFMAs,
+     fp32 accumulation, every elementwise update -- shrinks, E, dual L, T -- in fp32).  bf16 runs
+     on the per-layer kernels (path 3). */
+  int32_t precision;
+  int32_t pad1;
 } dladmm_fwd_desc;
+
+enum dladmm_precision { DLADMM_PREC_F32 = 0, DLADMM_PREC_BF16 = 1 };
 
 /* ABI version the library was built with. */
 int dladmm_abi_version(void);
@@ -148,7 +157,8 @@ int dladmm_abi_version(void);
 size_t dladmm_fwd_workspace_bytes(const dladmm_fwd_desc* d);
 
 /* Which kernel path this descriptor takes: 1 = fused persistent K-layer kernel,
-   2 = per-layer kernel pair (large shapes), <0 = DLADMM_E_* error. */
+   2 = per-layer kernel pair (large shapes), 3 = per-layer kernels on bf16 operands,
+   <0 = DLADMM_E_* error. */
 int dladmm_fwd_path(const dladmm_fwd_desc* d);
 
 /* Enqueue the whole K-layer forward on `stream` (hipStream_t). */

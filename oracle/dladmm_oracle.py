@@ -39,8 +39,29 @@ def self_active(x, theta):
     return np.maximum(x - theta, 0) - np.maximum(-1.0 * x - theta, 0)
 
 
+_GEMM = None  # None: fp32 BLAS as the reference; "bf16": see round_bf16 / forward(gemm=...)
+
+
+def round_bf16(x):
+    """fp32 -> bf16 -> fp32, round to nearest even (what the bf16 path feeds its MFMAs)."""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32)
+    r = ((u.astype(np.uint64) + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return r.astype(np.uint32).view(np.float32).reshape(np.shape(x))
+
+
+def _mm(a, b):
+    """The GEMMs of the forward: fp32 (reference) or, for the bf16 operand mode of BASELINE
+    config 5, both operands rounded to bf16 and the product accumulated in fp64, stored fp32."""
+    if _GEMM == "bf16":
+        return (round_bf16(a).astype(np.float64) @ round_bf16(b).astype(np.float64)).astype(
+            np.float32)
+    return a @ b
+
+
 def _fc(W, Var):
     """nn.Linear(m, d, bias=False) applied as fc[k](Var.t()).t()  (main_lena.py:72)."""
+    if _GEMM == "bf16":
+        return _mm(W, Var)
     return (Var.T @ W.T).T
 
 
@@ -63,21 +84,32 @@ def forward_news(variant, X, A, Z0, E0, L0, p, K, dtype):
         if k == 0:
             E.append(E0)
             L.append(L0)
-            Tn = A @ Z0 + E0 - X
+            Tn = _mm(A, Z0) + E0 - X
             Varn = L0 + p[f"beta1.{k}"] * Tn
             Z.append(self_active(Z0 - fcW(k, Varn), p[f"active_para.{k}"]))
         else:
-            VVar = L[-1] + p[f"beta2.{k-1}"] * (A @ Z[-1] + E[-1] - X)
+            VVar = L[-1] + p[f"beta2.{k-1}"] * (_mm(A, Z[-1]) + E[-1] - X)
             E.append(self_active(E[-1] - p[f"ss2.{k-1}"] * VVar, p[f"active_para1.{k-1}"]))
-            Tn = A @ Z[-1] + E[-1] - X
+            Tn = _mm(A, Z[-1]) + E[-1] - X
             L.append(L[-1] + p[f"beta3.{k-1}"] * Tn)
             Varn = L[-1] + p[f"beta1.{k}"] * Tn
             Z.append(self_active(Z[-1] - fcW(k, Varn), p[f"active_para.{k}"]))
     return dict(Z=Z, E=E, L=L)
 
 
-def forward(variant, X, A, Z0, E0, L0, state_dict, layers, dtype=np.float32):
-    """Run the reference forward of `variant` ('v1'..'v7p'); returns dict(Z, E, L[, T]) of lists."""
+def forward(variant, X, A, Z0, E0, L0, state_dict, layers, dtype=np.float32, gemm=None):
+    """Run the reference forward of `variant` ('v1'..'v7p'); returns dict(Z, E, L[, T]) of lists.
+    gemm="bf16" restates the bf16-operand mode (BASELINE config 5) instead of the reference's
+    fp32 GEMMs."""
+    global _GEMM
+    prev, _GEMM = _GEMM, gemm
+    try:
+        return _forward(variant, X, A, Z0, E0, L0, state_dict, layers, dtype)
+    finally:
+        _GEMM = prev
+
+
+def _forward(variant, X, A, Z0, E0, L0, state_dict, layers, dtype):
     c = lambda a: np.asarray(a, dtype=dtype)  # noqa: E731
     X, A, Z0, E0, L0 = c(X), c(A), c(Z0), c(E0), c(L0)
     p = {k: c(v) for k, v in state_dict.items()}
@@ -96,11 +128,11 @@ def forward(variant, X, A, Z0, E0, L0, state_dict, layers, dtype=np.float32):
             Lp = L0 if k == 0 else L[-1]
             Zp = Z0 if k == 0 else Z[-1]
             if k == 0:
-                T.append(A @ Z0 + E0 - X)
+                T.append(_mm(A, Z0) + E0 - X)
             Var = Lp + b1 * T[-1]
             Z.append(self_active(Zp - _fc(W, Var), thz))
-            E.append(self_active(X - A @ Z[-1] - b2 * Lp, the))
-            T.append(A @ Z[-1] + E[-1] - X)
+            E.append(self_active(X - _mm(A, Z[-1]) - b2 * Lp, the))
+            T.append(_mm(A, Z[-1]) + E[-1] - X)
             L.append(Lp + b1 * T[-1])
         elif variant in ("v3", "v4", "v5"):
             # main_syn_l1l1_full.py:53-82 (V3), main_syn_l1l1_scalar.py:89-118 (V4),
@@ -112,15 +144,15 @@ def forward(variant, X, A, Z0, E0, L0, state_dict, layers, dtype=np.float32):
             Zp = Z0 if k == 0 else Z[-1]
             Ep = E0 if k == 0 else E[-1]
             if k == 0:
-                T.append(A @ Z0 + E0 - X)
+                T.append(_mm(A, Z0) + E0 - X)
             Var = Lp + b1 * T[-1]
             if variant == "v5":
                 Z.append(self_active(Zp - p[f"ss1.{k}"] * _fc(p["fc.weight"], Var), thz))
             else:
                 Z.append(self_active(Zp - _fc(p[f"fc.{k}.weight"], Var), thz))
-            VVar = Lp + b2 * (A @ Z[-1] + Ep - X)
+            VVar = Lp + b2 * (_mm(A, Z[-1]) + Ep - X)
             E.append(self_active(Ep - ss2 * VVar, the))
-            T.append(A @ Z[-1] + E[-1] - X)
+            T.append(_mm(A, Z[-1]) + E[-1] - X)
             L.append(Lp + b3 * T[-1])
         elif variant == "v6":
             # main_syn_lasso_scalar.py:74-107
@@ -130,12 +162,12 @@ def forward(variant, X, A, Z0, E0, L0, state_dict, layers, dtype=np.float32):
             Lp = L0 if k == 0 else L[-1]
             Zp = Z0 if k == 0 else Z[-1]
             if k == 0:
-                T.append(A @ Z0 + E0 - X)
+                T.append(_mm(A, Z0) + E0 - X)
             Var = Lp + b1 * T[-1]
             Z.append(self_active(Zp - _fc(p[f"fc.{k}.weight"], Var), thz))
-            residual = X - A @ Z[-1]
+            residual = X - _mm(A, Z[-1])
             E.append(s21 * residual - s22 * Lp)
-            T.append(A @ Z[-1] + E[-1] - X)
+            T.append(_mm(A, Z[-1]) + E[-1] - X)
             L.append(Lp + b3 * T[-1])
         else:
             raise ValueError(f"unknown variant {variant!r}")
