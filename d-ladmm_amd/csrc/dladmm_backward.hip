@@ -42,8 +42,15 @@ __device__ __forceinline__ float col16_sum(float v) {
   return v;
 }
 
+#ifndef BWD_EPI_FENCE
+#define BWD_EPI_FENCE 1
+#endif
+#ifndef BWD_MIN_WG
+#define BWD_MIN_WG 2
+#endif
+
 template <int EMODE, int PKIND, int PH, int NW, int SB>
-__global__ __launch_bounds__(NW * 64, 1) void bwd_kernel(const BwdArgs a) {
+__global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs a) {
   __shared__ f32x4 ring[2 * kSliceCF * 64];
 
   const int tid = threadIdx.x;
@@ -64,12 +71,18 @@ __global__ __launch_bounds__(NW * 64, 1) void bwd_kernel(const BwdArgs a) {
 
   cfloat_p sp = (cfloat_p)a.scal + k * DLADMM_NSCALAR;
   const float* rp = a.rowp ? a.rowp + (int64_t)k * 8 * a.rstride : nullptr;
+  // fused training objective coefficients of layer k (0 without one)
+  const float czk = a.loss_kind ? ((cfloat_p)a.lcoef)[2 * k] : 0.0f;
+  const float cfk = a.loss_kind ? ((cfloat_p)a.lcoef)[2 * k + 1] : 0.0f;
+  const bool lossq = a.loss_kind == DLADMM_LOSS_LASSO;
+  // scalar kinds: the layer's parameters, loaded once (uniform registers)
+  float spv[DLADMM_NSCALAR];
+#pragma unroll
+  for (int sl = 0; sl < DLADMM_NSCALAR; ++sl)
+    spv[sl] = (PKIND == PK_ROW) ? 0.0f : sp[sl];
   auto pm = [&](int slot, int rowc) -> float {  // scalar or per-row parameter of layer k
     if constexpr (PKIND == PK_ROW) return rp[(int64_t)slot * a.rstride + rowc];
-    else return sp[slot];
-  };
-  auto up = [&](const float* gp, int rowc) -> float {  // upstream cotangent (NULL = 0)
-    return gp ? gp[(int64_t)rowc * a.ldg + colc] : 0.0f;
+    else return spv[slot];
   };
   const int64_t ldw = a.ldw;  // row stride of the adjoint / operand workspaces
 
@@ -90,27 +103,49 @@ __global__ __launch_bounds__(NW * 64, 1) void bwd_kernel(const BwdArgs a) {
     }
   };
 
+  // operand / adjoint views (uniform row part in soffset; NULL or out-of-range reads 0)
+  const int m = a.m, n = a.n;
+  const BView vX = make_view(a.X, m, a.ldx, g, col, cv);
+  const BView vEp = make_view(a.Ep, m, a.ldep, g, col, cv);
+  const BView vLp = make_view(a.Lp, m, a.ldlp, g, col, cv);
+  const BView vTk = make_view(a.Tk, m, a.ldt, g, col, cv);
+  const BView vZp = make_view(a.Zp, n, a.ldzp, g, col, cv);
+  const BView vgZ = make_view(a.gZ, n, a.ldg, g, col, cv);
+  const BView vgE = make_view(a.gE, m, a.ldg, g, col, cv);
+  const BView vgL = make_view(a.gL, m, a.ldg, g, col, cv);
+  const BView vgT = make_view(a.gT, m, a.ldg, g, col, cv);
+  const BView vAZ = make_view(a.AZ, n, ldw, g, col, cv);
+  const BView vAE = make_view(a.AE, m, ldw, g, col, cv);
+  const BView vAL = make_view(a.AL, m, ldw, g, col, cv);
+  const BView vAT = make_view(a.AT, m, ldw, g, col, cv);
+  const BView vGP = make_view(a.GP, m, ldw, g, col, cv);
+  const BView vVAR = make_view(a.VAR, m, ldw, g, col, cv);
+  const BView vb1 = make_view(PKIND == PK_ELEM ? a.b1e : nullptr, m, a.ldb, g, col, cv);
+  const BView vb2 = make_view(PKIND == PK_ELEM ? a.b2e : nullptr, m, a.ldb, g, col, cv);
+  const BView vgb1 = make_view(PKIND == PK_ELEM ? a.gb1e : nullptr, m, a.ldb, g, col, cv);
+  const BView vgb2 = make_view(PKIND == PK_ELEM ? a.gb2e : nullptr, m, a.ldb, g, col, cv);
+
   static_for<SB>([&](auto I_) {
     constexpr int i = decltype(I_)::value;
     static_for<4>([&](auto R_) {
       constexpr int r = decltype(R_)::value;
       const int row = 16 * (ib0 + i) + 4 * g + r;
+      const uint32_t ru = (uint32_t)(16 * (ib0 + i) + r);  // uniform part of the row
       float pv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if constexpr (PH == 1) {
         // ---------------- BK1: rows of m.  acc = P = A Z_k
-        const bool rok = row < a.m;
+        const bool rok = row < m;
         const bool ok = cv && rok;
         const int rowc = rok ? row : 0;
-        const int64_t o = (int64_t)rowc * ldw + colc;
         const float P = acc[i][r];
-        const float x = a.X[(int64_t)rowc * a.ldx + colc];
-        const float ep = a.Ep[(int64_t)rowc * a.ldep + colc];
-        const float lp = a.Lp[(int64_t)rowc * a.ldlp + colc];
-        const float tk = a.Tk[(int64_t)rowc * a.ldt + colc];
+        const float x = vX.ld(ru);
+        const float ep = vEp.ld(ru);
+        const float lp = vLp.ld(ru);
+        const float tk = vTk.ld(ru);
         float b1, b2 = 0.f, b3;
         if constexpr (PKIND == PK_ELEM) {
-          b1 = a.b1e[(int64_t)rowc * a.ldb + colc];
-          b2 = a.b2e[(int64_t)rowc * a.ldb + colc];
+          b1 = vb1.ld(ru);
+          b2 = vb2.ld(ru);
           b3 = b1;  // main_lena.py:85,89: beta1 serves Var and L
         } else {
           b1 = pm(DLADMM_P_BETA1, rowc);
@@ -118,9 +153,9 @@ __global__ __launch_bounds__(NW * 64, 1) void bwd_kernel(const BwdArgs a) {
           if constexpr (EMODE != EM_LASSO) b2 = pm(DLADMM_P_BETA2, rowc);
         }
         // incoming adjoints of L_k, T_{k+1}, E_k
-        const float aL = a.AL[o] + up(a.gL, rowc);
-        const float aT = a.AT[o] + up(a.gT, rowc);
-        const float aE = a.AE[o] + up(a.gE, rowc);
+        const float aL = vAL.ld(ru) + vgL.ld(ru);
+        const float aT = vAT.ld(ru) + vgT.ld(ru);
+        const float aE = vAE.ld(ru) + vgE.ld(ru);
         // recompute the forward's E_k and T_{k+1} (same expressions as the forward kernels)
         float e, gP, gEp = 0.f, gLp;
         float t;
@@ -170,23 +205,22 @@ __global__ __launch_bounds__(NW * 64, 1) void bwd_kernel(const BwdArgs a) {
           gLp = aL - ss2b * gEt;
         }
         (void)e;
-        if (a.loss_kind) {
-          // d/dP of cf_k * fit_k: fit = sum|X - P| (torch sgn(0) = 0) or 0.5 sum (X - P)^2
-          const float cf = ((cfloat_p)a.lcoef)[2 * k + 1];
+        {
+          // d/dP of cf_k * fit_k: fit = sum|X - P| (torch sgn(0) = 0) or 0.5 sum (X - P)^2.
+          // Branch-free (cf = 0 without a fused loss: gP - 0 * finite = gP exactly); a per-row
+          // branch here splits the unrolled epilogue and the compiler hoists whole rows.
           const float res = x - P;
-          const float dfit = a.loss_kind == DLADMM_LOSS_LASSO
-                                 ? res : (res > 0.f ? 1.f : (res < 0.f ? -1.f : 0.f));
-          gP = gP - cf * dfit;
+          const float dfit = lossq ? res : (res > 0.f ? 1.f : (res < 0.f ? -1.f : 0.f));
+          gP = gP - cfk * dfit;
         }
-        if (ok) {
-          a.GP[o] = gP;
-          a.AE[o] = gEp;
-          a.AL[o] = gLp;
-          a.VAR[o] = lp + b1 * tk;  // Var_k = L_{k-1} + b1 T_k (main_lena.py:71,85)
-          if constexpr (PKIND == PK_ELEM) {
-            a.gb1e[(int64_t)row * a.ldb + col] = pv[DLADMM_P_BETA3];  // BK3 adds gVar*T_k
-            a.gb2e[(int64_t)row * a.ldb + col] = pv[DLADMM_P_BETA2];
-          }
+        // out-of-range rows / columns: the stores are dropped by the buffer bounds
+        vGP.st(ru, gP);
+        vAE.st(ru, gEp);
+        vAL.st(ru, gLp);
+        vVAR.st(ru, lp + b1 * tk);  // Var_k = L_{k-1} + b1 T_k (main_lena.py:71,85)
+        if constexpr (PKIND == PK_ELEM) {
+          vgb1.st(ru, pv[DLADMM_P_BETA3]);  // BK3 adds gVar*T_k
+          vgb2.st(ru, pv[DLADMM_P_BETA2]);
         }
         if (!ok) {
 #pragma unroll
@@ -197,24 +231,22 @@ __global__ __launch_bounds__(NW * 64, 1) void bwd_kernel(const BwdArgs a) {
                                     (1u << DLADMM_P_SS2B));
       } else if constexpr (PH == 2) {
         // ---------------- BK2: rows of n.  acc = R = A^T gP, acc2 = q = W_k Var_k
-        const bool rok = row < a.n;
+        const bool rok = row < n;
         const bool ok = cv && rok;
         const int rowc = rok ? row : 0;
-        const int64_t o = (int64_t)rowc * ldw + colc;
         const float R = acc[i][r];
         const float q = acc2[i][r];
-        const float zp = a.Zp[(int64_t)rowc * a.ldzp + colc];
+        const float zp = vZp.ld(ru);
         float s1 = 1.0f;
-        if constexpr (PKIND == PK_SCALAR) s1 = sp[DLADMM_P_S1];
+        if constexpr (PKIND == PK_SCALAR) s1 = spv[DLADMM_P_S1];
         // U exactly as the forward kernels formed it: Z_{k-1} - s1 (W_k Var_k)
         const float U = zp - ((PKIND == PK_SCALAR) ? s1 * q : q);
         const float thz = pm(DLADMM_P_THETA_Z, rowc);
-        float gZt = (a.AZ[o] + up(a.gZ, rowc)) + R;
-        if (a.loss_kind) {
+        float gZt = (vAZ.ld(ru) + vgZ.ld(ru)) + R;
+        {
           // d/dZ_k of cz_k * sum|Z_k|, Z_k = S(U, theta_z) recomputed as the forward formed it
-          const float cz = ((cfloat_p)a.lcoef)[2 * k];
           const float z = shrink(U, thz);
-          gZt = gZt + cz * (z > 0.f ? 1.f : (z < 0.f ? -1.f : 0.f));
+          gZt = gZt + czk * (z > 0.f ? 1.f : (z < 0.f ? -1.f : 0.f));
         }
         const SD d = shrink_d(U, thz);
         const float gU = gZt * d.dx;
@@ -222,7 +254,7 @@ __global__ __launch_bounds__(NW * 64, 1) void bwd_kernel(const BwdArgs a) {
         if constexpr (PKIND == PK_SCALAR) {
           pv[DLADMM_P_S1] = -gU * q;  // dU/ds1 = -W Var
         }
-        if (ok) a.AZ[o] = gU;  // adjoint of Z_{k-1}; also BK3's operand and wgrad's gM rows
+        vAZ.st(ru, gU);  // adjoint of Z_{k-1}; also BK3's operand and wgrad's gM rows
         if (!ok) {
 #pragma unroll
           for (int sl = 0; sl < 8; ++sl) pv[sl] = 0.f;
@@ -230,28 +262,35 @@ __global__ __launch_bounds__(NW * 64, 1) void bwd_kernel(const BwdArgs a) {
         row_flush(row, rok, pv, 1u << DLADMM_P_THETA_Z);
       } else {
         // ---------------- BK3: rows of m.  acc = gVar = M_k^T gU
-        const bool rok = row < a.m;
+        const bool rok = row < m;
         const bool ok = cv && rok;
         const int rowc = rok ? row : 0;
-        const int64_t o = (int64_t)rowc * ldw + colc;
         const float gVar = acc[i][r];
-        const float tk = a.Tk[(int64_t)rowc * a.ldt + colc];
+        const float tk = vTk.ld(ru);
         float b1;
-        if constexpr (PKIND == PK_ELEM) b1 = a.b1e[(int64_t)rowc * a.ldb + colc];
+        if constexpr (PKIND == PK_ELEM) b1 = vb1.ld(ru);
         else b1 = pm(DLADMM_P_BETA1, rowc);
         pv[DLADMM_P_BETA1] = gVar * tk;
-        if (ok) {
-          a.AL[o] = a.AL[o] + gVar;
-          a.AT[o] = b1 * gVar;  // adjoint of T_k (main_lena.py:85)
-          if constexpr (PKIND == PK_ELEM)
-            a.gb1e[(int64_t)row * a.ldb + col] = a.gb1e[(int64_t)row * a.ldb + col] + pv[DLADMM_P_BETA1];
-        }
+        vAL.st(ru, vAL.ld(ru) + gVar);
+        vAT.st(ru, b1 * gVar);  // adjoint of T_k (main_lena.py:85)
+        if constexpr (PKIND == PK_ELEM) vgb1.st(ru, vgb1.ld(ru) + pv[DLADMM_P_BETA1]);
         if (!ok) pv[DLADMM_P_BETA1] = 0.f;
         row_flush(row, rok, pv, 1u << DLADMM_P_BETA1);
       }
 #pragma unroll
-      for (int sl = 0; sl < 8; ++sl) ps[sl] += pv[sl];
+      for (int sl = 0; sl < 8; ++sl) {
+        ps[sl] += pv[sl];
+        // materialise the running sum here: otherwise the scheduler sinks the whole serial
+        // chain below the last row and keeps every row's terms live (hundreds of registers)
+        if constexpr (PKIND != PK_ROW) asm volatile("" : "+v"(ps[sl]));
+      }
     });
+    // one output block at a time: bounds the epilogue's live operand loads (register budget
+    // of two workgroups per CU, so one workgroup's epilogue overlaps another's GEMM)
+    if constexpr (BWD_EPI_FENCE) {
+      asm volatile("" ::: "memory");  // no load of the next block moves above this one's stores
+      __builtin_amdgcn_sched_barrier(0);
+    }
   });
   if constexpr (PKIND == PK_SCALAR) {
     const int slot = blockIdx.y * gridDim.x * NW + cg;

@@ -192,3 +192,32 @@ __device__ __forceinline__ void slice_gemm_bf16(f32x4* ring, const float* Wp, in
 }
 
 }  // namespace dladmm
+
+namespace dladmm {
+
+// A [rows][ld] fp32 matrix seen by one lane of a slice epilogue in the C/D layout (lane: column
+// col, rows 16b + 4g + r): a raw buffer resource (NULL or out-of-range rows / columns read 0,
+// stores are dropped) plus the lane's voffset; a row's uniform part goes in soffset, so an access
+// costs no per-lane address arithmetic.  Requires rows * ld * 4 < 2^31 (checked on the host).
+struct BView {
+  rsrc_t r;
+  uint32_t vo, ld4;
+  __device__ __forceinline__ float ld(uint32_t row_u) const {
+    return __builtin_bit_cast(float,
+                              __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo, (int)(row_u * ld4), 0));
+  }
+  __device__ __forceinline__ void st(uint32_t row_u, float v) const {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)vo,
+                                          (int)(row_u * ld4), 0);
+  }
+};
+__device__ __forceinline__ BView make_view(const float* p, int rows, int64_t ld, int g,
+                                           int64_t col, bool cv) {
+  BView v;
+  v.r = mkrsrc(p, p ? (uint32_t)((int64_t)rows * ld * 4) : 0u);
+  v.vo = cv ? (uint32_t)(((int64_t)4 * g * ld + col) * 4) : kOOB;
+  v.ld4 = (uint32_t)(ld * 4);
+  return v;
+}
+
+}  // namespace dladmm
