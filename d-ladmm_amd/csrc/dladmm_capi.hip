@@ -78,15 +78,34 @@ __global__ __launch_bounds__(256) void col_loss_kernel(const float* part, int ns
   out[(int64_t)r * B + b] = s;
 }
 
-// sums[i] = sum_w part[i][w] in fp64, fixed order (bitwise reproducible)
-__global__ __launch_bounds__(256) void loss_reduce_kernel(const float* part, int nw, double* sums) {
-  __shared__ double red[256];
-  const int i = blockIdx.x;
+// Backward scalar-parameter slots: sums[sl] = sum_{w < cnt} part[sl][w], fp64, fixed order.
+// cnt: entries the owning kernel wrote (BK2's slots theta_z / s1 cover the n-row slices, the
+// others the m-row slices).  1024 threads: one launch per layer, no memset of the partials.
+__global__ __launch_bounds__(1024) void param_reduce_kernel(const float* part, int stride,
+                                                            int cnt_m, int cnt_n, double* sums) {
+  __shared__ double red[1024];
+  const int sl = blockIdx.x;
+  const int cnt = (sl == DLADMM_P_THETA_Z || sl == DLADMM_P_S1) ? cnt_n : cnt_m;
   double s = 0.0;
-  for (int wv = threadIdx.x; wv < nw; wv += 256) s += (double)part[(int64_t)i * nw + wv];
+  for (int w = threadIdx.x; w < cnt; w += 1024) s += (double)part[(int64_t)sl * stride + w];
   red[threadIdx.x] = s;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
+  for (int o = 512; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) sums[sl] = red[0];
+}
+
+// sums[i] = sum_w part[i][w] in fp64, fixed order (bitwise reproducible)
+__global__ __launch_bounds__(1024) void loss_reduce_kernel(const float* part, int nw, double* sums) {
+  __shared__ double red[1024];
+  const int i = blockIdx.x;
+  double s = 0.0;
+  for (int wv = threadIdx.x; wv < nw; wv += 1024) s += (double)part[(int64_t)i * nw + wv];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
@@ -392,6 +411,13 @@ inline int validate_bwd(const dladmm_bwd_desc* d) {
   const dladmm_fwd_desc& f = d->fwd;
   if (!f.keep_all || !f.T) return DLADMM_E_UNSUPPORTED;
   if (f.precision != DLADMM_PREC_F32) return DLADMM_E_UNSUPPORTED;  // backward is fp32
+  // the backward epilogues address every per-layer matrix with 32-bit buffer offsets
+  if (!fits_32bit(&f)) return DLADMM_E_UNSUPPORTED;
+  {
+    const int64_t mx = f.m > f.n ? f.m : f.n, lim = (int64_t)1 << 31;
+    const int64_t bpad = (f.batch + 15) / 16 * 16;
+    if (mx * bpad * 4 >= lim || mx * d->ld_g * 4 >= lim) return DLADMM_E_UNSUPPORTED;
+  }
   if (!d->gW) return DLADMM_E_NULL;
   if (d->ld_gw < f.m) return DLADMM_E_SHAPE;
   if ((d->gZ || d->gE || d->gL || d->gT) && d->ld_g < f.batch) return DLADMM_E_SHAPE;
@@ -511,7 +537,10 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
     if (hipError_t e = pack(wsrc, 1, m, n, f.ld_w, p.MBpm, p.NB, 1, Mt, s, -1.0f,
                             has_s1 ? f.scalar_params : nullptr, 1, k))
       return (int)e;
-    if (hipError_t e = hipMemsetAsync(part, 0, part_bytes, s)) return (int)e;
+    // scalar kinds: every slot's entries are rewritten per layer (counts fixed), so the
+    // partials are zeroed once; per-row kinds re-zero (rows past m/n are never written)
+    if (rowk || k == K - 1)
+      if (hipError_t e = hipMemsetAsync(part, 0, part_bytes, s)) return (int)e;
     a.k = k;
     a.Ep = k ? f.E + (k - 1) * ml : f.E0; a.ldep = k ? ldo : f.ld_e0;
     a.Lp = k ? f.L + (k - 1) * ml : f.L0; a.ldlp = k ? ldo : f.ld_l0;
@@ -554,12 +583,14 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
       return (int)e;
     // parameter slots: fixed-order fp64 sums of the per-wave partials
     if (v >= DLADMM_V4_SCALAR) {
-      hipLaunchKernelGGL(loss_reduce_kernel, dim3(DLADMM_NSCALAR), dim3(256), 0, s,
-                         (const float*)part, p.nslots, d->g_scalar + (int64_t)k * DLADMM_NSCALAR);
+      hipLaunchKernelGGL(param_reduce_kernel, dim3(DLADMM_NSCALAR), dim3(1024), 0, s,
+                         (const float*)part, p.nslots, p.gx * kBwdWaves * p.slices_m,
+                         p.gx * kBwdWaves * p.slices_n,
+                         d->g_scalar + (int64_t)k * DLADMM_NSCALAR);
       if (hipError_t e = hipGetLastError()) return (int)e;
     } else if (rowk) {
       hipLaunchKernelGGL(loss_reduce_kernel, dim3((unsigned)(DLADMM_NSCALAR * f.row_stride)),
-                         dim3(256), 0, s, (const float*)part, p.ncg,
+                         dim3(1024), 0, s, (const float*)part, p.ncg,
                          d->g_row + (int64_t)k * DLADMM_NSCALAR * f.row_stride);
       if (hipError_t e = hipGetLastError()) return (int)e;
     }
@@ -602,7 +633,7 @@ int dladmm_fwd_f32(const dladmm_fwd_desc* d, void* stream) {
   if (rc) return rc;
   // per-layer loss sums, fixed-order fp64 reduction of the per-column partials
   if (d->loss_kind) {
-    hipLaunchKernelGGL(loss_reduce_kernel, dim3(2 * d->layers), dim3(256), 0, s,
+    hipLaunchKernelGGL(loss_reduce_kernel, dim3(2 * d->layers), dim3(1024), 0, s,
                        (const float*)(ws + p.off_loss), p.nslots, d->loss_sums);
     if (hipError_t e = hipGetLastError()) return (int)e;
     if (d->col_loss) {
