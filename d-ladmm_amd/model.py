@@ -92,8 +92,19 @@ class _DLADMMBase(nn.Module):
     def _weights(self) -> List[torch.Tensor]:
         return [self.fc[k].weight for k in range(self.layers)]
 
-    def _tables(self, dev) -> dict:  # pragma: no cover - per variant
+    def _build_tables(self, dev) -> dict:  # pragma: no cover - per variant
         raise NotImplementedError
+
+    def _tables(self, dev) -> dict:
+        """Per-layer parameter tables for the C ABI, rebuilt only when a parameter changed
+        (storage or in-place version: optimizer steps and load_state_dict bump it).  Saves the
+        dozens of tiny copy kernels per call that assembling them costs."""
+        key = (str(dev),) + tuple((p.data_ptr(), p._version) for p in self.parameters())
+        c = self.__dict__.get("_tab_cache")
+        if c is None or c[0] != key:
+            c = (key, self._build_tables(dev))
+            self.__dict__["_tab_cache"] = c
+        return c[1]
 
     def _needs_grad(self) -> bool:
         return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
@@ -350,7 +361,7 @@ class DLADMMNet(_DLADMMBase):
         self.active_para = _dev(torch.tensor(0.025, dtype=torch.float32))
         self.active_para1 = _dev(torch.tensor(0.06, dtype=torch.float32))
 
-    def _tables(self, dev):
+    def _build_tables(self, dev):
         K = self.layers
         return dict(
             scalar_params=_scalar_table(K, dev, thz=self.active_para.detach().float(),
@@ -376,7 +387,7 @@ class DLADMMNetLTheta(_DLADMMBase):
         self._plist("active_para1", (self.m, 1), 0.06)
         self.fc = nn.ModuleList([nn.Linear(self.m, self.d, bias=False) for _ in range(self.layers)])
 
-    def _tables(self, dev):
+    def _build_tables(self, dev):
         K, R = self.layers, max(self.m, self.d)
         return dict(row_params=_row_table(K, R, dev, self.m, self.d, b1=self.beta1, b2=self.beta2,
                                           b3=self.beta1, the=self.active_para1,
@@ -400,7 +411,7 @@ class DLADMMNetFull(_DLADMMBase):
         self._plist("active_para1", (self.m, 1), 0.8)
         self.fc = nn.ModuleList([nn.Linear(self.m, self.d, bias=False) for _ in range(self.layers)])
 
-    def _tables(self, dev):
+    def _build_tables(self, dev):
         K, R = self.layers, max(self.m, self.d)
         return dict(row_params=_row_table(K, R, dev, self.m, self.d, b1=self.beta1, b2=self.beta2,
                                           b3=self.beta3, ss2=self.ss2, the=self.active_para1,
@@ -434,7 +445,7 @@ class DLADMMNetScalar(_DLADMMBase):
         self._plist("active_para1", (1, 1), 0.8)
         self.fc = nn.ModuleList([nn.Linear(self.m, self.d, bias=False) for _ in range(self.layers)])
 
-    def _tables(self, dev):
+    def _build_tables(self, dev):
         K = self.layers
         return dict(scalar_params=_scalar_table(
             K, dev, b1=_stack_scalar(self.beta1), b2=_stack_scalar(self.beta2),
@@ -459,7 +470,7 @@ class DLADMMNetScalarTied(DLADMMNetScalar):
     def _weights(self):
         return [self.fc.weight] * self.layers
 
-    def _tables(self, dev):
+    def _build_tables(self, dev):
         K = self.layers
         return dict(scalar_params=_scalar_table(
             K, dev, b1=_stack_scalar(self.beta1), b2=_stack_scalar(self.beta2),
@@ -485,7 +496,7 @@ class DLADMMNetLasso(DLADMMNetScalar):
         self._plist("active_para", (1, 1), 0.2)
         self.fc = nn.ModuleList([nn.Linear(self.m, self.d, bias=False) for _ in range(self.layers)])
 
-    def _tables(self, dev):
+    def _build_tables(self, dev):
         K = self.layers
         return dict(scalar_params=_scalar_table(
             K, dev, b1=_stack_scalar(self.beta1), b3=_stack_scalar(self.beta3),
@@ -540,8 +551,8 @@ class DLADMMNetTiedNewS(DLADMMNetNewS):
     def _weights(self):
         return [self.fc.weight] * self.layers
 
-    def _tables(self, dev):
-        return DLADMMNetScalarTied._tables(self, dev)
+    def _build_tables(self, dev):
+        return DLADMMNetScalarTied._build_tables(self, dev)
 
 
 class DLADMMNetPTiedNewS(DLADMMNetTiedNewS):
