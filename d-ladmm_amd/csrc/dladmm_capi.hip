@@ -101,8 +101,18 @@ __global__ __launch_bounds__(1024) void param_reduce_kernel(const float* part, i
 __global__ __launch_bounds__(1024) void loss_reduce_kernel(const float* part, int nw, double* sums) {
   __shared__ double red[1024];
   const int i = blockIdx.x;
+  const float* row = part + (int64_t)i * nw;
+  // 8 independent running sums per thread (loads in flight), combined in a fixed order
+  double acc8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int wv = threadIdx.x;
+  for (; wv + 7 * 1024 < nw; wv += 8 * 1024) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc8[u] += (double)row[wv + u * 1024];
+  }
+  for (int u = 0; wv < nw; wv += 1024, ++u) acc8[u & 7] += (double)row[wv];
   double s = 0.0;
-  for (int wv = threadIdx.x; wv < nw; wv += 1024) s += (double)part[(int64_t)i * nw + wv];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) s += acc8[u];
   red[threadIdx.x] = s;
   __syncthreads();
   for (int o = 512; o > 0; o >>= 1) {
