@@ -32,3 +32,27 @@ def global_objectives(local_sums: torch.Tensor, alpha: float, total_batch: int,
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(s, op=dist.ReduceOp.SUM, group=group)
     return (alpha * s[:, 0] + s[:, 1]) / total_batch
+
+
+def allreduce_grads(module: torch.nn.Module, group: Optional[dist.ProcessGroup] = None,
+                    average: bool = False) -> None:
+    """Data-parallel training over batch shards: ONE all-reduce of every parameter gradient,
+    flattened into a single bucket (the whole D-LADMM parameter set is a few MB: K weights of
+    n x m plus per-layer scalars), then scattered back.  With `training_loss(..., batch=B_global)`
+    each rank's gradient is its shard's share of the global-batch objective, so SUM (the default)
+    gives the full-batch gradient; `average=True` divides by the world size instead (losses
+    normalised by the local batch)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return
+    ps = [p for p in module.parameters() if p.grad is not None]
+    if not ps:
+        return
+    flat = torch.cat([p.grad.reshape(-1) for p in ps])
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    if average:
+        flat /= dist.get_world_size(group)
+    o = 0
+    for p in ps:
+        n = p.grad.numel()
+        p.grad.copy_(flat[o:o + n].view_as(p.grad))
+        o += n

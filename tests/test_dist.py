@@ -93,3 +93,38 @@ def test_shard_columns_cover_exactly():
                 assert a1 == b0
             sizes = [b - a for a, b in spans]
             assert max(sizes) - min(sizes) <= 1
+
+
+def _grad_worker(rank, world, port, q):
+    import importlib
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    ddist = importlib.import_module("d-ladmm_amd.dist")
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mod = torch.nn.Module()
+    mod.w = torch.nn.Parameter(torch.zeros(3, 4))
+    mod.b = torch.nn.Parameter(torch.zeros(1, 1))
+    mod.w.grad = torch.full((3, 4), float(rank + 1))
+    mod.b.grad = torch.full((1, 1), 10.0 * (rank + 1))
+    ddist.allreduce_grads(mod)
+    q.put((rank, mod.w.grad.clone().numpy(), mod.b.grad.clone().numpy()))
+    dist.destroy_process_group()
+
+
+def test_allreduce_grads_world2():
+    """The data-parallel training helper: one bucketed all-reduce of every parameter grad."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_grad_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in ps:
+        p.join(timeout=60)
+    for _, w, b in res:
+        np.testing.assert_array_equal(w, np.full((3, 4), 3.0))
+        np.testing.assert_array_equal(b, np.full((1, 1), 30.0))
