@@ -43,7 +43,12 @@ hipError_t launch_fused_shape(int shape, int variant, const FusedArgs& a, int gr
 namespace dladmm {
 
 // ---- per-layer path (dladmm_layered.hip)
-constexpr int kLayerWaves = 8;                      // waves per layer-kernel workgroup
+#ifndef DLADMM_LAYER_WAVES
+#define DLADMM_LAYER_WAVES 4
+#endif
+// waves per layer-kernel workgroup: 4 (one per SIMD) with two workgroups per CU, so one
+// workgroup's epilogue (HBM-bound) overlaps the other's MFMA main loop
+constexpr int kLayerWaves = DLADMM_LAYER_WAVES;
 constexpr int kLayerCols = 16 * kLayerWaves;        // batch columns per workgroup
 
 struct LayerArgs {

@@ -22,7 +22,7 @@
 namespace dladmm {
 
 template <int EMODE, int PKIND, int PH, int NW, int SB, int BF16>
-__global__ __launch_bounds__(NW * 64, 1) void layer_kernel(const LayerArgs a) {
+__global__ __launch_bounds__(NW * 64, 8 / NW) void layer_kernel(const LayerArgs a) {
   // fp32: 16-fragment chunks; bf16 (BASELINE config 5): one k-block of SB fragments per chunk
   __shared__ f32x4 ring[2 * (BF16 ? SB : kSliceCF) * 64];
 
