@@ -17,9 +17,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 UNITS = ("dladmm_capi.hip", "dladmm_fused.hip", "dladmm_layered.hip", "dladmm_backward.hip",
-         "dladmm_lskm.hip", "dladmm_eval.hip")
+         "dladmm_lskm.hip", "dladmm_eval.hip", "dladmm_tile_bf16.hip")
 HEADERS = (os.path.join(ROOT, "include", "dladmm.h"), os.path.join(CSRC, "dladmm_common.h"),
-           os.path.join(CSRC, "dladmm_internal.h"), os.path.join(CSRC, "dladmm_slice.h"))
+           os.path.join(CSRC, "dladmm_internal.h"), os.path.join(CSRC, "dladmm_slice.h"),
+           os.path.join(CSRC, "dladmm_layer_epi.h"))
 OUT = os.path.join(HERE, "lib", "libdladmm_hip.so")
 OBJ = os.path.join(HERE, "lib", "obj")
 ARCH = os.environ.get("DLADMM_ARCH", "gfx950")

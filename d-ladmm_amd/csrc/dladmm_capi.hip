@@ -145,7 +145,8 @@ struct Plan {
   int KB1, KB2, SB1, SB2, MBp1, MBp2, slices1, slices2, gx;
   int nslots;  // loss partials per (layer, term): slices x ldl per-column entries
   int ldl;     // columns per slice
-  size_t off_ap, off_wp, off_v, off_zw, off_ew, off_lw, off_loss, total;
+  int nbp;     // bf16 path: 16-column blocks of the packed state
+  size_t off_ap, off_wp, off_v, off_zb, off_zw, off_ew, off_lw, off_loss, total;
 };
 
 inline int validate(const dladmm_fwd_desc* d) {
@@ -224,25 +225,30 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
     p->total = p->off_loss + align256((size_t)2 * K * p->nslots * sizeof(float));
     return 0;
   }
-  // per-layer path (path 3: bf16 operands, k-blocks of 32, slices of 32 output blocks)
+  // per-layer path; path 3 = bf16 operands: 2-D tiles of 256 x 256, k-blocks of 32
   p->path = bf16 ? 3 : 2;
   const int MB = ceil_div(d->m, 16), NB = ceil_div(d->n, 16);
   p->KB1 = bf16 ? ceil_div(d->m, 32) : MB;  // G1 contracts over m
   p->KB2 = bf16 ? ceil_div(d->n, 32) : NB;  // G2 contracts over n
-  p->SB1 = (bf16 || NB >= 32) ? 32 : 16;    // G1 output rows: n
-  p->SB2 = (bf16 || MB >= 32) ? 32 : 16;    // G2 output rows: m
+  p->SB1 = bf16 ? kTileBlocks : (NB >= 32 ? 32 : 16);  // G1 output rows: n
+  p->SB2 = bf16 ? kTileBlocks : (MB >= 32 ? 32 : 16);  // G2 output rows: m
   p->MBp1 = ceil_div(NB, p->SB1) * p->SB1;
   p->MBp2 = ceil_div(MB, p->SB2) * p->SB2;
   p->slices1 = p->MBp1 / p->SB1;
   p->slices2 = p->MBp2 / p->SB2;
-  p->gx = ceil_div(d->batch, kLayerCols);
-  p->ldl = p->gx * kLayerCols;
-  p->nslots = p->ldl * (p->slices1 > p->slices2 ? p->slices1 : p->slices2);
+  const int cols = bf16 ? kBf16TileCols : kLayerCols;
+  p->gx = ceil_div(d->batch, cols);
+  p->ldl = p->gx * cols;
+  p->nbp = p->ldl / 16;
+  // loss partial slots per column: one per slice (bf16 tiles: one per slice and wave row)
+  p->nslots = p->ldl * (p->slices1 > p->slices2 ? p->slices1 : p->slices2) * (bf16 ? 2 : 1);
   const size_t fb = (size_t)kFrag * sizeof(float);
   p->off_ap = 0;
   p->off_wp = align256(fb * p->KB2 * p->MBp2);
   p->off_v = p->off_wp + align256(fb * p->KB1 * p->MBp1 * (shared_weight(d) ? 1 : K));
-  p->off_zw = p->off_v + align256((size_t)d->m * B * sizeof(float));
+  // fp32 Var [m][B], or (bf16) packed Var [KB1][nbp] and packed Z [KB2][nbp] fragments
+  p->off_zb = p->off_v + align256(bf16 ? fb * p->KB1 * p->nbp : (size_t)d->m * B * sizeof(float));
+  p->off_zw = p->off_zb + (bf16 ? align256(fb * p->KB2 * p->nbp) : 0);
   const bool lean = !d->keep_all && K > 1;
   p->off_ew = p->off_zw + (lean ? align256((size_t)d->n * B * sizeof(float)) : 0);
   p->off_lw = p->off_ew + (lean ? align256((size_t)d->m * B * sizeof(float)) : 0);
@@ -323,7 +329,13 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
   float* lossp = (float*)(ws + p.off_loss);
   const size_t wl = (size_t)kFrag * p.KB1 * p.MBp1;  // floats per packed W_k
   const int bf = p.path == 3 ? 1 : 0;
-  const int sb1 = bf ? -32 : p.SB1, sb2 = bf ? -32 : p.SB2;  // launch code: -32 = bf16
+  const int sb1 = p.SB1, sb2 = p.SB2;
+  char* Vb = ws + p.off_v;   // bf16: packed Var_k (B operand of G1)
+  char* Zb = ws + p.off_zb;  // bf16: packed Z_k / Z0 (B operand of G2)
+  auto launch = [&](int phase, const LayerArgs& la, dim3 grid, int sb) -> hipError_t {
+    return bf ? launch_tile_bf16(phase, d->variant, la, grid, s)
+              : launch_layer(phase, d->variant, la, grid, sb, s);
+  };
   // 1. pack A (rows m, contraction n) and every W_k (rows n, contraction m), k-major
   const float* asrc[1] = {d->A};
   if (hipError_t e = pack(asrc, 1, m, n, d->ld_a, p.MBp2, p.KB2, 1, Ap, s, 1.0f, nullptr, 0, 0, bf))
@@ -343,7 +355,8 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
   a.m = m; a.n = n; a.B = d->batch; a.K = K;
   a.loss_kind = d->loss_kind; a.nslots = p.nslots; a.ldl = p.ldl;
   a.X = d->X; a.ldx = d->ld_x;
-  a.Vo = V; a.ldv = B;
+  a.Vo = bf ? nullptr : V; a.ldv = B;
+  a.nbp = p.nbp;
   a.scal = d->scalar_params;
   a.rowp = d->row_params; a.rstride = d->row_stride;
   a.ldb = d->ld_beta;
@@ -358,11 +371,17 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
     LayerArgs b = a;
     b.k = -1; b.KB = p.KB2; b.MBp = p.MBp2; b.Krows = n; b.Wp = Ap;
     b.S = d->Z0; b.ldS = d->ld_z0;
+    if (bf) {
+      if (hipError_t e = pack_state_bf16(d->Z0, d->ld_z0, n, B, p.KB2, p.nbp, Zb, s))
+        return (int)e;
+      b.S = (const float*)Zb;
+      b.Pb = Vb; b.pb_kb = p.KB1;
+    }
     b.Eprev = d->E0; b.ldep = d->ld_e0; b.Lprev = d->L0; b.ldlp = d->ld_l0;
     b.ldo = ldo;
     b.To = (d->T && !lean) ? d->T : nullptr;
     b.b1n_e = v1 ? d->beta1_elem[0] : nullptr;
-    if (hipError_t e = launch_layer(2, d->variant, b, g2, sb2, s)) return (int)e;
+    if (hipError_t e = launch(2, b, g2, sb2)) return (int)e;
   }
   for (int k = 0; k < K; ++k) {
     const bool last = k == K - 1;
@@ -380,14 +399,16 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
     // G1(k): Z_k = S(Z_{k-1} - s1 * W_k Var_k)
     LayerArgs b = a;
     b.k = k; b.KB = p.KB1; b.MBp = p.MBp1; b.Krows = m; b.Wp = Wp + (shared ? 0 : k * wl);
-    b.S = V; b.ldS = B;
+    b.S = bf ? (const float*)Vb : V; b.ldS = B;
     b.Zprev = Zp; b.ldzp = ldzp;
     b.Zo = Zo; b.ldo = ldout;
-    if (hipError_t e = launch_layer(0, d->variant, b, g1, sb1, s)) return (int)e;
+    if (bf) { b.Pb = Zb; b.pb_kb = p.KB2; }
+    if (hipError_t e = launch(0, b, g1, sb1)) return (int)e;
     // G2(k): P = A Z_k -> E_k, L_k, T_{k+1}, Var_{k+1}
     LayerArgs c = a;
     c.k = k; c.KB = p.KB2; c.MBp = p.MBp2; c.Krows = n; c.Wp = Ap;
-    c.S = Zo; c.ldS = ldout;
+    c.S = bf ? (const float*)Zb : Zo; c.ldS = ldout;
+    if (bf && !last) { c.Pb = Vb; c.pb_kb = p.KB1; }  // the last Var feeds nothing
     c.Eprev = Ep; c.ldep = ldep; c.Lprev = Lp; c.ldlp = ldlp;
     c.Eo = Eo; c.Lo = Lo; c.ldo = ldout;
     c.To = d->T ? (lean ? (last ? d->T : nullptr) : d->T + (k + 1) * ml) : nullptr;
@@ -396,7 +417,7 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
       c.b2e = d->beta2_elem[k];
       c.b1n_e = k + 1 < K ? d->beta1_elem[k + 1] : nullptr;
     }
-    if (hipError_t e = launch_layer(1, d->variant, c, g2, sb2, s)) return (int)e;
+    if (hipError_t e = launch(1, c, g2, sb2)) return (int)e;
   }
   if (d->ev_kernel_stop) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_stop, s)) return (int)e;

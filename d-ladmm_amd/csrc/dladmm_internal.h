@@ -70,13 +70,27 @@ struct LayerArgs {
   const float* rowp; int64_t rstride;
   const float* b1e; const float* b2e; const float* b1n_e; int64_t ldb;  // V1 betas
   float* lossp;
+  // bf16 tile path (path 3): S is the PACKED bf16 B operand ([KB][nbp] fragments of 32 rows x
+  // 16 columns); Pb receives this product's output state packed the same way for the next
+  // product (pb_kb k-blocks); Vo is unused there
+  void* Pb; int nbp, pb_kb;
 };
 
 // phase 0 = G1 (W_k Var -> Z_k), 1 = G2 (A Z_k -> E_k, L_k, T_{k+1}, Var_{k+1}),
-// 2 = prologue G2 (A Z0 -> T_0, Var_0).  sb = output blocks per slice (16 or 32; -32 = 32 with
-// bf16 operands, k-blocks of 32).
+// 2 = prologue G2 (A Z0 -> T_0, Var_0).  sb = output blocks per slice (16 or 32).
 hipError_t launch_layer(int phase, int variant, const LayerArgs& a, dim3 grid, int sb,
                         hipStream_t s);
+
+// ---- bf16 2-D tile kernels (dladmm_tile_bf16.hip), BASELINE config 5
+// A workgroup of 8 waves owns a 256 x 256 output tile (16 row blocks x 16 column blocks); both
+// operands are packed bf16 fragments streamed by LDS-DMA through a 4-stage ring.
+constexpr int kTileWaves = 8;
+constexpr int kTileBlocks = 16;                 // row and column blocks per tile
+constexpr int kBf16TileCols = 16 * kTileBlocks;  // batch columns per tile
+hipError_t launch_tile_bf16(int phase, int variant, const LayerArgs& a, dim3 grid, hipStream_t s);
+// Z0 [rows][ld] fp32 -> packed bf16 B operand [KB][nbp] (RNE, zero padding)
+hipError_t pack_state_bf16(const float* S, int64_t ld, int rows, int64_t cols, int KB, int nbp,
+                           void* out, hipStream_t s);
 
 }  // namespace dladmm
 

@@ -18,13 +18,13 @@
 #include "dladmm_common.h"
 #include "dladmm_internal.h"
 #include "dladmm_slice.h"
+#include "dladmm_layer_epi.h"
 
 namespace dladmm {
 
-template <int EMODE, int PKIND, int PH, int NW, int SB, int BF16>
+template <int EMODE, int PKIND, int PH, int NW, int SB>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void layer_kernel(const LayerArgs a) {
-  // fp32: 16-fragment chunks; bf16 (BASELINE config 5): one k-block of SB fragments per chunk
-  __shared__ f32x4 ring[2 * (BF16 ? SB : kSliceCF) * 64];
+  __shared__ f32x4 ring[2 * kSliceCF * 64];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -37,92 +37,41 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void layer_kernel(const LayerArgs 
   const int k = a.k;
 
   f32x4 acc[SB];
-  if constexpr (BF16)
-    slice_gemm_bf16<NW, SB>(ring, a.Wp, a.MBp, ib0, a.KB, a.S, a.ldS, a.Krows, colc, cv, acc);
-  else
-    slice_gemm<NW, SB>(ring, a.Wp, a.MBp, ib0, a.KB, a.S, a.ldS, a.Krows, colc, cv, acc);
+  slice_gemm<NW, SB>(ring, a.Wp, a.MBp, ib0, a.KB, a.S, a.ldS, a.Krows, colc, cv, acc);
 
   // ---------------------------------------------------------------- epilogue
-  const bool lasso = a.loss_kind == DLADMM_LOSS_LASSO;
+  // units of IB output blocks, software-pipelined: the loads of unit u + 1 are issued before
+  // unit u computes and stores (see LayerEpi::load)
+  const LayerEpi<EMODE, PKIND, PH> epi(a);
+  using In = typename LayerEpi<EMODE, PKIND, PH>::In;
+  constexpr int IB = (PH == 0 && PKIND != PK_ROW) ? 4 : 2;
+  constexpr int NU = SB / IB;
   float lsum = 0.f;
-  cfloat_p sp = (cfloat_p)a.scal + (k < 0 ? 0 : k) * DLADMM_NSCALAR;
-  cfloat_p spn = (cfloat_p)a.scal + (k + 1 < a.K ? k + 1 : (k < 0 ? 0 : k)) * DLADMM_NSCALAR;
-  const float* rp = a.rowp ? a.rowp + (int64_t)(k < 0 ? 0 : k) * 8 * a.rstride : nullptr;
-  const float* rpn = a.rowp ? a.rowp + (int64_t)(k + 1 < a.K ? k + 1 : 0) * 8 * a.rstride
-                            : nullptr;
-  auto prow = [&](const float* base, int slot, int row) -> float {  // per-row param
-    return base[(int64_t)slot * a.rstride + row];
+  In buf[2][IB][4];
+  auto load_unit = [&](auto U_) {
+    constexpr int u = decltype(U_)::value;
+#pragma unroll
+    for (int ii = 0; ii < IB; ++ii)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        buf[u & 1][ii][r] = epi.load(16 * (ib0 + u * IB + ii) + 4 * g + r, cv, colc);
   };
-  static_for<SB>([&](auto I_) {
-    constexpr int i = decltype(I_)::value;
-    static_for<4>([&](auto R_) {
-      constexpr int r = decltype(R_)::value;
-      const int row = 16 * (ib0 + i) + 4 * g + r;
-      const float accv = acc[i][r];
-      if constexpr (PH == 0) {
-        // G1: Z_k = S(Z_{k-1} - s1*U, theta_z)
-        const bool ok = cv && row < a.n;
-        const int rowc = ok ? row : 0;
-        float u = accv;
-        if constexpr (PKIND == PK_SCALAR) u = sp[DLADMM_P_S1] * u;
-        const float thz = (PKIND == PK_ROW) ? prow(rp, DLADMM_P_THETA_Z, rowc)
-                                            : sp[DLADMM_P_THETA_Z];
-        const float zp = a.Zprev[(int64_t)rowc * a.ldzp + colc];
-        const float z = shrink(zp - u, thz);
-        if (ok) a.Zo[(int64_t)row * a.ldo + col] = z;
-        lsum += ok ? fabsf(z) : 0.0f;
-      } else {
-        const bool ok = cv && row < a.m;
-        const int rowc = ok ? row : 0;
-        const float P = accv;
-        const float x = a.X[(int64_t)rowc * a.ldx + colc];
-        const float e0 = a.Eprev[(int64_t)rowc * a.ldep + colc];
-        const float l0 = a.Lprev[(int64_t)rowc * a.ldlp + colc];
-        float t, l;
-        if constexpr (PH == 2) {
-          t = (P + e0) - x;  // T0 = A Z0 + E0 - X   main_lena.py:70
-          l = l0;
-        } else {
-          float e;
-          auto pm = [&](int slot) -> float {
-            return (PKIND == PK_ROW) ? prow(rp, slot, rowc) : sp[slot];
-          };
-          if constexpr (EMODE == EM_V1) {
-            const float b2 = (PKIND == PK_ELEM) ? a.b2e[(int64_t)rowc * a.ldb + colc]
-                                                : pm(DLADMM_P_BETA2);
-            e = shrink((x - P) - b2 * l0, pm(DLADMM_P_THETA_E));          // main_lena.py:87
-          } else if constexpr (EMODE == EM_VVAR) {
-            const float vv = l0 + pm(DLADMM_P_BETA2) * ((P + e0) - x);     // scalar :114
-            e = shrink(e0 - pm(DLADMM_P_SS2) * vv, pm(DLADMM_P_THETA_E));  // scalar :115
-          } else {
-            e = pm(DLADMM_P_SS2) * (x - P) - pm(DLADMM_P_SS2B) * l0;        // lasso :102-103
-          }
-          t = (P + e) - x;                                                   // main_lena.py:88
-          const float b3 = (PKIND == PK_ELEM) ? a.b1e[(int64_t)rowc * a.ldb + colc]
-                                              : pm(DLADMM_P_BETA3);
-          l = l0 + b3 * t;                                                   // main_lena.py:89
-          if (ok) {
-            a.Eo[(int64_t)row * a.ldo + col] = e;
-            a.Lo[(int64_t)row * a.ldo + col] = l;
-          }
-          const float res = x - P;
-          lsum += ok ? (lasso ? res * res : fabsf(res)) : 0.0f;
-        }
-        if (ok && a.To) a.To[(int64_t)row * a.ldo + col] = t;
-        // Var of layer k+1 = L + b1*T (main_lena.py:85)
-        float b1n;
-        if constexpr (PKIND == PK_ELEM) b1n = a.b1n_e ? a.b1n_e[(int64_t)rowc * a.ldb + colc] : 0.f;
-        else if constexpr (PKIND == PK_ROW) b1n = prow(rpn, DLADMM_P_BETA1, rowc);
-        else b1n = (k < 0) ? sp[DLADMM_P_BETA1] : spn[DLADMM_P_BETA1];
-        if (ok) a.Vo[(int64_t)row * a.ldv + col] = l + b1n * t;
-      }
-    });
+  load_unit(std::integral_constant<int, 0>{});
+  static_for<NU>([&](auto U_) {
+    constexpr int u = decltype(U_)::value;
+    if constexpr (u + 1 < NU) load_unit(std::integral_constant<int, u + 1>{});
+#pragma unroll
+    for (int ii = 0; ii < IB; ++ii)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        epi.finish(16 * (ib0 + u * IB + ii) + 4 * g + r, col, cv, buf[u & 1][ii][r],
+                   acc[u * IB + ii][r], lsum);
   });
   if (a.lossp && k >= 0 && !(PH == 2)) {
     // per-column partial over this slice's rows
     const float s = col_sum(lsum);
     if (g == 0) {
-      const float v = (PH == 1 && lasso) ? 0.5f * s : s;
+      const float v = (PH == 1 && epi.lasso) ? 0.5f * s : s;
       a.lossp[(int64_t)(2 * k + (PH == 0 ? 0 : 1)) * a.nslots + (int64_t)blockIdx.y * a.ldl +
               (int64_t)blockIdx.x * (16 * NW) + w * 16 + (lane & 15)] = v;
     }
@@ -132,12 +81,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void layer_kernel(const LayerArgs 
 template <int EM, int PK, int PH>
 hipError_t launch_layer_v(const LayerArgs& a, dim3 grid, int sb, hipStream_t s) {
   constexpr int NW = kLayerWaves;
-  if (sb == -32)  // bf16 operands (config 5)
-    hipLaunchKernelGGL((layer_kernel<EM, PK, PH, NW, 32, 1>), grid, dim3(NW * 64), 0, s, a);
-  else if (sb == 32)
-    hipLaunchKernelGGL((layer_kernel<EM, PK, PH, NW, 32, 0>), grid, dim3(NW * 64), 0, s, a);
+  if (sb == 32)
+    hipLaunchKernelGGL((layer_kernel<EM, PK, PH, NW, 32>), grid, dim3(NW * 64), 0, s, a);
   else
-    hipLaunchKernelGGL((layer_kernel<EM, PK, PH, NW, 16, 0>), grid, dim3(NW * 64), 0, s, a);
+    hipLaunchKernelGGL((layer_kernel<EM, PK, PH, NW, 16>), grid, dim3(NW * 64), 0, s, a);
   return hipGetLastError();
 }
 

@@ -121,80 +121,6 @@ __device__ __forceinline__ void slice_gemm(f32x4* ring, const float* Wp, int MBp
 
 namespace dladmm {
 
-// ------------------------------------------------------------------------ bf16 operands
-// BASELINE config 5 (m = 1024, n = 4096): the same slice structure on v_mfma_f32_16x16x32_bf16.
-// The packed operand is bf16 fragments of 16 x 32 (lane l: row l & 15, columns 8(l >> 4) .. +7:
-// still 1 KiB per fragment); the B operand -- the fp32 state (Var or Z_k) -- is read from HBM as
-// 8 rows 32kb + 8g + j of the lane's column and rounded to bf16 in registers.  Accumulation is
-// fp32 (MFMA), and every elementwise state update of the epilogue stays fp32.  A k-block of 32
-// rows feeds SB MFMAs (one per output block), so one ring chunk is a whole k-block (SB
-// fragments, SB KiB), double-buffered.
-__device__ __forceinline__ bf16x8 load_bfrag_bf16(const float* S, int64_t ld, int Krows, int kb,
-                                                  int g, int64_t colc, bool cv) {
-  bf16x8 v;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int row = 32 * kb + 8 * g + q;
-    const bool ok = cv && row < Krows;
-    const float x = S[(int64_t)(ok ? row : 0) * ld + colc];
-    v[q] = (__bf16)(ok ? x : 0.0f);
-  }
-  return v;
-}
-
-template <int NW, int SB>
-__device__ __forceinline__ void slice_gemm_bf16(f32x4* ring, const float* Wp, int MBp, int ib0,
-                                                int KB, const float* S, int64_t ldS, int Krows,
-                                                int64_t colc, bool cv, f32x4 (&acc)[SB]) {
-  constexpr int CF = SB;  // fragments per chunk = one k-block of the slice
-  constexpr int D = 2;
-  constexpr int NBUF = D + 1;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = lane >> 4;
-  auto issue = [&](int kb, int slot) {
-    uint64_t sb = (uint64_t)(Wp + ((int64_t)kb * MBp + ib0) * kFrag);
-    asm volatile("" : "+s"(sb));
-    const float* base = (const float*)sb;
-    f32x4* dst = ring + slot * (CF * 64);
-#pragma unroll
-    for (int i = 0; i < (CF + NW - 1) / NW; ++i) {
-      const int f = i * NW + w;
-      if (CF % NW == 0 || f < CF) glds16(base + f * kFrag, lane * 16, dst + f * 64);
-    }
-  };
-#pragma unroll
-  for (int i = 0; i < SB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  issue(0, 0);
-  bf16x8 bn1 = load_bfrag_bf16(S, ldS, Krows, 0, g, colc, cv);
-  bf16x8 bn2 = load_bfrag_bf16(S, ldS, Krows, 1, g, colc, cv);
-  for (int kb = 0; kb < KB; ++kb) {
-    const bf16x8 bcur = bn1;
-    bn1 = bn2;
-    bn2 = load_bfrag_bf16(S, ldS, Krows, kb + 2, g, colc, cv);
-    const int slot = kb & 1;
-    ring_barrier();
-    issue(kb + 1 < KB ? kb + 1 : 0, slot ^ 1);  // past the end: re-read block 0, never used
-    const bf16x8* rs = reinterpret_cast<const bf16x8*>(ring + slot * (CF * 64));
-    bf16x8 fr[NBUF];
-    static_for<D>([&](auto Dd) {
-      constexpr int d = decltype(Dd)::value;
-      fr[d] = rs[d * 64 + lane];
-    });
-    static_for<CF>([&](auto F_) {
-      constexpr int f = decltype(F_)::value;
-      if constexpr (f + D < CF) fr[(f + D) % NBUF] = rs[(f + D) * 64 + lane];
-      acc[f] = mfma_bf16(fr[f % NBUF], bcur, acc[f]);
-      if constexpr (f % 4 == 3) __builtin_amdgcn_sched_barrier(0);
-    });
-  }
-  ring_barrier();
-}
-
-}  // namespace dladmm
-
-namespace dladmm {
-
 // A [rows][ld] fp32 matrix seen by one lane of a slice epilogue in the C/D layout (lane: column
 // col, rows 16b + 4g + r): a raw buffer resource (NULL or out-of-range rows / columns read 0,
 // stores are dropped) plus the lane's voffset; a row's uniform part goes in soffset, so an access

@@ -78,3 +78,53 @@ def test_bf16_is_inference_only(dl):
     net.precision = "bf16"
     with pytest.raises(RuntimeError):
         net(t(inp["X"]).cuda())
+
+
+@pytest.mark.parametrize("variant", ["v4", "v2", "v6"])
+def test_bf16_multi_tile_ragged(variant, dl, oracle):
+    """Several 256 x 256 tiles in both directions with ragged edges (rows m, n and batch B not
+    multiples of 16 / 32 / 256): the packed-state padding and the per-tile epilogue offsets."""
+    m, n, B, K = 300, 530, 600, 3
+    inp, sd, out = run(dl, variant, m, n, B, K, 9302)
+    args = (variant, inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd, K)
+    rb = oracle.forward(*args, gemm="bf16")
+    r32 = oracle.forward(*args)
+    for i, nm in enumerate("ZEL"):
+        for k in range(K):
+            got = out[i][k].cpu().numpy()
+            scale = nrel(rb[nm][k], r32[nm][k])
+            assert nrel(got, rb[nm][k]) <= max(1e-5, 0.25 * scale), (variant, nm, k)
+            assert nrel(got, r32[nm][k]) <= 1e-5 + 1.25 * scale, (variant, nm, k)
+
+
+def test_bf16_loss_lean_and_determinism(dl):
+    """Fused per-layer objective sums equal the objective recomputed from the returned Z/E/T
+    (fp64, 1e-6 relative: the sums are fp32 partials reduced in fixed order); lean mode returns
+    the full run's last layer bit for bit; two runs are bitwise identical."""
+    m, n, B, K = 288, 544, 520, 4
+    inp = P.make_inputs(m, n, B, 9303)
+    sd = P.make_state_dict("v4", m, n, B, K, inp["A"], 9303, perturb=0.1)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+    net = dl.VARIANTS["v4"](m=m, n=0, d=n, batch_size=B, A=t(inp["A"]), Z0=t(inp["Z0"]),
+                            E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K)
+    net.load_state_dict({k: t(v) for k, v in sd.items()})
+    net.requires_grad_(False)
+    net.cuda()
+    net.precision = "bf16"
+    X = t(inp["X"]).cuda()
+    with torch.no_grad():
+        full = net.run(X, keep_all=True, loss_kind=1)
+        full2 = net.run(X, keep_all=True, loss_kind=1)
+        lean = net.run(X, keep_all=False, loss_kind=1)
+    for a, b in ((full.Z, full2.Z), (full.E, full2.E), (full.L, full2.L), (full.T, full2.T),
+                 (full.loss_sums, full2.loss_sums)):
+        assert torch.equal(a, b)
+    for a, b in ((lean.Z[0], full.Z[-1]), (lean.E[0], full.E[-1]), (lean.L[0], full.L[-1]),
+                 (lean.T[0], full.T[-1]), (lean.loss_sums, full.loss_sums)):
+        assert torch.equal(a, b)
+    ls = full.loss_sums.cpu().numpy()
+    for k in range(K):
+        z = full.Z[k].double().cpu().numpy()
+        res = (full.E[k] - full.T[k + 1]).double().cpu().numpy()   # X - A Z_k = E_k - T_{k+1}
+        assert abs(ls[k, 0] - np.abs(z).sum()) <= 1e-6 * np.abs(z).sum(), k
+        assert abs(ls[k, 1] - np.abs(res).sum()) <= 1e-4 * np.abs(res).sum(), k
