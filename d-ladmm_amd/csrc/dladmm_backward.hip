@@ -20,6 +20,8 @@
 // those of the forward, bit for bit.
 // Parameter gradients of broadcast parameters are reduced per wave (scalars: over the wave; per
 // row: over the wave's 16 columns) into partial buffers and summed in fp64 in a fixed order.
+#include <array>
+
 #include "dladmm_common.h"
 #include "dladmm_internal.h"
 #include "dladmm_slice.h"
@@ -125,10 +127,35 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
   const BView vgb1 = make_view(PKIND == PK_ELEM ? a.gb1e : nullptr, m, a.ldb, g, col, cv);
   const BView vgb2 = make_view(PKIND == PK_ELEM ? a.gb2e : nullptr, m, a.ldb, g, col, cv);
 
-  static_for<SB>([&](auto I_) {
+  // The epilogue is software-pipelined over output blocks: pass 1 (bload) issues every load of
+  // block i + 1 before pass 2 (bfinish) computes and stores block i -- the compiler cannot move a
+  // load above a store it may alias, so element order would pay one memory round trip per block.
+  struct BIn { float x, ep, lp, tk, b1, b2, AL, gL, AT, gT, AE, gE, zp, AZ, gZ, gb1; };
+  auto bload_row = [&](int i, int r) {
+    const uint32_t ru = (uint32_t)(16 * (ib0 + i) + r);  // uniform part of the row
+    BIn v;
+    if constexpr (PH == 1) {
+      v.x = vX.ld(ru); v.ep = vEp.ld(ru); v.lp = vLp.ld(ru); v.tk = vTk.ld(ru);
+      if constexpr (PKIND == PK_ELEM) { v.b1 = vb1.ld(ru); v.b2 = vb2.ld(ru); }
+      v.AL = vAL.ld(ru); v.gL = vgL.ld(ru);
+      v.AT = vAT.ld(ru); v.gT = vgT.ld(ru);
+      v.AE = vAE.ld(ru); v.gE = vgE.ld(ru);
+    } else if constexpr (PH == 2) {
+      v.zp = vZp.ld(ru); v.AZ = vAZ.ld(ru); v.gZ = vgZ.ld(ru);
+    } else {
+      v.tk = vTk.ld(ru);
+      if constexpr (PKIND == PK_ELEM) { v.b1 = vb1.ld(ru); v.gb1 = vgb1.ld(ru); }
+      v.AL = vAL.ld(ru);
+    }
+    return v;
+  };
+  auto bload = [&](auto I_) {
     constexpr int i = decltype(I_)::value;
-    static_for<4>([&](auto R_) {
-      constexpr int r = decltype(R_)::value;
+    return std::array<BIn, 4>{bload_row(i, 0), bload_row(i, 1), bload_row(i, 2),
+                              bload_row(i, 3)};
+  };
+  auto bfinish_row = [&](int i, int r, const BIn& v) {
+    {
       const int row = 16 * (ib0 + i) + 4 * g + r;
       const uint32_t ru = (uint32_t)(16 * (ib0 + i) + r);  // uniform part of the row
       float pv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -138,14 +165,14 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
         const bool ok = cv && rok;
         const int rowc = rok ? row : 0;
         const float P = acc[i][r];
-        const float x = vX.ld(ru);
-        const float ep = vEp.ld(ru);
-        const float lp = vLp.ld(ru);
-        const float tk = vTk.ld(ru);
+        const float x = v.x;
+        const float ep = v.ep;
+        const float lp = v.lp;
+        const float tk = v.tk;
         float b1, b2 = 0.f, b3;
         if constexpr (PKIND == PK_ELEM) {
-          b1 = vb1.ld(ru);
-          b2 = vb2.ld(ru);
+          b1 = v.b1;
+          b2 = v.b2;
           b3 = b1;  // main_lena.py:85,89: beta1 serves Var and L
         } else {
           b1 = pm(DLADMM_P_BETA1, rowc);
@@ -153,9 +180,9 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
           if constexpr (EMODE != EM_LASSO) b2 = pm(DLADMM_P_BETA2, rowc);
         }
         // incoming adjoints of L_k, T_{k+1}, E_k
-        const float aL = vAL.ld(ru) + vgL.ld(ru);
-        const float aT = vAT.ld(ru) + vgT.ld(ru);
-        const float aE = vAE.ld(ru) + vgE.ld(ru);
+        const float aL = v.AL + v.gL;
+        const float aT = v.AT + v.gT;
+        const float aE = v.AE + v.gE;
         // recompute the forward's E_k and T_{k+1} (same expressions as the forward kernels)
         float e, gP, gEp = 0.f, gLp;
         float t;
@@ -236,13 +263,13 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
         const int rowc = rok ? row : 0;
         const float R = acc[i][r];
         const float q = acc2[i][r];
-        const float zp = vZp.ld(ru);
+        const float zp = v.zp;
         float s1 = 1.0f;
         if constexpr (PKIND == PK_SCALAR) s1 = spv[DLADMM_P_S1];
         // U exactly as the forward kernels formed it: Z_{k-1} - s1 (W_k Var_k)
         const float U = zp - ((PKIND == PK_SCALAR) ? s1 * q : q);
         const float thz = pm(DLADMM_P_THETA_Z, rowc);
-        float gZt = (vAZ.ld(ru) + vgZ.ld(ru)) + R;
+        float gZt = (v.AZ + v.gZ) + R;
         {
           // d/dZ_k of cz_k * sum|Z_k|, Z_k = S(U, theta_z) recomputed as the forward formed it
           const float z = shrink(U, thz);
@@ -266,14 +293,14 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
         const bool ok = cv && rok;
         const int rowc = rok ? row : 0;
         const float gVar = acc[i][r];
-        const float tk = vTk.ld(ru);
+        const float tk = v.tk;
         float b1;
-        if constexpr (PKIND == PK_ELEM) b1 = vb1.ld(ru);
+        if constexpr (PKIND == PK_ELEM) b1 = v.b1;
         else b1 = pm(DLADMM_P_BETA1, rowc);
         pv[DLADMM_P_BETA1] = gVar * tk;
-        vAL.st(ru, vAL.ld(ru) + gVar);
+        vAL.st(ru, v.AL + gVar);
         vAT.st(ru, b1 * gVar);  // adjoint of T_k (main_lena.py:85)
-        if constexpr (PKIND == PK_ELEM) vgb1.st(ru, vgb1.ld(ru) + pv[DLADMM_P_BETA1]);
+        if constexpr (PKIND == PK_ELEM) vgb1.st(ru, v.gb1 + pv[DLADMM_P_BETA1]);
         if (!ok) pv[DLADMM_P_BETA1] = 0.f;
         row_flush(row, rok, pv, 1u << DLADMM_P_BETA1);
       }
@@ -284,13 +311,33 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
         // chain below the last row and keeps every row's terms live (hundreds of registers)
         if constexpr (PKIND != PK_ROW) asm volatile("" : "+v"(ps[sl]));
       }
-    });
-    // one output block at a time: bounds the epilogue's live operand loads (register budget
-    // of two workgroups per CU, so one workgroup's epilogue overlaps another's GEMM)
-    if constexpr (BWD_EPI_FENCE) {
-      asm volatile("" ::: "memory");  // no load of the next block moves above this one's stores
-      __builtin_amdgcn_sched_barrier(0);
     }
+  };
+  auto bfinish = [&](auto I_, const std::array<BIn, 4>& in) {
+    constexpr int i = decltype(I_)::value;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bfinish_row(i, r, in[r]);
+  };
+  // BK1 loads up to 12 operands per element: pipelined it needs > 128 registers and loses the
+  // 4-workgroups-per-CU occupancy that hides its latency better, so it runs block by block
+  constexpr bool kPipe = PH != 1;
+  std::array<BIn, 4> cur;
+  if constexpr (kPipe) cur = bload(std::integral_constant<int, 0>{});
+  static_for<SB>([&](auto I_) {
+    constexpr int i = decltype(I_)::value;
+    if constexpr (!kPipe) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bfinish_row(i, r, bload_row(i, r));
+      asm volatile("" ::: "memory");  // no load of the next block moves above this one's stores
+    } else if constexpr (i + 1 < SB) {
+      const auto nxt = bload(std::integral_constant<int, i + 1>{});
+      asm volatile("" ::: "memory");  // block i+1's loads stay above block i's stores
+      bfinish(I_, cur);
+      cur = nxt;
+    } else {
+      bfinish(I_, cur);
+    }
+    if constexpr (BWD_EPI_FENCE) __builtin_amdgcn_sched_barrier(0);
   });
   if constexpr (PKIND == PK_SCALAR) {
     const int slot = blockIdx.y * gridDim.x * NW + cg;
