@@ -327,7 +327,11 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
     constexpr int i = decltype(I_)::value;
     if constexpr (!kPipe) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bfinish_row(i, r, bload_row(i, r));
+      for (int r = 0; r < 4; r += 2) {  // two rows' loads, then their stores
+        const BIn v0 = bload_row(i, r), v1 = bload_row(i, r + 1);
+        bfinish_row(i, r, v0);
+        bfinish_row(i, r + 1, v1);
+      }
       asm volatile("" ::: "memory");  // no load of the next block moves above this one's stores
     } else if constexpr (i + 1 < SB) {
       const auto nxt = bload(std::integral_constant<int, i + 1>{});
