@@ -127,7 +127,11 @@ __device__ __forceinline__ void bstore(rsrc_t r, uint32_t off, float v) {
 }
 // store with a wave-uniform row offset in soffset: no per-lane address arithmetic
 __device__ __forceinline__ void bstore_s(rsrc_t r, uint32_t voff, uint32_t soff, float v) {
+#ifdef DLADMM_ABLATE_NOSTORE  // timing experiment only: drop the store, keep the value live
+  asm volatile("" ::"v"(v));
+#else
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)voff, (int)soff, 0);
+#endif
 }
 typedef const __attribute__((address_space(4))) float* cfloat_p;  // scalar-loaded
 
