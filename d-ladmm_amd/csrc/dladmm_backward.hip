@@ -53,7 +53,9 @@ __device__ __forceinline__ float col16_sum(float v) {
 
 template <int EMODE, int PKIND, int PH, int NW, int SB>
 __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs a) {
-  __shared__ f32x4 ring[2 * kSliceCF * 64];
+  // BK1 keeps 4 workgroups per CU (its latency-bound epilogue needs them): a 2-deep B ring
+  constexpr int NSB = PH == 1 ? 2 : 3;
+  __shared__ f32x4 ring[slice_lds_f4<NW, NSB>()];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -66,10 +68,10 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
   const int k = a.k;
 
   f32x4 acc[SB];
-  slice_gemm<NW, SB>(ring, a.Wp, a.MBp, ib0, a.KB, a.S, a.ldS, a.Krows, colc, cv, acc);
+  slice_gemm<NW, SB, NSB>(ring, a.Wp, a.MBp, ib0, a.KB, a.S, a.ldS, a.Krows, a.B, acc);
   f32x4 acc2[PH == 2 ? SB : 1];
   if constexpr (PH == 2)
-    slice_gemm<NW, SB>(ring, a.Wp2, a.MBp, ib0, a.KB, a.S2, a.ldS2, a.Krows, colc, cv, acc2);
+    slice_gemm<NW, SB, NSB>(ring, a.Wp2, a.MBp, ib0, a.KB, a.S2, a.ldS2, a.Krows, a.B, acc2);
 
   cfloat_p sp = (cfloat_p)a.scal + k * DLADMM_NSCALAR;
   const float* rp = a.rowp ? a.rowp + (int64_t)k * 8 * a.rstride : nullptr;

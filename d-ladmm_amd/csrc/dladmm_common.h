@@ -67,6 +67,28 @@ __device__ __forceinline__ void glds16(const float* sbase, uint32_t voff, f32x4*
       : "memory");
 }
 
+// 4-byte variant: lane i's dword lands at ldst + 4 i (64 lanes = 256 consecutive bytes).
+__device__ __forceinline__ void glds4(const float* sbase, uint32_t voff, void* ldst) {
+  unsigned keep;
+  const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ldst);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "global_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(dst)
+      : "memory");
+}
+
+// Counted form of ring_barrier(): this wave's VM operations except the newest N are complete
+// (the LDS-DMAs that must have landed), its LDS reads are complete, then the barrier.
+template <int N>
+__device__ __forceinline__ void ring_barrier_n() {
+  static_assert(N == 0 || N == 4 || N == 8, "counts used by the slice loop");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // All waves: own LDS-DMA + LDS reads complete, then workgroup barrier.  One opaque statement,
 // so the compiler can neither hoist ring reads above it nor sink earlier ones below it.
 #ifndef DLADMM_SYNC_MODE

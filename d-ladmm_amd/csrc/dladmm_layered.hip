@@ -24,7 +24,7 @@ namespace dladmm {
 
 template <int EMODE, int PKIND, int PH, int NW, int SB>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void layer_kernel(const LayerArgs a) {
-  __shared__ f32x4 ring[2 * kSliceCF * 64];
+  __shared__ f32x4 ring[slice_lds_f4<NW, 3>()];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -37,7 +37,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void layer_kernel(const LayerArgs 
   const int k = a.k;
 
   f32x4 acc[SB];
-  slice_gemm<NW, SB>(ring, a.Wp, a.MBp, ib0, a.KB, a.S, a.ldS, a.Krows, colc, cv, acc);
+  slice_gemm<NW, SB, 3>(ring, a.Wp, a.MBp, ib0, a.KB, a.S, a.ldS, a.Krows, a.B, acc);
 
   // ---------------------------------------------------------------- epilogue
   // units of IB output blocks, software-pipelined: the loads of unit u + 1 are issued before

@@ -19,36 +19,37 @@ namespace dladmm {
 
 constexpr int kSliceCF = 16;  // fragments per ring chunk (16 KiB)
 
-// B operand of one k-block for this lane: rows 16kb + 4g + q (q = 0..3) of column col of
-// S[Krows][ld]; rows >= Krows (padding) and invalid columns read 0.  Branch-free: the address is
-// clamped, the value selected.
-__device__ __forceinline__ f32x4 load_bfrag(const float* S, int64_t ld, int Krows, int kb, int g,
-                                            int64_t colc, bool cv) {
-  f32x4 v;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int row = 16 * kb + 4 * g + q;
-    const bool ok = cv && row < Krows;
-    const float x = S[(int64_t)(ok ? row : 0) * ld + colc];
-    v[q] = ok ? x : 0.0f;
-  }
-  return v;
-}
+// LDS of a slice kernel: the weight ring (2 chunks) followed by the B-operand ring (NSB k-blocks
+// of NW KiB).  One __shared__ array per kernel, so the compiler sees a single LDS object.
+template <int NW, int NSB>
+constexpr int slice_lds_f4() { return 2 * kSliceCF * 64 + NSB * NW * 64; }
 
-// ring: __shared__ f32x4[2 * kSliceCF * 64] of the calling kernel.  Ends with a ring barrier (the
-// speculative prefetch has landed), so the ring may be reused by a second call.
-template <int NW, int SB>
+// ring: __shared__ f32x4[slice_lds_f4<NW, NSB>()] of the calling kernel.  Ends with a ring
+// barrier (the speculative prefetches have landed), so the ring may be reused by a second call.
+//
+// The B operand (4 rows of S, the lane's column) is LDS-DMA'd by the wave itself, NSB - 1
+// k-blocks ahead: 4 dword DMAs per wave and k-block, instruction i bringing rows 4i + (l & 3)
+// of columns (l >> 2) in the order the MFMA lane (column l & 15, rows 4(l >> 4) + q) reads them
+// back with one ds_read_b128.  Rows past Krows are clamped to the last row (the packed weights
+// are zero there, so they add exactly 0) and columns past B to column 0 (discarded outputs).
+// Every VM operation of the loop is an LDS-DMA issued here, so the waits are exact counts: a
+// freshly issued prefetch is never drained by a barrier or a register copy.
+template <int NW, int SB, int NSB = 3>
 __device__ __forceinline__ void slice_gemm(f32x4* ring, const float* Wp, int MBp, int ib0, int KB,
-                                           const float* S, int64_t ldS, int Krows, int64_t colc,
-                                           bool cv, f32x4 (&acc)[SB]) {
+                                           const float* S, int64_t ldS, int Krows, int64_t B,
+                                           f32x4 (&acc)[SB]) {
   constexpr int CF = kSliceCF;
   constexpr int NCI = SB / CF;       // chunks per k-block
   constexpr int D = 2;               // fragment read-ahead
   constexpr int NBUF = D + 2;        // a step consumes a PAIR of fragments: D + 2 in rotation
+  constexpr int WPW = CF / NW;       // weight DMAs per wave and chunk
   static_assert(SB % CF == 0, "slice must be whole chunks");
+  static_assert(CF % NW == 0 && WPW == 4, "4 weight DMAs per wave and chunk (vmcnt counts)");
+  static_assert(NSB == 2 || NSB == 3, "B ring depth");
+  static_assert(NCI <= 2, "vmcnt counts below assume at most 2 chunks per k-block");
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = lane >> 4;
+  f32x4* bring = ring + 2 * CF * 64;
 
   auto chunk_src = [&](int kb, int c) -> const float* {
     return Wp + ((int64_t)kb * MBp + ib0 + c * CF) * kFrag;
@@ -59,9 +60,24 @@ __device__ __forceinline__ void slice_gemm(f32x4* ring, const float* Wp, int MBp
     const float* base = (const float*)sb;
     f32x4* dst = ring + slot * (CF * 64);
 #pragma unroll
-    for (int i = 0; i < (CF + NW - 1) / NW; ++i) {
+    for (int i = 0; i < WPW; ++i) {
       const int f = i * NW + w;
-      if (CF % NW == 0 || f < CF) glds16(base + f * kFrag, lane * 16, dst + f * 64);
+      glds16(base + f * kFrag, lane * 16, dst + f * 64);
+    }
+  };
+  // B DMA lanes: column (l >> 2) of this wave's 16, row offset (l & 3) within each group of 4
+  const int64_t colD = (int64_t)blockIdx.x * (16 * NW) + w * 16 + (lane >> 2);
+  const uint32_t colDo = (uint32_t)(colD < B ? colD : 0);
+  const int rq = lane & 3;
+  auto issue_b = [&](int kb, int slot) {
+    uint64_t sb = (uint64_t)(S + (int64_t)(16 * kb) * ldS);
+    asm volatile("" : "+s"(sb));
+    const int rmax = Krows - 1 - 16 * kb;  // >= 0 for every k-block of the contraction
+    char* dst = reinterpret_cast<char*>(bring + (slot * NW + w) * 64);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 4 * i + rq < rmax ? 4 * i + rq : rmax;
+      glds4((const float*)sb, (uint32_t)(((int64_t)r * ldS + colDo) * 4), dst + 256 * i);
     }
   };
 
@@ -69,24 +85,34 @@ __device__ __forceinline__ void slice_gemm(f32x4* ring, const float* Wp, int MBp
   for (int i = 0; i < SB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   issue(chunk_src(0, 0), 0);
-  f32x4 bn1 = load_bfrag(S, ldS, Krows, 0, g, colc, cv);
-  f32x4 bn2 = load_bfrag(S, ldS, Krows, 1, g, colc, cv);
+  issue_b(0, 0);
+  if constexpr (NSB == 3) issue_b(KB > 1 ? 1 : 0, 1);
   f32x4 fr[NBUF];
   int chunk_id = 0;  // running chunk index (slot = chunk_id & 1)
 
   for (int kb = 0; kb < KB; ++kb) {
-    const f32x4 bcur = bn1;
-    bn1 = bn2;
-    bn2 = load_bfrag(S, ldS, Krows, kb + 2, g, colc, cv);
+    f32x4 bcur;
     static_for<NCI>([&](auto C_) {
       constexpr int c = decltype(C_)::value;
       const int slot = chunk_id & 1;
-      ring_barrier();
+      // VM operations issued after the one awaited (NSB 3): one chunk per k-block -> the B
+      // prefetch issued after this chunk's weights; two -> none at c = 0 (the weights of
+      // (kb, 0) were issued last), the B prefetch at c = 1.  NSB 2: the awaited DMA is the
+      // newest.
+      ring_barrier_n<(NSB == 3 && (NCI == 1 || c == 1)) ? 4 : 0>();
       {  // prefetch the next chunk (past the end: re-read chunk 0, never consumed)
         const int nc = c + 1 < NCI ? c + 1 : 0;
         const int nkb = c + 1 < NCI ? kb : (kb + 1 < KB ? kb + 1 : 0);
         issue(chunk_src(nkb, nc), slot ^ 1);
       }
+      if constexpr (c == 0) {
+        // NSB 3: B(kb+2) right after the next chunk's weights (slot (kb+2) % 3 was last read
+        // at kb - 1, before this barrier)
+        if constexpr (NSB == 3) issue_b(kb + 2 < KB ? kb + 2 : 0, (kb + 2) % 3);
+        bcur = bring[((kb % NSB) * NW + w) * 64 + lane];
+      }
+      // NSB 2: B(kb+1) after the last chunk's weights, into the slot read at kb - 1
+      if constexpr (NSB == 2 && c == NCI - 1) issue_b(kb + 1 < KB ? kb + 1 : 0, (kb + 1) % 2);
       const f32x4* rs = ring + slot * (CF * 64);
       static_for<D>([&](auto Dd) {
         constexpr int d = decltype(Dd)::value;
@@ -114,7 +140,7 @@ __device__ __forceinline__ void slice_gemm(f32x4* ring, const float* Wp, int MBp
       ++chunk_id;
     });
   }
-  ring_barrier();  // drain the speculative prefetch before the ring is reused / the WG exits
+  ring_barrier();  // drain the speculative prefetches before the ring is reused / the WG exits
 }
 
 }  // namespace dladmm
