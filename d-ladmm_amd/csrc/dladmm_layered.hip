@@ -12,9 +12,9 @@
 // Kernel geometry: a workgroup of NW waves owns 16*NW batch columns and a slice of SB output
 // blocks (16*SB rows); wave w owns 16 columns and keeps the slice's SB 16x16 accumulators
 // (4*SB registers).  The contraction runs as a RUNTIME loop over k-blocks of 16: the B operand
-// (4 rows of the state, this lane's column) is loaded straight from HBM two k-blocks ahead, the
-// A operands (packed weights, k-major fragment order) stream through a double-buffered LDS ring
-// by LDS-DMA, shared by the NW waves.  Code size is one k-block of MFMAs, not a whole layer.
+// (4 rows of the state, this lane's column) is LDS-DMA'd two k-blocks ahead, the A operands
+// (packed weights, k-major fragment order) stream through a double-buffered LDS ring by LDS-DMA,
+// shared by the NW waves (dladmm_slice.h).  Code size is one k-block of MFMAs, not a whole layer.
 #include "dladmm_common.h"
 #include "dladmm_internal.h"
 #include "dladmm_slice.h"

@@ -6,9 +6,9 @@
 // C/D layout of v_mfma_f32_16x16x4_f32 (lane l: column l&15, rows 16b + 4(l>>4) + r).
 //   acc[i] += sum_kb  Wp-fragment(kb, ib0+i) * S[16kb + 4g + q][col]
 // The contraction runs as a RUNTIME loop over k-blocks of 16: the B operand (4 rows of S, this
-// lane's column) is loaded straight from HBM two k-blocks ahead, the A operands (packed
-// fragments, k-major order [KB][MBp]) stream through a double-buffered LDS ring by LDS-DMA,
-// shared by the NW waves.  Each output block is ONE accumulation chain in k order starting from
+// lane's column) is LDS-DMA'd by each wave for itself two k-blocks ahead (one ds_read_b128 per
+// k-block), the A operands (packed fragments, k-major order [KB][MBp]) stream through a
+// double-buffered LDS ring by LDS-DMA, shared by the NW waves.  Each output block is ONE accumulation chain in k order starting from
 // zero, so every caller computing the same product with the same packing gets the same bits
 // (the backward recomputes A*Z_k and W_k*Var_k bit-identically to the forward).
 #pragma once
