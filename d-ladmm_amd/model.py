@@ -204,19 +204,27 @@ class _DLADMMBase(nn.Module):
         """Gradients by state_dict key from a BackwardResult of the first `nl` layers (layers
         >= nl were not run: their parameters get no gradient, as in the reference)."""
         out = {}
+        # one fp64 -> fp32 conversion per table; a single-slot gradient is then a view of it
+        # (per-parameter sum / cast ops were ~180 tiny launches per training step)
+        kinds = {kind for kind, _ in self.GRAD_SLOTS.values()}
+        gs32 = res.g_scalar.to(torch.float32) if "scalar" in kinds else None
+        gr32 = res.g_row.to(torch.float32) if "row" in kinds else None
         for name, (kind, slots) in self.GRAD_SLOTS.items():
             for k in range(nl):
                 key = f"{name}.{k}"
                 if kind == "scalar":
-                    g = sum(res.g_scalar[k, s] for s in slots).reshape(1, 1)
+                    g = (gs32[k, slots[0]] if len(slots) == 1 else
+                         sum(res.g_scalar[k, s] for s in slots).to(torch.float32)).reshape(1, 1)
                 elif kind == "row":
                     rows = self.d if slots[0] == _lib.P_THETA_Z else self.m
-                    g = sum(res.g_row[k, s, :rows] for s in slots).reshape(rows, 1)
+                    g = (gr32[k, slots[0], :rows] if len(slots) == 1 else
+                         sum(res.g_row[k, s, :rows] for s in slots).to(torch.float32))
+                    g = g.reshape(rows, 1)
                 elif kind == "elem1":
-                    g = res.g_beta1[k]
+                    g = res.g_beta1[k].to(torch.float32)
                 else:
-                    g = res.g_beta2[k]
-                out[key] = g.to(torch.float32)
+                    g = res.g_beta2[k].to(torch.float32)
+                out[key] = g
         if self._shared_weight():
             out[self._fc_key(0)] = res.gW[0]
         else:
