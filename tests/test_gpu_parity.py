@@ -287,3 +287,26 @@ def test_news_partial_depth(variant, extra, dl, oracle):
             for k in range(nl):
                 tol = max(REL, 3.0 * nrel(ref[nm][k], r64[nm][k]))  # the oracle's own fp32 gap
                 assert nrel(seq[k].cpu().numpy(), r64[nm][k]) <= tol, (nm, K, k)
+
+
+@pytest.mark.parametrize("precision", ["f32", "bf16"])
+def test_strided_views_per_layer_paths(precision, dl):
+    """Per-layer (m > 256) and bf16-tile paths with every input a column slice of a wider array
+    (odd leading dimension 3B, B = 201): the state DMAs and epilogues address through ld, so the
+    result equals the contiguous run bit for bit."""
+    m, n, B, K = 300, 530, 201, 3
+    inp = P.make_inputs(m, n, 3 * B, 6002)
+    sd = P.make_state_dict("v4", m, n, B, K, inp["A"], 6002, perturb=0.1)
+    sl = slice(B, 2 * B)
+    net = make_net(dl, "v4", dict(inp, X=inp["X"][:, sl], Z0=inp["Z0"][:, sl],
+                                  E0=inp["E0"][:, sl], L0=inp["L0"][:, sl]), sd, K)
+    net.precision = precision
+    Xw = torch.from_numpy(inp["X"]).cuda()
+    Xv = Xw[:, sl]
+    assert Xv.stride(0) == 3 * B
+    with torch.no_grad():
+        out_v = net(Xv)
+        out_c = net(Xv.contiguous())
+    for a, b in zip(out_v, out_c):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
