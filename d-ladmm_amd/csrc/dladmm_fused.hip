@@ -305,6 +305,15 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   const uint32_t ve = lane_off(a.lde0);
   SWalk ew{0u, (uint32_t)(a.lde0 * 4)};
   auto prefetch_elem = [&](int k, bool pro) {
+#if DLADMM_ABLATE & 8  // timing experiment: no per-element beta loads (WRONG results)
+    if constexpr (PKIND == PK_ELEM) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { pn[h][0][r] = 1.f; pn[h][1][r] = 0.5f; pn[h][2][r] = 1.f; }
+      return;
+    }
+#endif
     if constexpr (PKIND == PK_ELEM) {
       const uint32_t eb = (uint32_t)(m * a.ldb * 4);
       const rsrc_t r1 = mkrsrc(pro ? nullptr : a.b1e[k], pro ? 0u : eb);
