@@ -89,6 +89,15 @@ __device__ __forceinline__ void ring_barrier_n() {
   else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// ring_barrier() that lets this wave's newest N VM operations stay in flight: correct when at
+// least N operations were issued after the awaited LDS-DMA (VM operations complete in issue
+// order for vmcnt; counting fewer than were issued only waits longer).
+template <int N>
+__device__ __forceinline__ void ring_barrier_cnt() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
 // All waves: own LDS-DMA + LDS reads complete, then workgroup barrier.  One opaque statement,
 // so the compiler can neither hoist ring reads above it nor sink earlier ones below it.
 #ifndef DLADMM_SYNC_MODE

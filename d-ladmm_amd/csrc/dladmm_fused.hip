@@ -60,10 +60,66 @@ struct Fused {
 // SP steps
 constexpr bool rows_at(int step, int SP, int i) { return (i * SP) / 8 == step; }
 
+// Static VM-operation windows of the ring barriers (V1 / PK_ELEM: its 24 beta loads per G2 pair
+// would otherwise be drained by the vmcnt(0) of the next barrier, one chunk after issue).  A
+// barrier at step s (the last step of a chunk of SPC steps) waits for the chunk DMA issued at
+// the previous barrier step s - SPC; every store and beta load issued in the bodies of steps
+// s - SPC .. s - 1 (the barrier step's own body follows its head) is newer.  Counted: the
+// stores of the epilogue rows (always issued; out-of-range ones go to 0-record buffers) and the
+// beta prefetch at each G2 pair start.  Not counted (conditional): the per-column objective
+// stores -- counting too few only waits longer.  Other variants return 0 (plain vmcnt(0)).
+template <int MB, int NB, int CF, int PKIND>
+struct WinCount {
+  static constexpr int SPC = CF / 2;  // steps per chunk
+  static constexpr int rows_in(int step, int SP) {
+    int c = 0;
+    for (int i = 0; i < 8; ++i) c += ((i * SP) / 8 == step) ? 1 : 0;
+    return c;
+  }
+  // VM operations issued in the body of step t of a G1 / G2 pass
+  static constexpr int ops1(int t) {
+    return rows_in(t % MB, MB) * (t / MB == 0 ? 3 : 1);  // pair 0 runs G2 rows (E, L, T)
+  }
+  // step of the pair that issues beta-prefetch part `part` (3 loads)
+  static constexpr int part_step(int part) { return (part * NB) / 16; }
+  static constexpr int parts_at(int kb) {
+    int c = 0;
+    for (int q = 0; q < 8; ++q) c += part_step(q) == kb ? 1 : 0;
+    return c;
+  }
+  static constexpr int ops2(int t, bool pro) {
+    const int p = t / NB, kb = t % NB;
+    if (p == 0) return (pro ? 0 : rows_in(kb, NB)) + 3 * parts_at(kb);  // G1 rows + prefetch
+    return 6 * rows_in(kb, NB);  // G2 rows (E, L, T stores) + one 3-load prefetch part each
+  }
+  static constexpr int last1 = (NB / 2) * MB - 1, last2 = (MB / 2) * NB - 1;
+  template <int S>
+  static constexpr int g1() {
+    if constexpr (PKIND != PK_ELEM || S % SPC != SPC - 1) return 0;
+    int n = 0;
+    for (int t = S - SPC; t < S; ++t) {
+      if (t >= 0) n += ops1(t);
+      else n += ops2(last2, true) < ops2(last2, false) ? ops2(last2, true) : ops2(last2, false);
+    }
+    return n < 63 ? n : 63;
+  }
+  template <int S, bool PRO>
+  static constexpr int g2() {
+    if constexpr (PKIND != PK_ELEM || S % SPC != SPC - 1) return 0;
+    int n = 0;
+    for (int t = S - SPC; t < S; ++t) {
+      if (t >= 0) n += ops2(t, PRO);
+      else n += PRO ? 0 : ops1(last1);
+    }
+    return n < 63 ? n : 63;
+  }
+};
+
 template <int MP, int NP, int EMODE, int PKIND>
 __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   using F = Fused<MP, NP, EMODE, PKIND>;
   constexpr int MB = F::MB, NB = F::NB, CF = F::CF, NCH = F::NCH, TAB = F::TAB;
+  using Win = WinCount<MB, NB, CF, PKIND>;
   __shared__ f32x4 smem[F::RING_F4 + F::X_F4 + F::TAB_F4];
   f32x4* ring = smem;
   f32x4* xs = smem + F::RING_F4;  // xs[w][b][lane] = X rows 16b+4g+0..3 of this lane's column
@@ -88,8 +144,9 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   // the prologue's E0 arrives through the per-element prefetch instead (b2's slot).
   constexpr bool kEState = !(EMODE == EM_V1 && PKIND == PK_ELEM);
   float Zr[NB][4], Er[MB][4], Lr[MB][4], Vr[MB][4];
-  float pb[2][3][4];  // PK_ELEM: betas (b3, b2, b1 of k+1) of the pending G2 pair
-  float pn[2][3][4];  // PK_ELEM: the same for the pair being computed (loads in flight)
+  // PK_ELEM: betas (b3, b2, b1 of k+1) of the pending G2 pair.  One buffer: the slot of row
+  // (h, r) is reloaded for the pair being computed right after that row's epilogue read it.
+  float pb[2][3][4];
   float regsum = 0.f, fit1 = 0.f, fit2 = 0.f;
 
   // ---------------------------------------------------------------- ring (LDS-DMA) stream
@@ -304,13 +361,14 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   // the next layer's b1.  The prologue (k = -1) loads E0 into b2's slot and b1 of layer 0.
   const uint32_t ve = lane_off(a.lde0);
   SWalk ew{0u, (uint32_t)(a.lde0 * 4)};
-  auto prefetch_elem = [&](int k, bool pro) {
+  // Part `part` (0..7: block half h = part / 4, row r = part % 4) of the beta prefetch for the
+  // pair being computed: right after the pending pair's row `part` consumed its slot (G2 pairs
+  // p > 0), or spread over the first half of pair 0's steps (step (part * NB) / 16).
+  auto prefetch_part = [&](int k, bool pro, auto PART_) {
+    constexpr int part = decltype(PART_)::value, h = part / 4, r = part % 4;
 #if DLADMM_ABLATE & 8  // timing experiment: no per-element beta loads (WRONG results)
     if constexpr (PKIND == PK_ELEM) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) { pn[h][0][r] = 1.f; pn[h][1][r] = 0.5f; pn[h][2][r] = 1.f; }
+      pb[h][0][r] = 1.f; pb[h][1][r] = 0.5f; pb[h][2][r] = 1.f;
       return;
     }
 #endif
@@ -319,29 +377,15 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
       const rsrc_t r1 = mkrsrc(pro ? nullptr : a.b1e[k], pro ? 0u : eb);
       const rsrc_t r2 = pro ? mkrsrc(a.E0, (uint32_t)(m * a.lde0 * 4)) : mkrsrc(a.b2e[k], eb);
       const rsrc_t rn = mkrsrc(k + 1 < K ? a.b1e[k + 1] : nullptr, k + 1 < K ? eb : 0u);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t so = bw.at(r);
-          pn[h][0][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r1, (int)vb, (int)so, 0));
-          pn[h][1][r] = pro ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r2, (int)ve, (int)ew.at(r), 0))
-                            : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r2, (int)vb, (int)so, 0));
-          pn[h][2][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rn, (int)vb, (int)so, 0));
-        }
+      const uint32_t so = bw.at(r);
+      pb[h][0][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r1, (int)vb, (int)so, 0));
+      pb[h][1][r] = pro ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r2, (int)ve, (int)ew.at(r), 0))
+                        : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r2, (int)vb, (int)so, 0));
+      pb[h][2][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rn, (int)vb, (int)so, 0));
+      if constexpr (r == 3) {
         bw.next();
         if (pro) ew.next();
       }
-    }
-  };
-  auto take_elem = [&]() {  // the pair that just finished becomes the pending one
-    if constexpr (PKIND == PK_ELEM) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) pb[h][i][r] = pn[h][i][r];
     }
   };
 
@@ -352,14 +396,19 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   // epilogue rows scheduled here, then 8 MFMAs on two independent chains; a sched_barrier
   // pins that order.  fr[] rotates over 4 registers (2 steps x 2 fragments).
   f32x4 fr[4];
-  auto step_head = [&](auto S_, int gi) {
+  // WIN = VM operations (stores, V1 beta loads) definitely issued since the awaited chunk's DMA
+  // (PK_ELEM only, see window_ops): they stay in flight across the barrier
+  auto step_head = [&](auto S_, int gi, auto WIN_) {
     constexpr int s = decltype(S_)::value;
+    constexpr int WIN = decltype(WIN_)::value;
     constexpr int fi = 2 * s, fc = fi % CF, ch = fi / CF;
     if constexpr (fc + 2 < CF) {
       fr[(fi + 2) % 4] = frag(cur, fc + 2);
       fr[(fi + 3) % 4] = frag(cur, fc + 3);
     } else {
-      ring_barrier();  // chunk ch+1 landed for every wave; every wave is done with chunk ch-1
+      // chunk ch+1 landed for every wave; every wave is done with chunk ch-1
+      if constexpr (WIN > 0) ring_barrier_cnt<WIN>();
+      else ring_barrier();
       issue(chunk_src(gi, ch + 2), slot_add(cur, 2));
       const int nx = slot_add(cur, 1);
       fr[(fi + 2) % 4] = frag(nx, 0);
@@ -400,14 +449,12 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     static_for<NB / 2>([&](auto P_) {
       constexpr int p = decltype(P_)::value;
       f32x4 ca = zero4, cb = zero4;
-      if constexpr (p == 0) {
-        take_elem();
-        load_x(MB / 2 - 1);
-      }
+      if constexpr (p == 0) load_x(MB / 2 - 1);
       static_for<MB>([&](auto J_) {
         constexpr int jb = decltype(J_)::value;
         constexpr int s = p * MB + jb;
-        step_head(std::integral_constant<int, s>{}, gi);
+        step_head(std::integral_constant<int, s>{}, gi,
+                  std::integral_constant<int, Win::template g1<s>()>{});
         static_for<8>([&](auto I_) {
           constexpr int i = decltype(I_)::value;
           constexpr int h = i / 4, r = i % 4;
@@ -446,15 +493,18 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     static_for<MB / 2>([&](auto P_) {
       constexpr int p = decltype(P_)::value;
       f32x4 ca = zero4, cb = zero4;
-      if constexpr (p > 0) {
-        take_elem();
-        load_x(p - 1);
-      }
-      prefetch_elem(k, PRO);
+      if constexpr (p > 0) load_x(p - 1);
       static_for<NB>([&](auto K_) {
         constexpr int kb = decltype(K_)::value;
         constexpr int s = p * NB + kb;
-        step_head(std::integral_constant<int, s>{}, gi);
+        step_head(std::integral_constant<int, s>{}, gi,
+                  std::integral_constant<int, Win::template g2<s, PRO>()>{});
+        if constexpr (p == 0) {
+          static_for<8>([&](auto PT_) {
+            constexpr int part = decltype(PT_)::value;
+            if constexpr (Win::part_step(part) == kb) prefetch_part(k, PRO, PT_);
+          });
+        }
         static_for<8>([&](auto I_) {
           constexpr int i = decltype(I_)::value;
           constexpr int h = i / 4, r = i % 4;
@@ -463,6 +513,7 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
               if constexpr (!PRO) epi1_row(P, rzo, k, NB - 2 + h, r, h ? qb : qa);
             } else {
               epi2_row(P, O, k, PRO, 2 * p - 2 + h, h, r, h ? qb : qa, h ? xb : xa);
+              prefetch_part(k, PRO, I_);  // this row's beta slot, for pair p
             }
           }
         });
@@ -505,7 +556,6 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     Op = O;
   }
   // epilogue of the last G2 pair of layer K-1
-  take_elem();
   load_x(MB / 2 - 1);
 #pragma unroll
   for (int i = 0; i < 8; ++i)
