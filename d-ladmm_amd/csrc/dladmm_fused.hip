@@ -46,7 +46,8 @@ struct Fused {
   static constexpr int GF = MB * NB;                // fragments per GEMM
   static constexpr int CF = GF < DLADMM_CHUNK ? GF : DLADMM_CHUNK;  // fragments per ring chunk
   static constexpr int NCH = GF / CF;               // chunks per GEMM
-  static constexpr int TAB = 6 * MP + NP;           // per-row param table (floats)
+  static constexpr int TAB = ((6 * MP + NP + 63) / 64) * 64;  // per-row param table (floats,
+                                                              // whole 64-entry DMA pieces)
   static constexpr int RING_F4 = 3 * CF * 64;       // 3 slots
   static constexpr int TAB_F4 = (PKIND == PK_ROW) ? (3 * TAB) / 4 : 0;  // 3 layer buffers
   static constexpr int X_F4 = kWaves * MB * 64;     // the tile's X, resident in LDS
@@ -182,15 +183,25 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   auto frag = [&](int slot, int fc) -> f32x4 { return ring[(slot * CF + fc) * 64 + lane]; };
 
   // ---------------------------------------------------------------- parameters
-  auto row_tab_load = [&](int k, int buf) {  // per-row params of layer k -> tab[buf]
+  // per-row params of layer k -> tab[buf], by LDS-DMA (each wave fills 64 consecutive entries
+  // per piece; no register round trip).  Rows past m (n for theta_z) read the last valid row:
+  // the padded rows' state is exactly zero whatever finite parameter they see.  Readers are
+  // ring barriers away (their vmcnt(0) covers the DMA).
+  auto row_tab_load = [&](int k, int buf) {
     if constexpr (PKIND == PK_ROW) {
+      static_assert(TAB % 64 == 0, "whole wave pieces");  // entries past 6 MP + NP: padding
       float* t = tab + buf * TAB;
       const float* src = a.rowp + (int64_t)k * 8 * a.rstride;
-      for (int i = tid; i < TAB; i += 256) {
-        const int slot = i < 6 * MP ? i / MP : 6;
-        const int row = i < 6 * MP ? i % MP : i - 6 * MP;
-        const int lim = slot == 6 ? n : m;
-        t[i] = row < lim ? src[(int64_t)slot * a.rstride + row] : 0.0f;
+#pragma unroll
+      for (int j = 0; j < (TAB + 255) / 256; ++j) {
+        if (256 * j + 64 * w < TAB) {  // wave-uniform
+          const int i = 256 * j + 64 * w + lane;
+          const int slot = i < 6 * MP ? i / MP : 6;
+          const int row = i < 6 * MP ? i % MP : i - 6 * MP;
+          const int lim = slot == 6 ? n : m;
+          const int rowc = row < lim ? row : lim - 1;
+          glds4(src, (uint32_t)(((int64_t)slot * a.rstride + rowc) * 4), t + 256 * j + 64 * w);
+        }
       }
     }
   };
