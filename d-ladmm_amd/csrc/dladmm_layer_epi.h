@@ -14,6 +14,14 @@
 
 namespace dladmm {
 
+#ifndef DLADMM_EPI_NT
+#define DLADMM_EPI_NT 0  // experiment knob: 1 = non-temporal (nt) epilogue stores
+#endif
+__device__ __forceinline__ void epi_store(float* p, float v) {
+  if constexpr (DLADMM_EPI_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 template <int EMODE, int PKIND, int PH>
 struct LayerEpi {
   const LayerArgs& a;
@@ -80,7 +88,7 @@ struct LayerEpi {
       float u = accv;
       if constexpr (PKIND == PK_SCALAR) u = sp[DLADMM_P_S1] * u;
       const float z = shrink(v.zp - u, v.thz);                        // main_lena.py:79-80
-      if (ok) a.Zo[(int64_t)row * a.ldo + col] = z;
+      if (ok) epi_store(a.Zo + (int64_t)row * a.ldo + col, z);
       lsum += ok ? fabsf(z) : 0.0f;
       return ok ? z : 0.0f;
     } else {
@@ -108,15 +116,15 @@ struct LayerEpi {
         t = (P + e) - x;                                                   // main_lena.py:88
         l = l0 + v.b3 * t;                                                 // main_lena.py:89
         if (ok) {
-          a.Eo[(int64_t)row * a.ldo + col] = e;
-          a.Lo[(int64_t)row * a.ldo + col] = l;
+          epi_store(a.Eo + (int64_t)row * a.ldo + col, e);
+          epi_store(a.Lo + (int64_t)row * a.ldo + col, l);
         }
         const float res = x - P;
         lsum += ok ? (lasso ? res * res : fabsf(res)) : 0.0f;
       }
-      if (ok && a.To) a.To[(int64_t)row * a.ldo + col] = t;
+      if (ok && a.To) epi_store(a.To + (int64_t)row * a.ldo + col, t);
       const float var = l + v.b1n * t;                      // Var_{k+1} = L + b1 T  main_lena.py:85
-      if (ok && a.Vo) a.Vo[(int64_t)row * a.ldv + col] = var;
+      if (ok && a.Vo) epi_store(a.Vo + (int64_t)row * a.ldv + col, var);
       return ok ? var : 0.0f;
     }
   }

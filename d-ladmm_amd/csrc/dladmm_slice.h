@@ -145,6 +145,10 @@ __device__ __forceinline__ void slice_gemm(f32x4* ring, const float* Wp, int MBp
 
 }  // namespace dladmm
 
+#ifndef DLADMM_BVIEW_AUX
+#define DLADMM_BVIEW_AUX 0  // cache-policy bits of the backward epilogue stores (experiment)
+#endif
+
 namespace dladmm {
 
 // A [rows][ld] fp32 matrix seen by one lane of a slice epilogue in the C/D layout (lane: column
@@ -160,7 +164,7 @@ struct BView {
   }
   __device__ __forceinline__ void st(uint32_t row_u, float v) const {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)vo,
-                                          (int)(row_u * ld4), 0);
+                                          (int)(row_u * ld4), DLADMM_BVIEW_AUX);
   }
 };
 __device__ __forceinline__ BView make_view(const float* p, int rows, int64_t ld, int g,
