@@ -4,6 +4,7 @@ Import with ``importlib.import_module("d-ladmm_amd")`` (the directory name is no
 identifier) or put the repo root on sys.path and use the same call.
 """
 from . import _lib  # noqa: F401
+from . import dist  # noqa: F401
 from .model import (DLADMMNet, DLADMMNetFull, DLADMMNetLasso, DLADMMNetLTheta,  # noqa: F401
                     DLADMMNetScalar, DLADMMNetScalarTied, VARIANTS, load_checkpoint)
 from .model import DLADMMNetNewS, DLADMMNetPTiedNewS, DLADMMNetTiedNewS  # noqa: F401

@@ -92,19 +92,29 @@ class _DLADMMBase(nn.Module):
     def _weights(self) -> List[torch.Tensor]:
         return [self.fc[k].weight for k in range(self.layers)]
 
-    def _build_tables(self, dev) -> dict:  # pragma: no cover - per variant
+    def _table_spec(self) -> dict:  # pragma: no cover - per variant
+        """{"scalar" | "row": {slot: source}}: which parameter feeds which slot of the C ABI's
+        per-layer table.  A source is a ParameterList (one entry per layer), a 0-dim tensor
+        (every layer) or a float constant."""
         raise NotImplementedError
 
-    def _tables(self, dev) -> dict:
-        """Per-layer parameter tables for the C ABI, rebuilt only when a parameter changed
-        (storage or in-place version: optimizer steps and load_state_dict bump it).  Saves the
-        dozens of tiny copy kernels per call that assembling them costs."""
-        key = (str(dev),) + tuple((p.data_ptr(), p._version) for p in self.parameters())
-        c = self.__dict__.get("_tab_cache")
-        if c is None or c[0] != key:
-            c = (key, self._build_tables(dev))
-            self.__dict__["_tab_cache"] = c
-        return c[1]
+    def _elem_betas(self, cols=None) -> dict:
+        """V1's per-sample betas (passed to the C ABI by pointer, read live); others: none."""
+        return {}
+
+    def _tables(self, dev, cols=None) -> dict:
+        """Per-layer parameter tables for the C ABI, assembled from the live parameters on every
+        call (one cat + one index_copy, _assemble_table).  Nothing is cached across calls:
+        an optimizer step, load_state_dict, or an in-place edit through p.data (which does not
+        bump the version counter) all take effect on the next call."""
+        out = {}
+        for kind, spec in self._table_spec().items():
+            R = 1 if kind == "scalar" else max(self.m, self.d)
+            rows = {nm: (1 if kind == "scalar" else (self.d if nm == "thz" else self.m))
+                    for nm in spec}
+            out[f"{kind}_params"] = _assemble_table(self.layers, R, dev, spec, rows)
+        out.update(self._elem_betas(cols))
+        return out
 
     def _needs_grad(self) -> bool:
         return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
@@ -165,52 +175,91 @@ class _DLADMMBase(nn.Module):
         return r, obj
 
     def training_loss(self, x, alpha: float, coeffs=None, kind: str = "l1l1",
-                      batch: Optional[int] = None):
+                      batch: Optional[int] = None, cols=None):
         """The reference training objective as one fused, differentiable op:
             total = sum_k coeffs[k] * (alpha * sum(|Z_k|,0).mean() + sum(|X - A Z_k|,0).mean())
         (main_syn_l1l1_scalar.py:283-296; kind='lasso': 0.5*sum((X - A Z_k)^2,0), lasso
         :270-283).  coeffs default: all 1; the reference uses decay 0.6**epoch for k < K-1.
-        `batch` = the column count of the mean (default x.shape[1]; the global batch when the
-        columns are sharded over ranks).  Returns (total, per-layer losses [K]); call
-        total.backward() as the reference does.  Mathematically the same gradients as building
-        the loss from forward()'s outputs with torch ops, without the K products A Z_k."""
+        Returns (total, per-layer losses [K]); call total.backward() as the reference does.
+        Mathematically the same gradients as building the loss from forward()'s outputs with
+        torch ops, without the K products A Z_k.
+
+        Data-parallel shards: `cols` = (c0, c1) runs the columns c0..c1-1 of the model's batch
+        (x is that shard, (m, c1 - c0); Z0/E0/L0 and V1's per-sample betas are sliced to it) and
+        `batch` = the column count of the mean (default x.shape[1]; pass the global batch).
+        Each rank's gradient is then its shard's share of the global objective, and
+        dist.allreduce_grads (SUM) gives the full-batch gradient."""
         K = self.layers
         coeffs = [1.0] * K if coeffs is None else [float(c) for c in coeffs]
         if len(coeffs) != K:
             raise ValueError(f"dladmm: coeffs must have {K} entries")
         if kind not in ("l1l1", "lasso"):
             raise ValueError(f"dladmm: unknown loss kind {kind!r}")
+        if cols is not None:
+            cols = (int(cols[0]), int(cols[1]))
+            if not (0 <= cols[0] < cols[1] <= self.Z0.shape[1]) or \
+                    x.shape[1] != cols[1] - cols[0]:
+                raise ValueError(f"dladmm: cols {cols} do not match x {tuple(x.shape)} and the "
+                                 f"model's batch of {self.Z0.shape[1]} columns")
         denom = float(batch if batch is not None else x.shape[1])
         if self._needs_grad():
             if x.requires_grad:
                 raise RuntimeError("dladmm: gradients w.r.t. the input X are not supported")
-            return _DLADMMLossFunction.apply(self, x, coeffs, float(alpha), kind, denom,
+            return _DLADMMLossFunction.apply(self, x, coeffs, float(alpha), kind, denom, cols,
                                              *self.parameters())
-        r, per_layer = self.layer_objectives(x, alpha, kind)
-        per_layer = (per_layer * x.shape[1] / denom)
+        lk = {"l1l1": _lib.LOSS_L1L1, "lasso": _lib.LOSS_LASSO}[kind]
+        with torch.no_grad():
+            r = self._run_shard(x, cols, loss_kind=lk, want_T=self.RETURNS_T)
+        per_layer = (alpha * r.loss_sums[:, 0] + r.loss_sums[:, 1]) / denom
         c = torch.as_tensor(coeffs, dtype=torch.float64, device=per_layer.device)
         return (c * per_layer).sum().to(torch.float32), per_layer.to(torch.float32)
+
+    def _init_state(self, cols=None):
+        """(Z0, E0, L0) of the whole model batch or of the column shard cols = (c0, c1)."""
+        if cols is None:
+            return self.Z0, self.E0, self.L0
+        c0, c1 = cols
+        return self.Z0[:, c0:c1], self.E0[:, c0:c1], self.L0[:, c0:c1]
+
+    def _run_shard(self, x, cols, **kw):
+        """Forward of every layer on the column shard `cols` (None: the whole batch)."""
+        dev = self.A.device
+        Z0, E0, L0 = self._init_state(cols)
+        W = [w.detach() for w in self._weights()]
+        return dladmm_forward(self.VARIANT, x, self.A, W, Z0, E0, L0, keep_all=True,
+                              **kw, **self._tables(dev, cols))
 
     # --- backward: map the C ABI's gradient tables onto the reference parameters ------------
     # GRAD_SLOTS: ParameterList name -> (kind, slots summed).  kind 'scalar' reads g_scalar,
     # 'row' reads g_row (theta_z rows = d, else m), 'elem1'/'elem2' the V1 per-sample betas.
     GRAD_SLOTS: dict = {}
+    # which update steps of a layer read each parameter: z = Z-step (Var, shrink of Z), e = E-step,
+    # l = L-step.  V1/V2 use beta1 for Var and L (main_lena.py:85,89): "zl".
+    PARAM_STEPS = {"beta1": "z", "beta2": "e", "beta3": "l", "ss2": "e", "ss2_1": "e",
+                   "ss2_2": "e", "ss1": "z", "active_para": "z", "active_para1": "e"}
 
     def _fc_key(self, k: int) -> str:
         """state_dict key of the weight layer k uses."""
         return "fc.weight" if self._shared_weight() else f"fc.{k}.weight"
 
-    def _param_grads(self, res, nl: int) -> dict:
-        """Gradients by state_dict key from a BackwardResult of the first `nl` layers (layers
-        >= nl were not run: their parameters get no gradient, as in the reference)."""
+    def _param_grads(self, res, nl: int, reach: Optional[dict] = None, cols=None) -> dict:
+        """Gradients by state_dict key from a BackwardResult of the first `nl` layers.  As in the
+        reference's autograd, a parameter no cotangent can reach gets None, not a zero tensor:
+        layers >= nl were not run, and `reach` (_reachable) marks the layer steps the loss
+        depends on.  cols = (c0, c1): the forward ran on that column shard of a (m, batch_size)
+        V1 beta, whose gradient is zero outside it."""
         out = {}
+        rz = reach["z"] if reach else [True] * nl
         # one fp64 -> fp32 conversion per table; a single-slot gradient is then a view of it
         # (per-parameter sum / cast ops were ~180 tiny launches per training step)
         kinds = {kind for kind, _ in self.GRAD_SLOTS.values()}
         gs32 = res.g_scalar.to(torch.float32) if "scalar" in kinds else None
         gr32 = res.g_row.to(torch.float32) if "row" in kinds else None
         for name, (kind, slots) in self.GRAD_SLOTS.items():
+            steps = self.PARAM_STEPS[name]
             for k in range(nl):
+                if reach is not None and not any(reach[s][k] for s in steps):
+                    continue
                 key = f"{name}.{k}"
                 if kind == "scalar":
                     g = (gs32[k, slots[0]] if len(slots) == 1 else
@@ -220,15 +269,21 @@ class _DLADMMBase(nn.Module):
                     g = (gr32[k, slots[0], :rows] if len(slots) == 1 else
                          sum(res.g_row[k, s, :rows] for s in slots).to(torch.float32))
                     g = g.reshape(rows, 1)
-                elif kind == "elem1":
-                    g = res.g_beta1[k].to(torch.float32)
                 else:
-                    g = res.g_beta2[k].to(torch.float32)
+                    g = (res.g_beta1 if kind == "elem1" else res.g_beta2)[k].to(torch.float32)
+                    if cols is not None:
+                        full = torch.zeros((self.m, self.batch_size), dtype=torch.float32,
+                                           device=g.device)
+                        full[:, cols[0]:cols[1]] = g
+                        g = full
                 out[key] = g
         if self._shared_weight():
-            out[self._fc_key(0)] = res.gW[0]
+            if any(rz[:nl]):
+                out[self._fc_key(0)] = res.gW[0]
         else:
             for k in range(nl):
+                if not rz[k]:
+                    continue
                 key = self._fc_key(k)
                 out[key] = res.gW[k] if key not in out else out[key] + res.gW[k]
         return out
@@ -281,7 +336,7 @@ class _DLADMMFunction(torch.autograd.Function):
                               g[:K], g[K:2 * K], g[2 * K:3 * K],
                               g[3 * K:] if mod.RETURNS_T else None,
                               tied=mod._shared_weight(), **ctx.tables)
-        grads = mod._param_grads(res, K)
+        grads = mod._param_grads(res, K, _reachable(K, g, mod.RETURNS_T))
         names = [n for n, _ in mod.named_parameters()]
         return (None, None, None) + tuple(grads.get(n) for n in names)
 
@@ -296,17 +351,18 @@ class _DLADMMLossFunction(torch.autograd.Function):
     (non-differentiable, for logging as the reference prints loss[k])."""
 
     @staticmethod
-    def forward(ctx, mod, x, coeffs, alpha, kind, denom, *params):
+    def forward(ctx, mod, x, coeffs, alpha, kind, denom, cols, *params):
         dev = mod.A.device
-        tables = mod._tables(dev)
+        tables = mod._tables(dev, cols)
         W = [w.detach() for w in mod._weights()]
+        Z0, E0, L0 = mod._init_state(cols)
         lk = {"l1l1": _lib.LOSS_L1L1, "lasso": _lib.LOSS_LASSO}[kind]
-        r = dladmm_forward(mod.VARIANT, x, mod.A, W, mod.Z0, mod.E0, mod.L0, keep_all=True,
-                           want_T=True, loss_kind=lk, **tables)
+        r = dladmm_forward(mod.VARIANT, x, mod.A, W, Z0, E0, L0, keep_all=True, want_T=True,
+                           loss_kind=lk, **tables)
         per_layer = (alpha * r.loss_sums[:, 0] + r.loss_sums[:, 1]) / denom  # fp64 [K]
         c = torch.as_tensor(coeffs, dtype=torch.float64, device=dev)
         total = (c * per_layer).sum().to(torch.float32)
-        ctx.mod, ctx.tables, ctx.W, ctx.lk = mod, tables, W, lk
+        ctx.mod, ctx.tables, ctx.W, ctx.lk, ctx.cols = mod, tables, W, lk, cols
         # (cz_k, cf_k) per unit upstream gradient
         ctx.base = torch.stack([c * alpha / denom, c / denom], 1).to(torch.float32)
         ctx.save_for_backward(x, r.Z, r.E, r.L, r.T)
@@ -318,37 +374,94 @@ class _DLADMMLossFunction(torch.autograd.Function):
     def backward(ctx, g_total, g_layers):
         x, Z, E, L, T = ctx.saved_tensors
         mod = ctx.mod
+        K = mod.layers
         coef = (ctx.base * g_total).contiguous()  # device-side scale, no host sync
-        res = dladmm_backward(mod.VARIANT, x, mod.A, ctx.W, mod.Z0, mod.E0, mod.L0,
+        Z0, E0, L0 = mod._init_state(ctx.cols)
+        res = dladmm_backward(mod.VARIANT, x, mod.A, ctx.W, Z0, E0, L0,
                               ForwardResult(Z, E, L, T, None), loss_kind=ctx.lk, loss_coef=coef,
                               tied=mod._shared_weight(), **ctx.tables)
-        grads = mod._param_grads(res, mod.layers)
+        # the objective reads Z_0..Z_{K-1} only: the last layer's E/L steps feed nothing
+        reach = {"z": [True] * K, "e": [k < K - 1 for k in range(K)],
+                 "l": [k < K - 1 for k in range(K)]}
+        grads = mod._param_grads(res, K, reach, ctx.cols)
         names = [n for n, _ in mod.named_parameters()]
-        return (None,) * 6 + tuple(grads.get(n) for n in names)
+        return (None,) * 7 + tuple(grads.get(n) for n in names)
 
 
-def _stack_scalar(pl) -> torch.Tensor:
-    return torch.cat([p.detach().reshape(1) for p in pl])
+def _reachable(K: int, g, has_t: bool) -> dict:
+    """Which layer steps of a K-layer forward the cotangents g (Z_0..Z_{K-1}, E.., L..,
+    T_0..T_K; None = not read) depend on, as reference autograd sees the graph:
+      E-step k: E_k feeds T_{k+1}, L_k and everything after layer k
+      L-step k: L_k feeds layer k+1 (Var, E-step, L) but not T_{k+1}
+      Z-step k: Z_k feeds E_k (through A Z_k) and Z_{k+1}
+    Returns {"z" | "e" | "l": [bool] * K}."""
+    def suffix(seq, n):
+        out, acc = [False] * (n + 1), False
+        for i in range(n - 1, -1, -1):
+            acc = acc or (seq is not None and seq[i] is not None)
+            out[i] = acc
+        return out
+    gZ, gE, gL = g[:K], g[K:2 * K], g[2 * K:3 * K]
+    gT = g[3 * K:] if has_t else None
+    sZ, sE, sL, sT = suffix(gZ, K), suffix(gE, K), suffix(gL, K), suffix(gT, K + 1)
+    sT = sT + [False]
+    re = [sE[k] or sL[k] or sT[k + 1] or sZ[k + 1] for k in range(K)]
+    rl = [sL[k] or sZ[k + 1] or sE[k + 1] or sT[k + 2] for k in range(K)]
+    rz = [sZ[k] or re[k] for k in range(K)]
+    return {"z": rz, "e": re, "l": rl}
+
+
+_SLOTS = {"b1": _lib.P_BETA1, "b2": _lib.P_BETA2, "b3": _lib.P_BETA3, "ss2": _lib.P_SS2,
+          "ss2b": _lib.P_SS2B, "the": _lib.P_THETA_E, "thz": _lib.P_THETA_Z, "s1": _lib.P_S1}
+_TABLE_IDX = {}
+
+
+def _assemble_table(K: int, R: int, dev, spec: dict, rows: dict) -> torch.Tensor:
+    """(K, 8) fp32 table (R = 1) or (K, 8, R) per-row table of the C ABI from the live
+    parameter values: ONE torch.cat of every source plus ONE index_copy into a base holding the
+    constant slots (missing slots 0).  The scatter index depends only on the layout and is built
+    once per (device, layout)."""
+    tensors, layout = [], []
+    consts = []
+    for nm, src in spec.items():
+        if isinstance(src, (int, float)):
+            consts.append((nm, float(src)))
+            continue
+        seq = [src] * K if torch.is_tensor(src) else list(src)
+        if len(seq) < K:
+            raise ValueError(f"dladmm: {len(seq)} entries for parameter slot {nm}, need {K}")
+        layout.append((nm, rows[nm]))
+        tensors += [t.detach().reshape(-1) for t in seq[:K]]
+    key = (str(dev), K, R, tuple(layout), tuple(consts))
+    ent = _TABLE_IDX.get(key)
+    if ent is None:
+        idx = []
+        for nm, nr in layout:
+            for k in range(K):
+                base = (k * _lib.NSCALAR + _SLOTS[nm]) * R
+                idx.extend(range(base, base + nr))
+        base_t = torch.zeros(K * _lib.NSCALAR * R, dtype=torch.float32)
+        for nm, v in consts:
+            for k in range(K):
+                o = (k * _lib.NSCALAR + _SLOTS[nm]) * R
+                base_t[o:o + R] = v
+        ent = (torch.tensor(idx, dtype=torch.int64).to(dev), base_t.to(dev))
+        _TABLE_IDX[key] = ent
+    idx, base_t = ent
+    out = base_t.clone()
+    if tensors:
+        flat = torch.cat(tensors).to(device=dev, dtype=torch.float32)
+        if flat.numel() != idx.numel():
+            raise ValueError("dladmm: parameter shapes do not match the table layout")
+        out.index_copy_(0, idx, flat)
+    return out.view(K, _lib.NSCALAR) if R == 1 else out.view(K, _lib.NSCALAR, R)
 
 
 def _scalar_table(K, dev, **cols) -> torch.Tensor:
-    """(K, 8) fp32 table of per-layer scalars; missing slots 0 (unused by the variant)."""
-    slots = {"b1": _lib.P_BETA1, "b2": _lib.P_BETA2, "b3": _lib.P_BETA3, "ss2": _lib.P_SS2,
-             "ss2b": _lib.P_SS2B, "the": _lib.P_THETA_E, "thz": _lib.P_THETA_Z, "s1": _lib.P_S1}
+    """(K, 8) fp32 table of per-layer scalars from floats / 0-dim tensors (KM constants)."""
     t = torch.zeros((K, _lib.NSCALAR), dtype=torch.float32, device=dev)
     for k, v in cols.items():
-        t[:, slots[k]] = v.to(device=dev, dtype=torch.float32) if torch.is_tensor(v) else v
-    return t
-
-
-def _row_table(K, R, dev, m, n, **cols) -> torch.Tensor:
-    """(K, 8, R) fp32 table of per-row params (R = max(m, n)); theta_z holds n rows, the rest m."""
-    slots = {"b1": _lib.P_BETA1, "b2": _lib.P_BETA2, "b3": _lib.P_BETA3, "ss2": _lib.P_SS2,
-             "ss2b": _lib.P_SS2B, "the": _lib.P_THETA_E, "thz": _lib.P_THETA_Z}
-    t = torch.zeros((K, _lib.NSCALAR, R), dtype=torch.float32, device=dev)
-    for k, pl in cols.items():
-        rows = n if k == "thz" else m
-        t[:, slots[k], :rows] = torch.stack([p.detach().reshape(-1) for p in pl]).to(dev)
+        t[:, _SLOTS[k]] = v.to(device=dev, dtype=torch.float32) if torch.is_tensor(v) else v
     return t
 
 
@@ -356,6 +469,7 @@ class DLADMMNet(_DLADMMBase):
     """V1, main_lena.py:16-102 (also main_syn_l1l1.py, main_syn_gt.py)."""
     VARIANT = _lib.V1_LENA
     GRAD_SLOTS = {"beta1": ("elem1", ()), "beta2": ("elem2", ())}
+    PARAM_STEPS = dict(_DLADMMBase.PARAM_STEPS, beta1="zl")   # main_lena.py:85,89
 
     def _register_params(self):
         # main_lena.py:30-41: beta1/beta2 (m, batch_size) per layer; thresholds are plain tensors
@@ -369,13 +483,16 @@ class DLADMMNet(_DLADMMBase):
         self.active_para = _dev(torch.tensor(0.025, dtype=torch.float32))
         self.active_para1 = _dev(torch.tensor(0.06, dtype=torch.float32))
 
-    def _build_tables(self, dev):
-        K = self.layers
-        return dict(
-            scalar_params=_scalar_table(K, dev, thz=self.active_para.detach().float(),
-                                        the=self.active_para1.detach().float(), s1=1.0),
-            beta1_elem=[b.detach() for b in self.beta1],
-            beta2_elem=[b.detach() for b in self.beta2])
+    def _table_spec(self):
+        return {"scalar": dict(thz=self.active_para.float(), the=self.active_para1.float(),
+                               s1=1.0)}
+
+    def _elem_betas(self, cols=None):
+        def sl(b):
+            b = b.detach()
+            # a column shard (training_loss(cols=...)): the backward needs contiguous betas
+            return b if cols is None else b[:, cols[0]:cols[1]].contiguous()
+        return dict(beta1_elem=[sl(b) for b in self.beta1], beta2_elem=[sl(b) for b in self.beta2])
 
 
 class DLADMMNetLTheta(_DLADMMBase):
@@ -386,6 +503,7 @@ class DLADMMNetLTheta(_DLADMMBase):
                   "beta2": ("row", (_lib.P_BETA2,)),
                   "active_para": ("row", (_lib.P_THETA_Z,)),
                   "active_para1": ("row", (_lib.P_THETA_E,))}
+    PARAM_STEPS = dict(_DLADMMBase.PARAM_STEPS, beta1="zl")   # main_syn_l1l1_ltheta.py:74,80
 
     def _register_params(self):
         # main_syn_l1l1_ltheta.py:30-43
@@ -395,11 +513,9 @@ class DLADMMNetLTheta(_DLADMMBase):
         self._plist("active_para1", (self.m, 1), 0.06)
         self.fc = nn.ModuleList([nn.Linear(self.m, self.d, bias=False) for _ in range(self.layers)])
 
-    def _build_tables(self, dev):
-        K, R = self.layers, max(self.m, self.d)
-        return dict(row_params=_row_table(K, R, dev, self.m, self.d, b1=self.beta1, b2=self.beta2,
-                                          b3=self.beta1, the=self.active_para1,
-                                          thz=self.active_para))
+    def _table_spec(self):
+        return {"row": dict(b1=self.beta1, b2=self.beta2, b3=self.beta1, the=self.active_para1,
+                            thz=self.active_para)}
 
 
 class DLADMMNetFull(_DLADMMBase):
@@ -419,11 +535,9 @@ class DLADMMNetFull(_DLADMMBase):
         self._plist("active_para1", (self.m, 1), 0.8)
         self.fc = nn.ModuleList([nn.Linear(self.m, self.d, bias=False) for _ in range(self.layers)])
 
-    def _build_tables(self, dev):
-        K, R = self.layers, max(self.m, self.d)
-        return dict(row_params=_row_table(K, R, dev, self.m, self.d, b1=self.beta1, b2=self.beta2,
-                                          b3=self.beta3, ss2=self.ss2, the=self.active_para1,
-                                          thz=self.active_para))
+    def _table_spec(self):
+        return {"row": dict(b1=self.beta1, b2=self.beta2, b3=self.beta3, ss2=self.ss2,
+                            the=self.active_para1, thz=self.active_para)}
 
 
 class DLADMMNetScalar(_DLADMMBase):
@@ -453,12 +567,9 @@ class DLADMMNetScalar(_DLADMMBase):
         self._plist("active_para1", (1, 1), 0.8)
         self.fc = nn.ModuleList([nn.Linear(self.m, self.d, bias=False) for _ in range(self.layers)])
 
-    def _build_tables(self, dev):
-        K = self.layers
-        return dict(scalar_params=_scalar_table(
-            K, dev, b1=_stack_scalar(self.beta1), b2=_stack_scalar(self.beta2),
-            b3=_stack_scalar(self.beta3), ss2=_stack_scalar(self.ss2),
-            the=_stack_scalar(self.active_para1), thz=_stack_scalar(self.active_para), s1=1.0))
+    def _table_spec(self):
+        return {"scalar": dict(b1=self.beta1, b2=self.beta2, b3=self.beta3, ss2=self.ss2,
+                               the=self.active_para1, thz=self.active_para, s1=1.0)}
 
 
 class DLADMMNetScalarTied(DLADMMNetScalar):
@@ -478,13 +589,9 @@ class DLADMMNetScalarTied(DLADMMNetScalar):
     def _weights(self):
         return [self.fc.weight] * self.layers
 
-    def _build_tables(self, dev):
-        K = self.layers
-        return dict(scalar_params=_scalar_table(
-            K, dev, b1=_stack_scalar(self.beta1), b2=_stack_scalar(self.beta2),
-            b3=_stack_scalar(self.beta3), ss2=_stack_scalar(self.ss2),
-            the=_stack_scalar(self.active_para1), thz=_stack_scalar(self.active_para),
-            s1=_stack_scalar(self.ss1)))
+    def _table_spec(self):
+        return {"scalar": dict(b1=self.beta1, b2=self.beta2, b3=self.beta3, ss2=self.ss2,
+                               the=self.active_para1, thz=self.active_para, s1=self.ss1)}
 
 
 class DLADMMNetLasso(DLADMMNetScalar):
@@ -504,12 +611,9 @@ class DLADMMNetLasso(DLADMMNetScalar):
         self._plist("active_para", (1, 1), 0.2)
         self.fc = nn.ModuleList([nn.Linear(self.m, self.d, bias=False) for _ in range(self.layers)])
 
-    def _build_tables(self, dev):
-        K = self.layers
-        return dict(scalar_params=_scalar_table(
-            K, dev, b1=_stack_scalar(self.beta1), b3=_stack_scalar(self.beta3),
-            ss2=_stack_scalar(self.ss2_1), ss2b=_stack_scalar(self.ss2_2),
-            thz=_stack_scalar(self.active_para), s1=1.0))
+    def _table_spec(self):
+        return {"scalar": dict(b1=self.beta1, b3=self.beta3, ss2=self.ss2_1, ss2b=self.ss2_2,
+                               thz=self.active_para, s1=1.0)}
 
 
 class DLADMMNetNewS(DLADMMNetScalar):
@@ -559,8 +663,8 @@ class DLADMMNetTiedNewS(DLADMMNetNewS):
     def _weights(self):
         return [self.fc.weight] * self.layers
 
-    def _build_tables(self, dev):
-        return DLADMMNetScalarTied._build_tables(self, dev)
+    def _table_spec(self):
+        return DLADMMNetScalarTied._table_spec(self)
 
 
 class DLADMMNetPTiedNewS(DLADMMNetTiedNewS):

@@ -270,11 +270,13 @@ _WS = {}
 
 
 def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
-    """Per-device cached workspace (grown on demand; torch's allocator keeps it 256-B aligned).
-
-    Reuse is stream-ordered: every call enqueues on the current stream of `dev`.
-    """
-    key = (dev.type, dev.index)
+    """Cached workspace per (device, stream), grown on demand (torch's allocator keeps it 256-B
+    aligned).  Reuse is safe because it is stream-ordered: a buffer is only ever used by calls
+    enqueued on the stream it was allocated on, so two streams of one device (say overlapping
+    eval and training) never share scratch memory, and a buffer dropped when it grows goes back
+    to the caching allocator under the one stream that used it."""
+    stream = torch.cuda.current_stream(dev)
+    key = (dev.type, dev.index, stream.cuda_stream)
     buf = _WS.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(nbytes, 1), device=dev, dtype=torch.uint8)

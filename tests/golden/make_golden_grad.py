@@ -55,17 +55,18 @@ def run_grad(cls, inp, sd, up, K, kind, dtype, interval=0, fwd_k=False):
             lk = alpha * torch.sum(torch.abs(Z[k]), dim=0).mean() + \
                 0.5 * torch.sum((X - torch.mm(A, Z[k])) ** 2.0, dim=0).mean()
         total = total + lk * coeffs[k]
-    for k in range(K):
+    for k in range(K if up is not None else 0):
         # newS: E[0] / L[0] are the inputs E0 / L0 (no parameter reaches them)
         total = total + (conv(up["Gz"][k]) * Z[k]).sum() + (conv(up["Ge"][k]) * E[k]).sum() + \
             (conv(up["Gl"][k]) * L[k]).sum()
-    if "Gt" in up:
+    if up is not None and "Gt" in up:
         T = out[3]
         for j in range(K + 1):
             total = total + (conv(up["Gt"][j]) * T[j]).sum()
     total.backward()
     grads = {k: (p.grad.detach().numpy().copy() if p.grad is not None
                  else np.zeros(tuple(p.shape))) for k, p in net.named_parameters()}
+    run_grad.none_keys = [k for k, p in net.named_parameters() if p.grad is None]
     return grads, float(total.detach())
 
 
@@ -100,12 +101,41 @@ def make_one(name, gdef, ref_root):
           f"max fp32-vs-fp64 grad gap {worst:.2e}")
 
 
+def make_none_keys(ref_root):
+    """tests/golden/grad_none_keys.json: the parameters whose .grad the REFERENCE autograd
+    leaves None (outside the loss graph; the .npz fixtures store zeros for them), for every
+    gradient fixture's loss and for the bare training loss (Z terms only, no linear terms)."""
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    nn.Module.cuda = lambda self, *a, **k: self
+    out = {}
+    for name, gdef in problems.GRAD_FIXTURES.items():
+        defn = problems.grad_defn(gdef)
+        variant = defn["variant"]
+        cls = load_ref_cls(os.path.join(ref_root, problems.VARIANT_SOURCES[variant]))
+        inp, sd = problems.build_problem(defn)
+        up = problems.make_upstream(defn, problems.VARIANT_SPECS[variant]["ret_t"])
+        kw = dict(interval=defn.get("interval", 0),
+                  fwd_k=problems.VARIANT_SPECS[variant].get("fwd_k", False))
+        rec = {}
+        for tag, u in (("fixture_loss", up), ("training_loss", None)):
+            run_grad(cls, inp, sd, u, defn["K"], gdef["loss"], torch.float32, **kw)
+            rec[tag] = run_grad.none_keys
+        out[name] = rec
+        print(name, rec)
+    with open(os.path.join(HERE, "grad_none_keys.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--none-keys", action="store_true")
     ap.add_argument("names", nargs="*")
     a = ap.parse_args()
     torch.set_num_threads(8)
+    if a.none_keys:
+        make_none_keys(a.ref)
+        return
     for nm in a.names or list(problems.GRAD_FIXTURES):
         make_one(nm, problems.GRAD_FIXTURES[nm], a.ref)
 
