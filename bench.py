@@ -49,9 +49,10 @@ def parse():
                          "(config 4: --m 512 --n 2048 --layers 40)")
     ap.add_argument("--alpha", type=float, default=0.001)
     ap.add_argument("--lean", action="store_true", help="write only the last layer (not default)")
-    ap.add_argument("--precision", default="f32", choices=["f32", "bf16"],
-                    help="bf16 = BASELINE config 5 mode (bf16 MFMA operands, fp32 state): "
-                         "--precision bf16 --m 1024 --n 4096 --batch 16384")
+    ap.add_argument("--precision", default="f32", choices=["f32", "f32_split", "bf16"],
+                    help="f32_split = fp32 GEMMs on the f16 matrix cores (exact hi/lo split, 3 "
+                         "products, fp32 accumulation); bf16 = BASELINE config 5 mode (bf16 MFMA "
+                         "operands, fp32 state): --precision bf16 --m 1024 --n 4096 --batch 16384")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=8192, help="columns of the CPU sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))

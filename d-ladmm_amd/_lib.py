@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DLADMM_LIB") or os.path.join(HERE, "lib", "libdladmm_hip.so")
 
 ABI_VERSION = 4
-PREC_F32, PREC_BF16 = 0, 1
+PREC_F32, PREC_BF16, PREC_F32_SPLIT = 0, 1, 2
 MAX_LAYERS = 65536
 MAX_LAYERS_V1 = 64
 NSCALAR = 8

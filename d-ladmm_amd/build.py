@@ -16,8 +16,8 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-UNITS = ("dladmm_capi.hip", "dladmm_fused.hip", "dladmm_layered.hip", "dladmm_backward.hip",
-         "dladmm_lskm.hip", "dladmm_eval.hip", "dladmm_tile_bf16.hip")
+UNITS = ("dladmm_capi.hip", "dladmm_fused.hip", "dladmm_fused_x3.hip", "dladmm_layered.hip",
+         "dladmm_backward.hip", "dladmm_lskm.hip", "dladmm_eval.hip", "dladmm_tile_bf16.hip")
 HEADERS = (os.path.join(ROOT, "include", "dladmm.h"), os.path.join(CSRC, "dladmm_common.h"),
            os.path.join(CSRC, "dladmm_internal.h"), os.path.join(CSRC, "dladmm_slice.h"),
            os.path.join(CSRC, "dladmm_layer_epi.h"))
@@ -26,6 +26,9 @@ OBJ = os.path.join(HERE, "lib", "obj")
 ARCH = os.environ.get("DLADMM_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", f"--offload-arch={ARCH}",
          "-I", os.path.join(ROOT, "include")]
+# per-unit extras: the split-f16 kernel keeps scalar f32 VALU beside its MFMAs (packed v_pk_*
+# f32 ops issue slower there; MI355X_MICROARCH.md, price of one filler beside MFMAs)
+UNIT_FLAGS = {"dladmm_fused_x3.hip": ["-fno-slp-vectorize"]}
 
 
 def hipcc() -> str:
@@ -63,7 +66,8 @@ def build(force: bool = False, verbose: bool = True, extra_flags=()) -> str:
         obj = os.path.join(OBJ, u.replace(".hip", ".o"))
         objs.append(obj)
         if force or extra_flags or _stale(obj, [src] + list(HEADERS)):
-            jobs.append([cc] + FLAGS + list(extra_flags) + ["-c", src, "-o", obj])
+            jobs.append([cc] + FLAGS + UNIT_FLAGS.get(u, []) + list(extra_flags) +
+                        ["-c", src, "-o", obj])
 
     def run(cmd):
         if verbose:

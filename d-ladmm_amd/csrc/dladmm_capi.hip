@@ -66,6 +66,69 @@ __global__ __launch_bounds__(256) void pack_frags_kernel(const PackArgs p) {
   reinterpret_cast<f32x4*>(p.dst)[((int64_t)t * p.RB * p.CB + fr) * 64 + lane] = v;
 }
 
+// ------------------------------------------------------------------------ split-f16 packing
+// (DLADMM_PREC_F32_SPLIT, dladmm_fused_x3.hip).  Matrix M (R x C valid, zero padded to RB
+// blocks of 16 rows x KS steps of 32) -> per-tensor scale 2^sw (max|M| * 2^sw in [2^14, 2^15)),
+// then x = sign * M * 2^sw split into hi = f16(x), lo = f16(x - hi).  Fragment (ib, s) = step
+// ib*KS + s: [hi | lo][lane] f16x8, lane l = row 16 ib + (l & 15), element q = column
+// 32 s + 16 (q >> 2) + 4 (l >> 4) + (q & 3) -- the k order in which the state registers of two
+// consecutive 16-row blocks form one v_mfma_f32_16x16x32_f16 B operand.
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+struct X3PackArgs {
+  const float* src[kPackBatch];
+  int R, C, RB, KS, t0;
+  int64_t ld;
+  float sign;
+  f16x8_t* dst;          // [T][RB*KS][2][64]
+  unsigned* umax;        // [t0 + T] max |M| bits
+  int* wexp;             // [t0 + T] scale exponents
+};
+static_assert(sizeof(X3PackArgs) <= 2048, "kernel argument size");
+
+__global__ __launch_bounds__(256) void absmax_kernel(const X3PackArgs p) {
+  const int t = blockIdx.y;
+  const float* src = p.src[t];
+  const int64_t total = (int64_t)p.R * p.C;
+  float mx = 0.0f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256)
+    mx = fmaxf(mx, fabsf(src[(i / p.C) * p.ld + i % p.C]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    atomicMax(p.umax + p.t0 + t, __float_as_uint(mx));  // non-negative floats order as uints
+  }
+}
+
+__global__ __launch_bounds__(256) void pack_x3_kernel(const X3PackArgs p) {
+  const int t = blockIdx.y;
+  const int st = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (st >= p.RB * p.KS) return;
+  const int lane = threadIdx.x & 63;
+  const int ib = st / p.KS, ks = st % p.KS;
+  int sw = 15 - __builtin_amdgcn_frexp_expf(__uint_as_float(p.umax[p.t0 + t]));
+  sw = sw < -126 ? -126 : (sw > 126 ? 126 : sw);
+  if (st == 0 && lane == 0) p.wexp[p.t0 + t] = sw;
+  const float f = p.sign * __builtin_amdgcn_ldexpf(1.0f, sw);
+  const float* src = p.src[t];
+  const int row = 16 * ib + (lane & 15);
+  f16x8_t hi, lo;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int c = 32 * ks + 16 * (q >> 2) + 4 * (lane >> 4) + (q & 3);
+    const float x = (row < p.R && c < p.C) ? src[(int64_t)row * p.ld + c] * f : 0.0f;
+    const _Float16 h = (_Float16)x;
+    hi[q] = h;
+    lo[q] = (_Float16)(x - (float)h);
+  }
+  f16x8_t* d = p.dst + ((int64_t)t * p.RB * p.KS + st) * 128;
+  d[lane] = hi;
+  d[64 + lane] = lo;
+}
+
 // ------------------------------------------------------------------------ loss reduction
 // per-column objective terms: out[r][b] = sum_s part[r][s][b] over the slices, in order
 __global__ __launch_bounds__(256) void col_loss_kernel(const float* part, int nslice, int ldl,
@@ -138,7 +201,7 @@ inline int pick_shape(int m, int n) {
 inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
 struct Plan {
-  int path;  // 1 fused, 2 per-layer
+  int path;  // 1 fused, 2 per-layer, 3 bf16 tiles, 4 fused split-f16
   // fused
   int shape, MP, NP, tiles;
   // per-layer
@@ -147,6 +210,8 @@ struct Plan {
   int ldl;     // columns per slice
   int nbp;     // bf16 path: 16-column blocks of the packed state
   size_t off_ap, off_wp, off_v, off_zb, off_zw, off_ew, off_lw, off_loss, total;
+  size_t off_wexp, off_umax;  // path 4
+  int64_t ldzw;               // path 4: lean-mode Z_k workspace row stride
 };
 
 inline int validate(const dladmm_fwd_desc* d) {
@@ -163,7 +228,8 @@ inline int validate(const dladmm_fwd_desc* d) {
     if (!d->W[k]) return DLADMM_E_NULL;
   if (d->loss_kind && !d->loss_sums) return DLADMM_E_NULL;
   if (d->col_loss && !d->loss_kind) return DLADMM_E_UNSUPPORTED;
-  if (d->precision != DLADMM_PREC_F32 && d->precision != DLADMM_PREC_BF16)
+  if (d->precision != DLADMM_PREC_F32 && d->precision != DLADMM_PREC_BF16 &&
+      d->precision != DLADMM_PREC_F32_SPLIT)
     return DLADMM_E_UNSUPPORTED;
   const int v = d->variant;
   if (v == DLADMM_V2_LTHETA || v == DLADMM_V3_FULL) {
@@ -210,6 +276,30 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
   const char* force = getenv("DLADMM_PATH");
   const bool force_layered = force && force[0] == 'l';
   const bool bf16 = d->precision == DLADMM_PREC_BF16;
+  // split-f16 fused kernel: register-resident shapes, scalar-parameter variants (V4-V6); other
+  // cases run the fp32 kernels (same results up to fp32 GEMM rounding)
+  if (s >= 0 && fits_32bit(d) && !force_layered && d->precision == DLADMM_PREC_F32_SPLIT &&
+      x3_supports(d->variant)) {
+    p->path = 4;
+    p->shape = s;
+    p->MP = kShapeMP[s];
+    p->NP = kShapeNP[s];
+    p->tiles = ceil_div(d->batch, kTileCols);
+    p->ldl = p->tiles * kTileCols;
+    p->nslots = p->ldl;
+    p->ldzw = p->ldl;
+    const size_t tb = (size_t)p->MP * p->NP * 2 * sizeof(_Float16);  // hi + lo per tensor
+    const int nw = shared_weight(d) ? 1 : K;
+    p->off_ap = 0;
+    p->off_wp = align256(tb);
+    p->off_wexp = p->off_wp + align256(tb * nw);
+    p->off_umax = p->off_wexp + align256((size_t)(nw + 1) * sizeof(int));
+    p->off_zw = p->off_umax + align256((size_t)(nw + 1) * sizeof(unsigned));
+    const bool lean = !d->keep_all && K > 1;
+    p->off_loss = p->off_zw + (lean ? align256((size_t)2 * d->n * p->ldzw * sizeof(float)) : 0);
+    p->total = p->off_loss + align256((size_t)2 * K * p->nslots * sizeof(float));
+    return 0;
+  }
   if (s >= 0 && fits_32bit(d) && !force_layered && !bf16) {
     p->path = 1;
     p->shape = s;
@@ -311,6 +401,65 @@ inline int run_fused(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStrea
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_start, s)) return (int)e;
   }
   if (hipError_t e = launch_fused_shape(p.shape, d->variant, a, p.tiles, s)) return (int)e;
+  if (d->ev_kernel_stop) {
+    if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_stop, s)) return (int)e;
+  }
+  return 0;
+}
+
+// absmax + split pack of T sources (scale exponents at wexp[t0 ..]), kPackBatch per launch
+inline hipError_t pack_x3(const float* const* srcs, int T, int R, int C, int64_t ld, int RB,
+                          int KS, float sign, _Float16* dst, unsigned* umax, int* wexp, int t0,
+                          hipStream_t s) {
+  for (int b = 0; b < T; b += kPackBatch) {
+    const int nb = T - b < kPackBatch ? T - b : kPackBatch;
+    X3PackArgs pa{};
+    for (int t = 0; t < nb; ++t) pa.src[t] = srcs[b + t];
+    pa.R = R; pa.C = C; pa.RB = RB; pa.KS = KS; pa.t0 = t0 + b; pa.ld = ld; pa.sign = sign;
+    pa.dst = reinterpret_cast<f16x8_t*>(dst) + (size_t)b * RB * KS * 128;
+    pa.umax = umax; pa.wexp = wexp;
+    const int blocks = ceil_div((int)(((int64_t)R * C + 255) / 256), 8);
+    hipLaunchKernelGGL(absmax_kernel, dim3(blocks < 64 ? blocks : 64, nb), dim3(256), 0, s, pa);
+    if (hipError_t e = hipGetLastError()) return e;
+    hipLaunchKernelGGL(pack_x3_kernel, dim3(ceil_div(RB * KS, 4), nb), dim3(256), 0, s, pa);
+    if (hipError_t e = hipGetLastError()) return e;
+  }
+  return hipSuccess;
+}
+
+inline int run_fused_x3(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStream_t s) {
+  _Float16* Ap = (_Float16*)(ws + p.off_ap);
+  _Float16* Wp = (_Float16*)(ws + p.off_wp);
+  int* wexp = (int*)(ws + p.off_wexp);
+  unsigned* umax = (unsigned*)(ws + p.off_umax);
+  const int MB = p.MP / 16, NB = p.NP / 16, KS1 = p.MP / 32, KS2 = p.NP / 32;
+  const bool shared = shared_weight(d);
+  const int nw = shared ? 1 : d->layers;
+  if (hipError_t e = hipMemsetAsync(umax, 0, (size_t)(nw + 1) * sizeof(unsigned), s)) return (int)e;
+  // A (rows m, contraction n) and every -W_k (rows n, contraction m)
+  const float* asrc[1] = {d->A};
+  if (hipError_t e = pack_x3(asrc, 1, d->m, d->n, d->ld_a, MB, KS2, 1.0f, Ap, umax, wexp, 0, s))
+    return (int)e;
+  if (hipError_t e = pack_x3(d->W, nw, d->n, d->m, d->ld_w, NB, KS1, -1.0f, Wp, umax, wexp, 1, s))
+    return (int)e;
+  FusedArgs a{};
+  a.m = d->m; a.n = d->n; a.B = d->batch; a.K = d->layers;
+  a.keep_all = d->keep_all ? 1 : 0; a.loss_kind = d->loss_kind; a.ldl = p.ldl;
+  a.X = d->X; a.ldx = d->ld_x;
+  a.Z0 = d->Z0; a.ldz0 = d->ld_z0;
+  a.E0 = d->E0; a.lde0 = d->ld_e0;
+  a.L0 = d->L0; a.ldl0 = d->ld_l0;
+  a.Ap = (const float*)Ap; a.Wp = (const float*)Wp;
+  a.wstep = shared ? 0 : 1;
+  a.scal = d->scalar_params;
+  a.Zo = d->Z; a.Eo = d->E; a.Lo = d->L; a.To = d->T; a.ldo = d->ld_out;
+  a.lossp = (float*)(ws + p.off_loss);
+  a.wexp = wexp;
+  a.Zw = (float*)(ws + p.off_zw); a.ldzw = p.ldzw;
+  if (d->ev_kernel_start) {
+    if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_start, s)) return (int)e;
+  }
+  if (hipError_t e = launch_fused_x3_shape(p.shape, d->variant, a, p.tiles, s)) return (int)e;
   if (d->ev_kernel_stop) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_stop, s)) return (int)e;
   }
@@ -660,7 +809,9 @@ int dladmm_fwd_f32(const dladmm_fwd_desc* d, void* stream) {
   if (((uintptr_t)d->workspace) & 255) return DLADMM_E_ALIGN;
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)d->workspace;
-  const int rc = p.path == 1 ? run_fused(d, p, ws, s) : run_layered(d, p, ws, s);
+  const int rc = p.path == 1   ? run_fused(d, p, ws, s)
+                 : p.path == 4 ? run_fused_x3(d, p, ws, s)
+                               : run_layered(d, p, ws, s);
   if (rc) return rc;
   // per-layer loss sums, fixed-order fp64 reduction of the per-column partials
   if (d->loss_kind) {

@@ -1,0 +1,595 @@
+// dladmm_fused_x3.hip -- MI355X (gfx950) fused K-layer D-LADMM forward whose fp32 GEMMs run on
+// the f16 matrix cores (DLADMM_PREC_F32_SPLIT).
+//
+// Same contract and the same one-launch, register-resident design as dladmm_fused.hip (the
+// whole K-layer loop of DLADMMNet.forward -- main_lena.py:57-98, main_syn_l1l1_scalar.py:80-127,
+// main_syn_lasso_scalar.py:65-114 -- in one kernel; state in registers in the MFMA C/D layout;
+// every elementwise update in fp32 in the reference's operation order).  What changes is how
+// each fp32 product M * S (M = -W_k or A, S = Var or Z) is formed:
+//
+//   * both operands are scaled by powers of two (M per tensor, by the pack kernel; S per batch
+//     column) so that their magnitudes sit at the top of the f16 range, then split exactly as
+//     x = hi + lo with hi = f16(x), lo = f16(x - hi): hi + lo carries 22 significant bits;
+//   * M S = Mhi Shi + Mhi Slo + Mlo Shi, three v_mfma_f32_16x16x32_f16 per 16 x 16 x 32 block,
+//     accumulated in fp32 (each product of two f16 is exact in fp32); the dropped Mlo Slo term
+//     is 2^-22 of the product; the result is scaled back by one exact power-of-two multiply.
+//   The error is that of an fp32 GEMM (measured: tools/probe/f16mfma.hip, 2.3e-7 vs 3.2e-7
+//   norm-relative for the native fp32 MFMA chain, vs fp64), at 3 x 16 cycles per 16 x 16 x 32
+//   block instead of 8 x 32 cycles for v_mfma_f32_16x16x4_f32.
+//
+// Geometry: one workgroup = 4 waves = 64 batch columns, wave w owns 16 columns; lane l holds
+// column l & 15 and rows 16 b + 4 (l >> 4) + r of every state block b.  A 16 x 16 x 32 k-step
+// s contracts rows 32 s .. 32 s + 31 = state blocks 2 s and 2 s + 1, i.e. exactly the lane's
+// registers [2s][0..3] and [2s+1][0..3]: the packed weight fragments carry the matching k order,
+// so the accumulator of one GEMM (after the epilogue) is the B operand of the next with no lane
+// movement.
+//
+// Registers.  The split operands live in AGPRs (MFMA srcB may be an AGPR): Vpk (Var, B operand
+// of G1, KS1 k-steps) and Zpk (Z_k, B operand of G2, KS2 k-steps).  fp32 Z is NOT kept across a
+// layer: G1's epilogue writes Z_k (output, or workspace in lean mode) and splits it into Zpk
+// right away, with a provisional column scale (the previous layer's column max + kHead bits of
+// headroom); G1(k+1)'s epilogue re-reads Z_k from memory kLA blocks ahead.  If a column of Z_k
+// outgrew the provisional scale (checked exactly at the end of G1), the wave re-reads Z_k and
+// re-splits it with the exact scale (rare: first layer).  fp32 Var is kept (it is not an
+// output) and split with its exact column scale at the start of G1.
+//
+// Weight stream: -W_k and A, packed as [step][hi|lo][64 lanes] f16x8 fragments (1 KiB each, 2
+// per k-step), stream through a 4-slot LDS ring of 16 KiB chunks by LDS-DMA (three chunks in
+// flight); the ring barrier waits with a counted vmcnt that leaves every younger VM operation
+// (stores, Z re-reads, the next chunks' DMA) in flight.
+#include "dladmm_common.h"
+#include "dladmm_internal.h"
+
+namespace dladmm {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+namespace x3 {
+
+constexpr int kSlots = 4;  // LDS ring slots
+constexpr int kLA = 2;     // Z_{k-1} re-read look-ahead, in 16-row blocks
+constexpr int kHead = 12;  // provisional-scale headroom (bits) of the in-epilogue Z split
+
+__device__ __forceinline__ f32x4 mfma(const f16x8& a, const f16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+struct BOp {
+  f16x8 hi, lo;
+};
+
+// x = v * sc (exact: sc is a power of two) -> hi = f16(x), lo = f16(x - hi), each one RNE
+// rounding (fma(v, sc, 0) / fma(v, sc, -hi) lower to v_fma_mix{lo,hi}_f16)
+__device__ __forceinline__ void split4(const float (&v)[4], float sc, f16x8& hi, f16x8& lo,
+                                       int o) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const _Float16 h = (_Float16)__builtin_fmaf(v[j], sc, 0.0f);
+    hi[o + j] = h;
+    lo[o + j] = (_Float16)__builtin_fmaf(v[j], sc, -(float)h);
+  }
+}
+__device__ __forceinline__ BOp split8(const float (&a)[4], const float (&b)[4], float sc) {
+  BOp r;
+  split4(a, sc, r.hi, r.lo, 0);
+  split4(b, sc, r.hi, r.lo, 4);
+  return r;
+}
+
+__device__ __forceinline__ void pin_agpr_b(BOp& b) {
+  asm("" : "+a"(b.hi));
+  asm("" : "+a"(b.lo));
+}
+
+// the 4 lane groups holding one batch column (lanes l, l^16, l^32, l^48)
+__device__ __forceinline__ float col_max(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+
+// column scale exponent: mx * 2^s in [2^14, 2^15) (f16 max 65504), clamped so that 2^s and the
+// combined inverse 2^-(s + sw) stay representable
+__device__ __forceinline__ int scale_exp(float mx, int sw, int head) {
+  int s = 15 - head - __builtin_amdgcn_frexp_expf(mx);
+  const int hi = 149 - sw < 126 ? 149 - sw : 126;
+  s = s < -126 ? -126 : s;
+  return s > hi ? hi : s;
+}
+__device__ __forceinline__ float exp2i(int e) { return __builtin_amdgcn_ldexpf(1.0f, e); }
+
+// Static VM-operation windows of the ring barriers.  The barrier of chunk ch sits at position
+// SPC-D of the chunk (D = fragment read-ahead in steps) and waits for chunk ch+1, whose DMA was
+// issued at the barrier 3 chunks earlier; younger: the bodies of the 3*SPC steps since, and the DMAs of chunks ch+2, ch+3.
+// Counted here: the stores and loads every step body issues unconditionally.  A step of the
+// other pass type (the window reaching back across a pass boundary) counts with that pass's
+// schedule; the unrolled tails between passes only add younger operations (not counted: a
+// lower bound only waits longer).
+template <int MB, int NB, int KS1, int KS2, int SPC, int ELOADS>
+struct Win {
+  static constexpr int ST = NB * KS1;
+  static constexpr int DMA = (2 * SPC + 3) / 4;
+  static constexpr int row_step(int r, int KS) { return (r * KS) / 4; }
+  static constexpr int rows_at(int s, int KS) {
+    int c = 0;
+    for (int r = 0; r < 4; ++r) c += row_step(r, KS) == s ? 1 : 0;
+    return c;
+  }
+  // G1 step body: rows of block ib-1 (Z store) + the re-read of block ib-1+kLA
+  static constexpr int ops1(int t) {
+    const int ib = t / KS1, s = t % KS1;
+    if (ib == 0) return 0;
+    return rows_at(s, KS1) * (1 + (ib - 1 + kLA < NB ? 1 : 0));
+  }
+  // G2 step body: rows of block ib-1 (E, L, T stores; V1: 3 beta loads)
+  static constexpr int ops2(int t) {
+    const int ib = t / KS2, s = t % KS2;
+    if (ib == 0) return 0;
+    return rows_at(s, KS2) * (3 + ELOADS);
+  }
+  template <int T, bool G1>
+  static constexpr int win() {
+    int n = 2 * DMA;
+    for (int u = T - 3 * SPC; u < T; ++u) {
+      if (u >= 0) n += G1 ? ops1(u) : ops2(u);
+      else if (ST + u >= 0) n += G1 ? ops2(ST + u) : ops1(ST + u);
+    }
+    return n < 63 ? n : 63;
+  }
+};
+
+}  // namespace x3
+
+template <int MP, int NP, int EMODE, int PKIND>
+__global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
+  using namespace x3;
+  constexpr int MB = MP / 16, NB = NP / 16, KS1 = MP / 32, KS2 = NP / 32;
+  constexpr int ST = NB * KS1;  // k-steps of either GEMM
+  static_assert(ST == MB * KS2, "both GEMMs have MP*NP/512 steps");
+  static_assert(MB % 2 == 0 && NB % 2 == 0, "k-steps cover two 16-row blocks");
+  constexpr int SPC = ST < 8 ? ST : 8;  // steps per ring chunk
+  static_assert(SPC >= 2 && ST % SPC == 0, "chunking");
+  constexpr int NCH = ST / SPC;
+  constexpr int D = ST >= 4 ? 2 : 1;  // fragment read-ahead (steps)
+  constexpr int R = 2 * D;            // fragment register rotation; divides ST, so every pass
+                                      // starts at rotation 0
+  static_assert(ST % R == 0 && SPC >= D + 1, "rotation");
+  constexpr int FPC = 2 * SPC;  // 1 KiB fragments per chunk
+  constexpr int RING_F4 = kSlots * FPC * 64;
+  constexpr int X_F4 = kWaves * MB * 64;
+  static_assert((RING_F4 + X_F4) * 16 <= 160 * 1024, "LDS budget");
+  static_assert(PKIND == PK_SCALAR || PKIND == PK_S1, "x3 path: scalar-parameter variants");
+  using W = Win<MB, NB, KS1, KS2, SPC, 0>;
+  __shared__ f32x4 smem[RING_F4 + X_F4];
+  f32x4* ring = smem;
+  f32x4* xs = smem + RING_F4;  // xs[w][b][lane] = X rows 16b+4g+0..3 of this lane's column
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 15, g = lane >> 4;
+  const int64_t col = (int64_t)blockIdx.x * kTileCols + w * 16 + j;
+  const bool cv = col < a.B;
+  const int m = a.m, n = a.n, K = a.K;
+  const bool lossz = a.loss_kind != 0;
+  const bool lasso = __builtin_amdgcn_readfirstlane(a.loss_kind) == DLADMM_LOSS_LASSO;
+  auto lane_off = [&](int64_t ld) -> uint32_t {
+    return cv ? (uint32_t)((col + (int64_t)(4 * g) * ld) * 4) : kOOB;
+  };
+  constexpr bool kEState = EMODE != EM_V1;  // V1 never reads E_{k-1} (main_lena.py:87)
+
+  float Er[MB][4], Lr[MB][4], Vr[MB][4];
+  BOp Vpk[KS1], Zpk[KS2];
+  float regsum = 0.f, fit1 = 0.f, fit2 = 0.f;
+
+  // ---------------------------------------------------------------- weight stream
+  // GEMM gi: 0 = prologue A, 2k+1 = -W_k, 2k+2 = A; past the last GEMM, A again as filler.
+  const int64_t wl = (int64_t)ST * 2 * kFrag;  // floats per packed tensor: ST x (hi, lo) KiB
+  auto gsrc = [&](int gi) -> const float* {
+    const int kk = gi >> 1;
+    return ((gi & 1) && kk < K) ? a.Wp + (int64_t)(kk * a.wstep) * wl : a.Ap;
+  };
+  auto chunk_src = [&](int gi, int ch) -> const float* {
+    uint64_t sb = (uint64_t)gsrc(gi + ch / NCH);
+    asm volatile("" : "+s"(sb));
+    return (const float*)sb + (int64_t)(ch % NCH) * FPC * kFrag;
+  };
+  auto issue = [&](const float* base, int slot) {
+    f32x4* dst = ring + slot * (FPC * 64);
+#pragma unroll
+    for (int i = 0; i < (FPC + 3) / 4; ++i) {
+      const int f = i * 4 + w;
+      if (FPC % 4 == 0 || f < FPC) glds16(base + f * kFrag, lane * 16, dst + f * 64);
+    }
+  };
+  auto slot_add = [](int s, int d) -> int { s += d; return s >= kSlots ? s - kSlots : s; };
+  int cur = 0;
+  auto frag = [&](int slot, int f) -> f16x8 {
+    return __builtin_bit_cast(f16x8, ring[(slot * FPC + f) * 64 + lane]);
+  };
+
+  // ---------------------------------------------------------------- parameters
+  struct LayerP { float b1n, b2, b3, ss2, ss2b, s1; ShrinkP the, thz; };
+  auto layer_params = [&](int k) -> LayerP {
+    LayerP p{};
+    const int kk = k < 0 ? 0 : k;
+    const int kn = k < 0 ? 0 : (k + 1 < K ? k + 1 : k);
+    cfloat_p sp = (cfloat_p)a.scal + kk * DLADMM_NSCALAR;
+    p.b2 = sp[DLADMM_P_BETA2];
+    p.b3 = sp[DLADMM_P_BETA3];
+    p.ss2 = sp[DLADMM_P_SS2];
+    p.ss2b = sp[DLADMM_P_SS2B];
+    p.the = shrink_params(sp[DLADMM_P_THETA_E]);
+    p.thz = shrink_params(sp[DLADMM_P_THETA_Z]);
+    if constexpr (PKIND == PK_S1) p.s1 = sp[DLADMM_P_S1];
+    p.b1n = ((cfloat_p)a.scal)[kn * DLADMM_NSCALAR + DLADMM_P_BETA1];
+    return p;
+  };
+  // weight scale exponents (pack kernel): wexp[0] = A, wexp[1 + k] = -W_k (shared: wexp[1])
+  const int sw_a = __builtin_amdgcn_readfirstlane(a.wexp[0]);
+  auto sw_w = [&](int k) -> int {
+    return __builtin_amdgcn_readfirstlane(a.wexp[1 + (a.wstep ? k : 0)]);
+  };
+
+  // ---------------------------------------------------------------- initial state
+  const uint32_t oz0 = lane_off(a.ldz0), oo = lane_off(a.ldo), ozw = lane_off(a.ldzw);
+  float zmx = 0.f;       // lane max of |Z_k| of the layer being formed
+  float zmx_prev;         // column max of Z_{k-1} (Z0 first), exact
+  int zexp;               // scale exponent the current Zpk was split with
+  {
+    const rsrc_t re = mkrsrc(a.E0, (uint32_t)(m * a.lde0 * 4));
+    const rsrc_t rl = mkrsrc(a.L0, (uint32_t)(m * a.ldl0 * 4));
+    const rsrc_t rx = mkrsrc(a.X, (uint32_t)(m * a.ldx * 4));
+    const uint32_t oe = lane_off(a.lde0), ol = lane_off(a.ldl0), ox = lane_off(a.ldx);
+#pragma unroll
+    for (int b = 0; b < MB; ++b) {
+      f32x4 xv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        xv[r] = bload(rx, ox + (uint32_t)((16 * b + r) * a.ldx * 4));
+        Er[b][r] = bload(re, oe + (uint32_t)((16 * b + r) * a.lde0 * 4));
+        Lr[b][r] = bload(rl, ol + (uint32_t)((16 * b + r) * a.ldl0 * 4));
+      }
+      xs[(w * MB + b) * 64 + lane] = xv;  // read back only by this wave
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // Z0: exact column max, then re-read and split (no fp32 copy of Z0 stays live)
+    const rsrc_t rz = mkrsrc(a.Z0, (uint32_t)(n * a.ldz0 * 4));
+    float mx = 0.f;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        mx = fmaxf(mx, fabsf(bload(rz, oz0 + (uint32_t)((16 * b + r) * a.ldz0 * 4))));
+      if (b % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // at most 16 loads in flight
+    }
+    zmx_prev = col_max(mx);
+    zexp = scale_exp(zmx_prev, sw_a, 0);
+    const float sc = exp2i(zexp);
+#pragma unroll
+    for (int s = 0; s < KS2; ++s) {
+      float va[4], vb[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        va[r] = bload(rz, oz0 + (uint32_t)((32 * s + r) * a.ldz0 * 4));
+        vb[r] = bload(rz, oz0 + (uint32_t)((32 * s + 16 + r) * a.ldz0 * 4));
+      }
+      Zpk[s] = split8(va, vb, sc);
+      pin_agpr_b(Zpk[s]);
+      if (s % 2 == 1) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  const uint32_t mbytes = (uint32_t)(m * a.ldo * 4);
+  SWalk zw{0u, (uint32_t)(a.ldo * 4)}, mw{0u, (uint32_t)(a.ldo * 4)};
+  SWalk zr{0u, (uint32_t)(a.ldo * 4)};  // Z_{k-1} re-read walker (row stride set per layer)
+
+  // ---------------------------------------------------------------- epilogues
+  // G1 block b, row r of layer k: Z = S(Z_{k-1} + s1 * q, theta_z) with q = -W_k Var (the packed
+  // weights are negated), main_lena.py:86 / main_syn_l1l1_scalar_tied.py:114
+  float zn[2][4];   // fp32 Z_k of the current block pair, split into Zpk when complete
+  float zo[kLA + 1][4];  // re-read Z_{k-1} of the next blocks (ring over blocks)
+  auto epi1_row = [&](const LayerP& P, rsrc_t rzo, uint32_t vzo, const SWalk& zs, int b, int r,
+                      float q) {
+    const float zp = zo[b % (kLA + 1)][r];
+    const float u = (PKIND == PK_S1) ? zp + P.s1 * q : zp + q;
+    const float z = shrink_u(u, P.thz);
+    zn[b & 1][r] = z;
+    bstore_s(rzo, vzo, zs.at(r), z);
+    regsum += fabsf(z);
+    zmx = fmaxf(zmx, fabsf(z));
+    // materialise the running sums here: left alone, the scheduler sinks both serial chains
+    // below the pass and keeps every row's z live (spills)
+    asm volatile("" : "+v"(regsum), "+v"(zmx));
+  };
+  // G2 block b, row r of layer k (Pv = A Z_k, x = X).  pro: T0 = A Z0 + E0 - X, Var_0.
+  struct OutR { rsrc_t e, l, t; };
+  float vmx = 0.f;
+  auto epi2_row = [&](const LayerP& P, const OutR& O, bool pro, int b, int r, float Pv, float x,
+                      uint32_t so) {
+    const float l0 = Lr[b][r];
+    const float e0 = Er[b][r];
+    float e;
+    if constexpr (EMODE == EM_V1) {
+      e = shrink_u((x - Pv) - P.b2 * l0, P.the);                     // main_lena.py:87
+    } else if constexpr (EMODE == EM_VVAR) {
+      const float vv = l0 + P.b2 * ((Pv + e0) - x);                  // scalar :114
+      e = shrink_u(e0 - P.ss2 * vv, P.the);                          // scalar :115
+    } else {
+      e = P.ss2 * (x - Pv) - P.ss2b * l0;                            // lasso :102-103
+    }
+    e = pro ? e0 : e;
+    const float t = (Pv + e) - x;                                    // main_lena.py:88
+    float l = l0 + P.b3 * t;                                         // main_lena.py:89
+    l = pro ? l0 : l;
+    Er[b][r] = e;
+    Lr[b][r] = l;
+    bstore_s(O.e, oo, so, e);
+    bstore_s(O.l, oo, so, l);
+    bstore_s(O.t, oo, so, t);
+    const float res = x - Pv;
+    fit1 += fabsf(res);
+    fit2 = __builtin_fmaf(res, res, fit2);
+    const float v = l + P.b1n * t;                                   // main_lena.py:85
+    vmx = fmaxf(vmx, fabsf(v));
+    asm volatile("" : "+v"(fit1), "+v"(fit2), "+v"(vmx));
+    Vr[b][r] = v;
+    pin_agpr(Vr[b][r]);  // AGPRs: Vr, Zpk (G2) / Vpk, Zpk (G1); VGPRs: E, L, fragments
+  };
+  auto flush_loss = [&](int k) {
+    if (lossz && k >= 0) {
+      const float rs = col_sum(regsum);
+      const float fs = lasso ? 0.5f * col_sum(fit2) : col_sum(fit1);
+      if (g == 0) {
+        const int64_t c = (int64_t)blockIdx.x * kTileCols + w * 16 + j;
+        a.lossp[(int64_t)(2 * k + 0) * a.ldl + c] = rs;
+        a.lossp[(int64_t)(2 * k + 1) * a.ldl + c] = fs;
+      }
+    }
+    regsum = 0.f;
+    fit1 = 0.f;
+    fit2 = 0.f;
+  };
+
+  // ---------------------------------------------------------------- ring steps
+  // Step t of a GEMM pass: head = read-ahead of step t+D's two fragments (at chunk position
+  // SPC-D: ring barrier, DMA of chunk ch+4 into the freed slot, first fragments of the next
+  // chunk), then the step body (epilogue rows / operand splits), then 3 MFMAs.
+  f16x8 frh[R], frl[R];
+  auto step_head = [&](auto T_, int gi, auto WIN_) {
+    constexpr int t = decltype(T_)::value;
+    constexpr int c = t % SPC, ch = t / SPC;
+    constexpr int tn = t + D;
+    if constexpr (c + D < SPC) {
+      frh[tn % R] = frag(cur, 2 * (c + D));
+      frl[tn % R] = frag(cur, 2 * (c + D) + 1);
+    } else {
+      // every wave has read all of chunk ch (its last fragments were read D steps ago)
+      if constexpr (c + D == SPC) {
+        ring_barrier_cnt<decltype(WIN_)::value>();
+        issue(chunk_src(gi, ch + kSlots), cur);
+      }
+      const int nx = slot_add(cur, 1);
+      frh[tn % R] = frag(nx, 2 * (c + D - SPC));
+      frl[tn % R] = frag(nx, 2 * (c + D - SPC) + 1);
+    }
+  };
+  auto step_tail = [&](auto T_) {
+    constexpr int t = decltype(T_)::value;
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (t % SPC == SPC - 1) cur = slot_add(cur, 1);
+  };
+  auto mfma3 = [&](int tr, const BOp& bop, f32x4 acc) -> f32x4 {
+    acc = mfma(frh[tr], bop.hi, acc);
+    acc = mfma(frh[tr], bop.lo, acc);
+    return mfma(frl[tr], bop.hi, acc);
+  };
+
+  // prime the ring: chunks 0..3 of the prologue GEMM, then steps 0 and 1's fragments
+#pragma unroll
+  for (int c = 0; c < kSlots; ++c) issue(chunk_src(0, c), c);
+  ring_barrier_cnt<(kSlots - 1) * W::DMA>();
+#pragma unroll
+  for (int t = 0; t < D; ++t) {
+    frh[t] = frag(0, 2 * t);
+    frl[t] = frag(0, 2 * t + 1);
+  }
+
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+
+  // ---------------------------------------------------------------- G1(k): -W_k Var -> Z_k
+  // Block ib's epilogue runs in block ib+1's steps (row r at step (r*KS1)/4) with the re-read
+  // of block ib-1+kLA of Z_{k-1}; Zpk[s] is split once blocks 2s, 2s+1 are complete; block 0's
+  // steps split Var into Vpk.  The last block's epilogue runs after the MFMAs.
+  auto g1_pass = [&](int k, const LayerP& P, rsrc_t rzo, uint32_t vzo, rsrc_t rzp,
+                     uint32_t vzp, float vsc, float vinv, float zsc) {
+    const int gi = 2 * k + 1;
+    zw.reset();
+    SWalk zs = zw;
+    f32x4 qp = zero4;
+    static_for<NB>([&](auto IB_) {
+      constexpr int ib = decltype(IB_)::value;
+      f32x4 acc = zero4;
+      static_for<KS1>([&](auto S_) {
+        constexpr int s = decltype(S_)::value;
+        constexpr int t = ib * KS1 + s;
+        step_head(std::integral_constant<int, t>{}, gi,
+                  std::integral_constant<int, W::template win<t, true>()>{});
+        if constexpr (ib == 0) {
+          Vpk[s] = split8(Vr[2 * s], Vr[2 * s + 1], vsc);
+          pin_agpr_b(Vpk[s]);
+        } else {
+          static_for<4>([&](auto R_) {
+            constexpr int r = decltype(R_)::value;
+            if constexpr (W::row_step(r, KS1) == s) {
+              epi1_row(P, rzo, vzo, zs, ib - 1, r, qp[r] * vinv);
+              if constexpr (r == 3) zs.next();
+              if constexpr (ib - 1 + kLA < NB)
+                zo[(ib - 1 + kLA) % (kLA + 1)][r] =
+                    bload(rzp, vzp + zr.at(16 * (ib - 1 + kLA) + r));
+            }
+          });
+          // blocks 2s', 2s'+1 complete (the odd block's last row ran at this step or before)
+          if constexpr (((ib - 1) & 1) && s == KS1 - 1) {
+            constexpr int sp = (ib - 1) / 2;
+            Zpk[sp] = split8(zn[0], zn[1], zsc);
+            pin_agpr_b(Zpk[sp]);
+          }
+        }
+        acc = mfma3(t % R, Vpk[s], acc);
+        step_tail(std::integral_constant<int, t>{});
+      });
+      qp = acc;
+    });
+    // tail: block NB-1
+#pragma unroll
+    for (int r = 0; r < 4; ++r) epi1_row(P, rzo, vzo, zs, NB - 1, r, qp[r] * vinv);
+    Zpk[KS2 - 1] = split8(zn[0], zn[1], zsc);
+    pin_agpr_b(Zpk[KS2 - 1]);
+  };
+
+  // ---------------------------------------------------------------- G2(k): A Z_k -> E, L, T, Var
+  auto g2_pass = [&](auto PRO_, int k, const LayerP& P, const OutR& O, float zinv) {
+    constexpr bool PRO = decltype(PRO_)::value;
+    const int gi = 2 * k + 2;
+    mw.reset();
+    f32x4 qp = zero4;
+    static_for<MB>([&](auto IB_) {
+      constexpr int ib = decltype(IB_)::value;
+      f32x4 acc = zero4;
+      f32x4 xv;
+      if constexpr (ib > 0) xv = xs[(w * MB + ib - 1) * 64 + lane];
+      static_for<KS2>([&](auto S_) {
+        constexpr int s = decltype(S_)::value;
+        constexpr int t = ib * KS2 + s;
+        step_head(std::integral_constant<int, t>{}, gi,
+                  std::integral_constant<int, W::template win<t, false>()>{});
+        if constexpr (ib > 0) {
+          static_for<4>([&](auto R_) {
+            constexpr int r = decltype(R_)::value;
+            if constexpr (W::row_step(r, KS2) == s) {
+              epi2_row(P, O, PRO, ib - 1, r, qp[r] * zinv, xv[r], mw.at(r));
+              if constexpr (r == 3) mw.next();
+            }
+          });
+        }
+        acc = mfma3(t % R, Zpk[s], acc);
+        step_tail(std::integral_constant<int, t>{});
+      });
+      qp = acc;
+    });
+    const f32x4 xv = xs[(w * MB + MB - 1) * 64 + lane];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      epi2_row(P, O, PRO, MB - 1, r, qp[r] * zinv, xv[r], mw.at(r));
+    }
+  };
+
+  // ---------------------------------------------------------------- prologue + K layers
+  const rsrc_t none = mkrsrc(nullptr, 0u);
+  {
+    const LayerP P0 = layer_params(-1);
+    const OutR O0{none, none,
+                  mkrsrc(a.keep_all ? a.To : nullptr, (a.keep_all && a.To) ? mbytes : 0u)};
+    g2_pass(std::true_type{}, -1, P0, O0, exp2i(-(zexp + sw_a)));
+  }
+  flush_loss(-1);
+  for (int k = 0; k < K; ++k) {
+    const bool last = k == K - 1;
+    const LayerP P = layer_params(k);
+    const int swk = sw_w(k);
+    // Var_k (from G2(k-1) / the prologue): exact column scale for this layer's weight
+    const int vexp = scale_exp(col_max(vmx), swk, 0);
+    vmx = 0.f;
+    // Z_{k-1}: where it was written, and its lane offset / row stride
+    const bool zp_in = k == 0;
+    const float* zpp = zp_in ? a.Z0
+                             : (a.keep_all ? a.Zo + (int64_t)(k - 1) * n * a.ldo
+                                           : a.Zw + (int64_t)((k - 1) & 1) * n * a.ldzw);
+    const int64_t ldzp = zp_in ? a.ldz0 : (a.keep_all ? a.ldo : a.ldzw);
+    const rsrc_t rzp = mkrsrc(zpp, (uint32_t)(n * ldzp * 4));
+    const uint32_t vzp = zp_in ? oz0 : (a.keep_all ? oo : ozw);
+    zr = SWalk{0u, (uint32_t)(ldzp * 4)};
+    // Z_k goes to the output (keep_all or last layer) or to the lean-mode workspace
+    const bool zout = a.keep_all || last;
+    const int64_t ldzo = zout ? a.ldo : a.ldzw;
+    float* zop = zout ? a.Zo + (int64_t)(a.keep_all ? k : 0) * n * a.ldo
+                      : a.Zw + (int64_t)(k & 1) * n * a.ldzw;
+    const rsrc_t rzo = mkrsrc(zop, (uint32_t)(n * ldzo * 4));
+    const uint32_t vzo = zout ? oo : ozw;
+    zw = SWalk{0u, (uint32_t)(ldzo * 4)};
+    // re-read the first kLA blocks of Z_{k-1}
+#pragma unroll
+    for (int b = 0; b < kLA; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) zo[b][r] = bload(rzp, vzp + zr.at(16 * b + r));
+    // provisional scale of Z_k's split: the column max of Z_{k-1} with kHead bits of headroom
+    const int zexp_p = scale_exp(zmx_prev, sw_a, kHead);
+    zmx = 0.f;
+    g1_pass(k, P, rzo, vzo, rzp, vzp, exp2i(vexp), exp2i(-(vexp + swk)), exp2i(zexp_p));
+    // exact column max of Z_k; re-split if a column outgrew the provisional scale
+    const float zm = col_max(zmx);
+    zmx_prev = zm;
+    zexp = zexp_p;
+    if (__any(zm * exp2i(zexp_p) >= 65504.0f)) {  // wave-uniform; rare (first layer)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // this wave's Z_k stores
+      zexp = scale_exp(zm, sw_a, 0);
+      const float sc = exp2i(zexp);
+      SWalk rw{0u, (uint32_t)(ldzo * 4)};
+#pragma unroll
+      for (int s = 0; s < KS2; ++s) {
+        float va[4], vb[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          va[r] = bload(rzo, vzo + rw.at(32 * s + r));
+          vb[r] = bload(rzo, vzo + rw.at(32 * s + 16 + r));
+        }
+        Zpk[s] = split8(va, vb, sc);
+        pin_agpr_b(Zpk[s]);
+        if (s % 2 == 1) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    const bool st = a.keep_all || last;
+    const int ko = a.keep_all ? k : 0;
+    const OutR O{mkrsrc(a.Eo + (int64_t)ko * m * a.ldo, st ? mbytes : 0u),
+                 mkrsrc(a.Lo + (int64_t)ko * m * a.ldo, st ? mbytes : 0u),
+                 mkrsrc(a.To ? a.To + (int64_t)(a.keep_all ? k + 1 : 0) * m * a.ldo : nullptr,
+                        (a.To && st) ? mbytes : 0u)};
+    g2_pass(std::false_type{}, k, P, O, exp2i(-(zexp + sw_a)));
+    flush_loss(k);
+  }
+  // drain: the ring's last LDS-DMAs must land before the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int MP, int NP, int EM, int PK>
+hipError_t launch_x3(const FusedArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((fused_x3_kernel<MP, NP, EM, PK>), dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int MP, int NP>
+hipError_t dispatch_x3_variant(int variant, const FusedArgs& a, int grid, hipStream_t s) {
+  switch (variant) {
+    case DLADMM_V4_SCALAR: return launch_x3<MP, NP, EM_VVAR, PK_SCALAR>(a, grid, s);
+    case DLADMM_V5_TIED: return launch_x3<MP, NP, EM_VVAR, PK_S1>(a, grid, s);
+    case DLADMM_V6_LASSO: return launch_x3<MP, NP, EM_LASSO, PK_SCALAR>(a, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+bool x3_supports(int variant) {
+  return variant == DLADMM_V4_SCALAR || variant == DLADMM_V5_TIED ||
+         variant == DLADMM_V6_LASSO;
+}
+
+hipError_t launch_fused_x3_shape(int shape, int variant, const FusedArgs& a, int grid,
+                                 hipStream_t s) {
+  switch (shape) {
+    case 0: return dispatch_x3_variant<kShapeMP[0], kShapeNP[0]>(variant, a, grid, s);
+    case 1: return dispatch_x3_variant<kShapeMP[1], kShapeNP[1]>(variant, a, grid, s);
+    case 2: return dispatch_x3_variant<kShapeMP[2], kShapeNP[2]>(variant, a, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace dladmm

@@ -27,6 +27,10 @@ struct FusedArgs {
   const float* b2e[DLADMM_MAX_LAYERS_V1];
   float* Zo; float* Eo; float* Lo; float* To; int64_t ldo;
   float* lossp;      // [K][2][ldl] per-column objective terms
+  // split-f16 path (dladmm_fused_x3.hip): per-tensor weight scale exponents (wexp[0] = A,
+  // wexp[1 + k] = -W_k) and the lean-mode Z_k workspace [2][n][ldzw]
+  const int* wexp;
+  float* Zw; int64_t ldzw;
 };
 
 
@@ -37,6 +41,10 @@ constexpr int kShapeNP[kNumShapes] = {32, 256, 512};
 
 hipError_t launch_fused_shape(int shape, int variant, const FusedArgs& a, int grid,
                               hipStream_t s);
+// split-f16 fused kernel (DLADMM_PREC_F32_SPLIT); Ap / Wp hold [step][hi|lo] f16 fragments
+bool x3_supports(int variant);
+hipError_t launch_fused_x3_shape(int shape, int variant, const FusedArgs& a, int grid,
+                                 hipStream_t s);
 
 }  // namespace dladmm
 

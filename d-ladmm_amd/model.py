@@ -119,8 +119,12 @@ class _DLADMMBase(nn.Module):
     def _needs_grad(self) -> bool:
         return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
 
-    # GEMM operand precision of forward / run: "f32" (the reference) or "bf16" (BASELINE config
-    # 5: bf16 MFMA operands, fp32 accumulation and fp32 elementwise state; inference only)
+    # GEMM precision of forward / run: "f32" (fp32 MFMA: every GEMM an exact fp32 fma chain),
+    # "f32_split" (the same fp32 GEMMs on the f16 matrix cores: operands split exactly into
+    # scaled hi + lo f16 halves, hi*hi + hi*lo + lo*hi accumulated in fp32 -- the error of an fp32
+    # GEMM, ~3x the throughput; V4-V6 fused shapes, others run f32) or "bf16" (BASELINE config 5:
+    # bf16 MFMA operands, fp32 accumulation and fp32 elementwise state).  The backward always
+    # differentiates the f32 forward, so training runs "f32".
     precision = "f32"
 
     def run(self, x: torch.Tensor, keep_all: bool = True, loss_kind: int = 0,
@@ -143,7 +147,8 @@ class _DLADMMBase(nn.Module):
                 raise RuntimeError("dladmm: gradients w.r.t. the input X are not supported (the "
                                    "reference trains the parameters only)")
             if self.precision != "f32":
-                raise RuntimeError("dladmm: the bf16 operand mode is inference-only")
+                raise RuntimeError(f"dladmm: precision {self.precision!r} is inference-only "
+                                   "(the backward differentiates the f32 forward)")
             outs = _DLADMMFunction.apply(self, x, nl, *self.parameters())
             return (list(outs[:nl]), list(outs[nl:2 * nl]), list(outs[2 * nl:3 * nl]),
                     list(outs[3 * nl:]))

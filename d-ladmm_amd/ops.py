@@ -110,6 +110,13 @@ def _fill_fwd_desc(d, variant, X, A, W, Z0, E0, L0, scalar_params, row_params, b
     return keep
 
 
+# GEMM precision modes (include/dladmm.h, dladmm_precision): "f32" fp32 MFMA (exact fp32 fma
+# chain); "f32_split" the same fp32 GEMMs on the f16 matrix cores (operands split exactly into
+# power-of-two-scaled hi + lo halves, three products, fp32 accumulation: fp32-GEMM error);
+# "bf16" bf16 operands (BASELINE config 5).
+_PRECISIONS = {"f32": _lib.PREC_F32, "f32_split": _lib.PREC_F32_SPLIT, "bf16": _lib.PREC_BF16}
+
+
 def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[torch.Tensor],
                    Z0: torch.Tensor, E0: torch.Tensor, L0: torch.Tensor, *,
                    scalar_params: Optional[torch.Tensor] = None,
@@ -147,9 +154,10 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
     d = _lib.FwdDesc()
     keep = _fill_fwd_desc(d, variant, X, A, W, Z0, E0, L0, scalar_params, row_params, beta1_elem,
                           beta2_elem, keep_all, loss_kind, out)
-    if precision not in ("f32", "bf16"):
-        raise ValueError(f"dladmm: precision must be 'f32' or 'bf16', got {precision!r}")
-    d.precision = _lib.PREC_BF16 if precision == "bf16" else _lib.PREC_F32
+    if precision not in _PRECISIONS:
+        raise ValueError(f"dladmm: precision must be one of {sorted(_PRECISIONS)}, "
+                         f"got {precision!r}")
+    d.precision = _PRECISIONS[precision]
     if want_col_loss:
         if not loss_kind:
             raise ValueError("dladmm: per-column objectives need loss_kind")

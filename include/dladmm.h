@@ -140,15 +140,23 @@ typedef struct dladmm_fwd_desc {
      reference's evaluation objectives reduce (test_syn_l1l1_scalar.py:460-478). NULL = off. */
   float* col_loss;
 
-  /* GEMM operand precision: DLADMM_PREC_F32 (default; the reference's fp32) or DLADMM_PREC_BF16
-     (BASELINE config 5: A, W_k and the state operands Var / Z_k rounded to bf16 for the MFMAs,
-     fp32 accumulation, every elementwise update -- shrinks, E, dual L, T -- in fp32).  bf16 runs
-     on the per-layer kernels (path 3). */
+  /* GEMM operand precision:
+       DLADMM_PREC_F32 (default; the reference's fp32): fp32 MFMA (v_mfma_f32_16x16x4_f32), an
+         exact fp32 fma chain per output;
+       DLADMM_PREC_F32_SPLIT: the same fp32 GEMMs on the f16 matrix cores -- both operands scaled
+         by powers of two (weights per tensor, state per batch column) and split exactly into
+         hi + lo f16 halves (22 significant bits), the product formed as hi*hi + hi*lo + lo*hi with
+         fp32 accumulation (every f16 x f16 product is exact in fp32).  Error of an fp32 GEMM
+         (same tolerance tests as PREC_F32); every elementwise update stays fp32.  Fused path
+         (m <= 256, n <= 512) for V4/V5/V6; other shapes / variants run PREC_F32;
+       DLADMM_PREC_BF16 (BASELINE config 5: A, W_k and the state operands Var / Z_k rounded to bf16
+         for the MFMAs, fp32 accumulation, every elementwise update -- shrinks, E, dual L, T -- in
+         fp32).  bf16 runs on the per-layer kernels (path 3). */
   int32_t precision;
   int32_t pad1;
 } dladmm_fwd_desc;
 
-enum dladmm_precision { DLADMM_PREC_F32 = 0, DLADMM_PREC_BF16 = 1 };
+enum dladmm_precision { DLADMM_PREC_F32 = 0, DLADMM_PREC_BF16 = 1, DLADMM_PREC_F32_SPLIT = 2 };
 
 /* ABI version the library was built with. */
 int dladmm_abi_version(void);

@@ -1,0 +1,201 @@
+"""Parity of the split-f16 fused forward (precision "f32_split", DLADMM_PREC_F32_SPLIT,
+csrc/dladmm_fused_x3.hip) with the reference -- the SAME bars as the fp32 path
+(tests/test_gpu_parity.py): per layer, norm-relative <= max(1e-5, 3 x the reference's own
+fp32-vs-fp64 gap), against the reference's golden outputs and the oracle.
+
+The mode forms every fp32 GEMM as hi*hi + hi*lo + lo*hi of exactly split, power-of-two-scaled f16
+halves with fp32 accumulation; these tests are what pins that its error is an fp32 GEMM's:
+every variant it runs (V4, V5, V6 and the newS schedules on them), padded shapes, ragged batches,
+the 65,536-column BASELINE shape, columns of very different magnitude (per-column scaling, the
+provisional-scale re-split), lean mode and determinism.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+import problems as P
+from test_gpu_parity import REL, _compare, _oracle_case, make_net, nrel
+
+pytestmark = pytest.mark.gpu
+
+SPLIT_VARIANTS = ("v4", "v5", "v6", "v7", "v7t", "v7p")
+
+
+def split_net(dl, variant, inp, sd, K, **extra):
+    net = make_net(dl, variant, inp, sd, K, **extra)
+    net.precision = "f32_split"
+    return net
+
+
+def _path(dl, net, X):
+    """The C ABI's plan for this call (4 = split-f16 fused kernel)."""
+    import ctypes
+    from importlib import import_module
+    ops = import_module("d-ladmm_amd.ops")
+    d = dl._lib.FwdDesc()
+    m, B = X.shape
+    K = net.layers
+    out = ops.ForwardResult(torch.empty(K, net.d, B, device="cuda"),
+                            torch.empty(K, m, B, device="cuda"),
+                            torch.empty(K, m, B, device="cuda"),
+                            torch.empty(K + 1, m, B, device="cuda"), None)
+    tabs = dict(scalar_params=None, row_params=None, beta1_elem=(), beta2_elem=())
+    tabs.update(net._tables(net.A.device))
+    keep = ops._fill_fwd_desc(d, net.VARIANT, X, net.A, [w.detach() for w in net._weights()],
+                              net.Z0, net.E0, net.L0, keep_all=True, loss_kind=0, out=out,
+                              **tabs)
+    d.precision = dl._lib.PREC_F32_SPLIT
+    del keep
+    return dl._lib.lib().dladmm_fwd_path(ctypes.byref(d))
+
+
+@pytest.mark.parametrize("name", sorted(n for n in P.FIXTURES
+                                        if P.FIXTURES[n]["variant"] in SPLIT_VARIANTS))
+def test_split_matches_reference_golden(name, dl):
+    g, meta = load_golden(name)
+    d = meta["defn"]
+    inp, sd = P.build_problem(d)
+    net = split_net(dl, d["variant"], inp, sd, d["K"], **P.ctor_extra(d))
+    X = torch.from_numpy(inp["X"]).cuda()
+    if d["m"] <= 256 and d["n"] <= 512:
+        assert _path(dl, net, X) == 4
+    with torch.no_grad():
+        out = net(X)
+    names = ["Z", "E", "L", "T"][: len(out)]
+    for nm, seq in zip(names, out):
+        for k, t in enumerate(seq):
+            tol = max(REL, 3.0 * float(g["gap_" + nm][k]))
+            e = nrel(t.cpu().numpy(), g[nm][k])
+            assert e <= tol, f"{name} {nm}[{k}] nrel {e:.3e} > {tol:.3e}"
+    otol = max(2e-5, 3.0 * max(float(np.max(g["gap_" + nm])) for nm in names))
+    _, obj = net.layer_objectives(X, meta["alpha"], "l1l1")
+    np.testing.assert_allclose(obj.cpu().numpy(), g["loss_l1l1"], rtol=otol)
+    _, obj = net.layer_objectives(X, meta["alpha"], "lasso")
+    np.testing.assert_allclose(obj.cpu().numpy(), g["loss_lasso"], rtol=otol)
+
+
+@pytest.mark.parametrize("variant", ["v4", "v5", "v6"])
+@pytest.mark.parametrize("B", [1, 64, 300])
+def test_split_vs_oracle_baseline_shape(variant, B, dl, oracle):
+    m, n, K = 256, 512, 15
+    inp, sd, ref = _oracle_case(oracle, variant, m, n, B, K, seed=2000 + B)
+    net = split_net(dl, variant, inp, sd, K)
+    with torch.no_grad():
+        out = net(torch.from_numpy(inp["X"]).cuda())
+    _compare(out, ref, tag=f"split {variant} B={B}")
+
+
+@pytest.mark.parametrize("shape", [(16, 32), (30, 70), (64, 256), (250, 500), (200, 512)])
+def test_split_padded_shapes(shape, dl, oracle):
+    m, n = shape
+    for variant in ("v4", "v6"):
+        inp, sd, ref = _oracle_case(oracle, variant, m, n, 77, 5, seed=3000 + m)
+        net = split_net(dl, variant, inp, sd, 5)
+        with torch.no_grad():
+            out = net(torch.from_numpy(inp["X"]).cuda())
+        _compare(out, ref, tag=f"split {variant} {shape}")
+
+
+def test_split_column_magnitudes(dl, oracle):
+    """Columns scaled by 1e-6 .. 1e6 (and an all-zero column): the per-column power-of-two
+    scales keep every column at the top of the f16 range; Z growing by far more than the
+    provisional scale's headroom between layers takes the exact re-split."""
+    m, n, B, K = 256, 512, 64, 6
+    inp = P.make_inputs(m, n, B, 4100)
+    scales = (10.0 ** np.linspace(-6, 6, B)).astype(np.float32)
+    scales[7] = 0.0
+    inp = dict(inp, X=inp["X"] * scales, Z0=inp["Z0"] * scales)
+    sd = P.make_state_dict("v6", m, n, B, K, inp["A"], 4100, perturb=0.1)
+    for k in range(K):   # thresholds scaled like the data would need: keep them tiny
+        sd[f"active_para.{k}"][:] = 1e-7
+    args = ("v6", inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd, K)
+    r64 = oracle.forward(*args, dtype=np.float64)
+    net = split_net(dl, "v6", inp, sd, K)
+    with torch.no_grad():
+        Z, E, L, T = net(torch.from_numpy(inp["X"]).cuda())
+    for nm, seq in (("Z", Z), ("E", E), ("L", L)):
+        for k in range(K):
+            got = seq[k].cpu().numpy().astype(np.float64)
+            ref = np.asarray(r64[nm][k], np.float64)
+            # per column: every column matches at its own scale
+            for c in range(B):
+                nr = np.linalg.norm(ref[:, c])
+                if nr == 0:
+                    assert np.all(got[:, c] == 0), (nm, k, c)
+                    continue
+                e = np.linalg.norm(got[:, c] - ref[:, c]) / nr
+                assert e <= 1e-5, (nm, k, c, e)
+
+
+def test_split_lean_mode_and_determinism(dl):
+    """Lean mode (Z_k through the ping-pong workspace) == the full run's last layer, bitwise;
+    two runs bitwise identical."""
+    m, n, B, K = 256, 512, 1000, 15
+    inp = P.make_inputs(m, n, B, 5001)
+    sd = P.make_state_dict("v4", m, n, B, K, inp["A"], 5001, perturb=0.1)
+    net = split_net(dl, "v4", inp, sd, K)
+    X = torch.from_numpy(inp["X"]).cuda()
+    with torch.no_grad():
+        full = net.run(X, keep_all=True, loss_kind=1)
+        full2 = net.run(X, keep_all=True, loss_kind=1)
+        lean = net.run(X, keep_all=False, loss_kind=1)
+    for a, b in ((full.Z, full2.Z), (full.E, full2.E), (full.L, full2.L), (full.T, full2.T),
+                 (full.loss_sums, full2.loss_sums)):
+        assert torch.equal(a, b)
+    assert torch.equal(lean.Z[0], full.Z[-1])
+    assert torch.equal(lean.E[0], full.E[-1])
+    assert torch.equal(lean.L[0], full.L[-1])
+    assert torch.equal(lean.T[0], full.T[-1])
+    assert torch.equal(lean.loss_sums, full.loss_sums)
+
+
+def test_split_baseline_size(dl, oracle):
+    """B = 65,536: a random column subset against the oracle, the fused objective against a
+    separate fp64 reduction of the returned outputs, and against the fp32 path."""
+    m, n, K, B = 256, 512, 15, 65536
+    inp = P.make_inputs(m, n, 64, 8001)
+    A = inp["A"]
+    rng = np.random.default_rng(8002)
+    zs = (rng.random((n, B)) < 0.1) * rng.standard_normal((n, B))
+    es = (rng.random((m, B)) < 0.1) * rng.standard_normal((m, B))
+    X = (A.astype(np.float64) @ zs + es).astype(np.float32)
+    Z0 = (rng.random((n, B)) / n).astype(np.float32)
+    E0 = np.zeros((m, B), np.float32)
+    L0 = np.zeros((m, B), np.float32)
+    sd = P.make_state_dict("v4", m, n, B, K, A, 8001, perturb=0.1)
+    net = split_net(dl, "v4", dict(A=A, X=X, Z0=Z0, E0=E0, L0=L0), sd, K)
+    Xd = torch.from_numpy(X).cuda()
+    with torch.no_grad():
+        r, obj = net.layer_objectives(Xd, 0.001, "l1l1")
+        net.precision = "f32"
+        r32, obj32 = net.layer_objectives(Xd, 0.001, "l1l1")
+    cols = np.sort(np.random.default_rng(8003).permutation(B)[:96])
+    ref = oracle.forward("v4", X[:, cols], A, Z0[:, cols], E0[:, cols], L0[:, cols], sd, K)
+    for nm, got, g32 in (("Z", r.Z, r32.Z), ("E", r.E, r32.E), ("L", r.L, r32.L)):
+        for k in range(K):
+            assert nrel(got[k][:, cols].cpu().numpy(), ref[nm][k]) <= REL, (nm, k)
+            assert nrel(got[k].cpu().numpy(), g32[k].cpu().numpy()) <= REL, (nm, k)
+    Ad = torch.from_numpy(A).cuda().double()
+    sep = []
+    for k in range(K):
+        Zk = r.Z[k].double()
+        sep.append(float((0.001 * Zk.abs().sum() + (Xd.double() - Ad @ Zk).abs().sum()) / B))
+    np.testing.assert_allclose(obj.cpu().numpy(), np.array(sep), rtol=1e-5)
+    np.testing.assert_allclose(obj.cpu().numpy(), obj32.cpu().numpy(), rtol=1e-5)
+
+
+def test_split_falls_back_where_unsupported(dl, oracle):
+    """V1-V3 and shapes beyond the register budget run the fp32 kernels under f32_split."""
+    for variant, (m, n) in (("v1", (64, 256)), ("v3", (64, 256)), ("v4", (300, 600))):
+        inp, sd, ref = _oracle_case(oracle, variant, m, n, 50, 3, seed=3100,
+                                    wscale=0.4 if variant == "v1" else None)
+        net = split_net(dl, variant, inp, sd, 3)
+        X = torch.from_numpy(inp["X"]).cuda()
+        assert _path(dl, net, X) in (1, 2)
+        with torch.no_grad():
+            out = net(X)
+        _compare(out, ref, tag=f"split fallback {variant}")
+    net.requires_grad_(True)
+    with pytest.raises(RuntimeError, match="inference-only"):
+        net(X)
