@@ -54,6 +54,8 @@ def parse():
                          "products, fp32 accumulation); bf16 = BASELINE config 5 mode (bf16 MFMA "
                          "operands, fp32 state): --precision bf16 --m 1024 --n 4096 --batch 16384")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-split", action="store_true",
+                    help="skip the secondary f32_split measurement of the f32 headline run")
     ap.add_argument("--cpu-batch", type=int, default=8192, help="columns of the CPU sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return ap.parse_args()
@@ -139,36 +141,56 @@ def main():
         obj = ddist.global_objectives(r.loss_sums, a.alpha, B * world)
         return r, obj
 
-    with torch.no_grad():
-        for _ in range(a.warmup):
-            r, obj = step()
-            del r
-        torch.cuda.synchronize()
+    def timed(precision):
+        """W untimed warmup steps, then exactly K timed steps between barrier + synchronize;
+        (max-over-ranks wall seconds, mean kernel seconds, objective)."""
+        net.precision = precision
+        with torch.no_grad():
+            for _ in range(a.warmup):
+                r, obj = step()
+                del r
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(a.steps):
+                r, obj = step((ev[2 * i], ev[2 * i + 1]))
+                del r
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t1 = time.perf_counter()
+        elapsed = t1 - t0
+        kern = float(np.mean([ev[2 * i].elapsed_time(ev[2 * i + 1])
+                              for i in range(a.steps)])) * 1e-3
         if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(a.steps):
-            r, obj = step((ev[2 * i], ev[2 * i + 1]))
-            del r
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t1 = time.perf_counter()
-    elapsed = t1 - t0
-    kern_ms = [ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(a.steps)]
-    kern_avg = float(np.mean(kern_ms)) * 1e-3
-    if world > 1:
-        tt = torch.tensor([elapsed, kern_avg], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, kern_avg = float(tt[0]), float(tt[1])
+            tt = torch.tensor([elapsed, kern], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed, kern = float(tt[0]), float(tt[1])
+        return elapsed, kern, obj
+
+    elapsed, kern_avg, obj = timed(a.precision)
+    # the same workload with the fp32 GEMMs on the f16 matrix cores (split-f16, same fp32
+    # tolerance tests; tests/test_gpu_split.py), timed the same way beside the headline
+    split = None
+    if a.precision == "f32" and m <= 256 and n <= 512 and B % 4 == 0 and \
+            os.environ.get("DLADMM_PATH", "")[:1] != "l" and not a.no_split:
+        s_el, s_kern, s_obj = timed("f32_split")
+        split = (s_el, s_kern, float(s_obj.cpu().numpy()[-1]))
     obj = obj.cpu().numpy()
 
     if rank == 0:
-        path = "fused" if (m <= 256 and n <= 512 and os.environ.get("DLADMM_PATH", "")[:1] != "l"
-                           and a.precision == "f32") else "per-layer"
-        peak = PEAK_BF16_MFMA if a.precision == "bf16" else PEAK_F32_MFMA
-        kname = ("dladmm::fused_kernel (one launch)" if path == "fused" else
+        fused = (m <= 256 and n <= 512 and os.environ.get("DLADMM_PATH", "")[:1] != "l"
+                 and a.precision in ("f32", "f32_split"))
+        path = ("fused-split-f16" if a.precision == "f32_split" else "fused") if fused \
+            else "per-layer"
+        # split-f16: 3 f16 MFMA products per fp32 product -> the fp32-GEMM ceiling of the
+        # scheme is the dense f16 MFMA peak / 3
+        peak = {"bf16": PEAK_BF16_MFMA, "f32": PEAK_F32_MFMA,
+                "f32_split": PEAK_BF16_MFMA / 3}[a.precision]
+        kname = ({"fused": "dladmm::fused_kernel (one launch)",
+                  "fused-split-f16": "dladmm::fused_x3_kernel (one launch)"}.get(path) or
                  f"dladmm::layer_kernel x {2 * K + 1} launches (timed together)")
         total = B * world * a.steps
         value = total / elapsed
@@ -199,7 +221,10 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32" if a.precision == "f32" else "bf16 operands / f32 state",
+            "dtype": {"f32": "f32",
+                      "f32_split": "f32 (GEMMs: exact hi/lo f16 split, 3 f16 MFMA products, "
+                                   "f32 accumulate)",
+                      "bf16": "bf16 operands / f32 state"}[a.precision],
             "data": "synthetic (gen_syn_data.py distribution generated on device; reference-init "
                     "V4 parameters, random W = 0.4(A^T + 1e-3 N))",
             "config": {
@@ -227,6 +252,25 @@ def main():
             },
             "objective_last_layer": float(obj[-1]),
         }
+        if split is not None:
+            s_el, s_kern, s_objl = split
+            s_peak = PEAK_BF16_MFMA / 3
+            res["split_f16"] = {
+                "precision": "f32_split",
+                "note": "same workload, fp32 GEMMs as hi*hi + hi*lo + lo*hi of exactly split "
+                        "power-of-two-scaled f16 halves on v_mfma_f32_16x16x32_f16, fp32 "
+                        "accumulate; fp32 elementwise state; parity at the fp32 tolerances",
+                "value": total / s_el,
+                "unit": "samples/s",
+                "ms_per_step": s_el / a.steps * 1e3,
+                "kernel": "dladmm::fused_x3_kernel (one launch)",
+                "kernel_ms": s_kern * 1e3,
+                "roofline_mfma": {"achieved": flop / s_kern / 1e12, "peak": s_peak / 1e12,
+                                  "unit": "TFLOP/s", "frac": flop / s_kern / s_peak,
+                                  "peak_note": "dense f16 MFMA peak / 3 products"},
+                "hbm_frac_algorithmic": bytes_launch / s_kern / PEAK_HBM,
+                "objective_last_layer": s_objl,
+            }
         if world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(m, n, K, a.cpu_batch, a.variant)
         print(json.dumps(res), flush=True)

@@ -260,6 +260,14 @@ inline bool fits_32bit(const dladmm_fwd_desc* d) {
            (d->variant == DLADMM_V1_LENA && mx * d->ld_beta * 4 >= lim));
 }
 
+// The split-f16 kernel moves every batch row in 16-B pieces (4 columns per lane): the batch must
+// be a multiple of 4 and the state / output rows 16-B aligned.  Otherwise: the fp32 kernel.
+inline bool x3_layout_ok(const dladmm_fwd_desc* d) {
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  return d->batch % 4 == 0 && d->ld_out % 4 == 0 && d->ld_z0 % 4 == 0 && al(d->Z0) &&
+         al(d->Z) && al(d->E) && al(d->L) && (!d->T || al(d->T));
+}
+
 // every layer uses the same weight tensor (V5 tied, the KM iteration): packed once
 inline bool shared_weight(const dladmm_fwd_desc* d) {
   for (int k = 1; k < d->layers; ++k)
@@ -279,11 +287,11 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
   // split-f16 fused kernel: register-resident shapes, scalar-parameter variants (V4-V6); other
   // cases run the fp32 kernels (same results up to fp32 GEMM rounding)
   if (s >= 0 && fits_32bit(d) && !force_layered && d->precision == DLADMM_PREC_F32_SPLIT &&
-      x3_supports(d->variant)) {
+      x3_supports(d->variant) && x3_layout_ok(d)) {
     p->path = 4;
-    p->shape = s;
-    p->MP = kShapeMP[s];
-    p->NP = kShapeNP[s];
+    p->shape = s < 1 ? 1 : s;  // the x3 kernel's smallest instantiation is shape 1
+    p->MP = kShapeMP[p->shape];
+    p->NP = kShapeNP[p->shape];
     p->tiles = ceil_div(d->batch, kTileCols);
     p->ldl = p->tiles * kTileCols;
     p->nslots = p->ldl;

@@ -28,7 +28,9 @@
 // of G1, KS1 k-steps) and Zpk (Z_k, B operand of G2, KS2 k-steps).  fp32 Z is NOT kept across a
 // layer: G1's epilogue writes Z_k (output, or workspace in lean mode) and splits it into Zpk
 // right away, with a provisional column scale (the previous layer's column max + kHead bits of
-// headroom); G1(k+1)'s epilogue re-reads Z_k from memory kLA blocks ahead.  If a column of Z_k
+// headroom); G1(k+1)'s epilogue gets Z_k back through the LDS ring (buffer LDS-DMA of 1 KiB
+// blocks issued with the weight chunks, so the ring barrier's counted vmcnt covers them: a
+// register load would make its wait drain every older output store).  If a column of Z_k
 // outgrew the provisional scale (checked exactly at the end of G1), the wave re-reads Z_k and
 // re-splits it with the exact scale (rare: first layer).  fp32 Var is kept (it is not an
 // output) and split with its exact column scale at the start of G1.
@@ -40,14 +42,21 @@
 #include "dladmm_common.h"
 #include "dladmm_internal.h"
 
+#ifndef X3_ABL
+#define X3_ABL 0  // timing experiments only (tools/x3_ablate.py), every bit gives WRONG results:
+                  // 1 no weight DMA, 2 no epilogue work, 4 no output stores, 8 no operand splits,
+                  // 16 no MFMAs, 32 no Z re-read DMA, 64 no fragment LDS reads, 128 ring barriers
+                  // do not wait for the DMA (vmcnt(63))
+#endif
+
 namespace dladmm {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 namespace x3 {
 
 constexpr int kSlots = 4;  // LDS ring slots
-constexpr int kLA = 2;     // Z_{k-1} re-read look-ahead, in 16-row blocks
 constexpr int kHead = 12;  // provisional-scale headroom (bits) of the in-epilogue Z split
 
 __device__ __forceinline__ f32x4 mfma(const f16x8& a, const f16x8& b, f32x4 c) {
@@ -71,6 +80,12 @@ __device__ __forceinline__ void split4(const float (&v)[4], float sc, f16x8& hi,
 }
 __device__ __forceinline__ BOp split8(const float (&a)[4], const float (&b)[4], float sc) {
   BOp r;
+  if constexpr (X3_ABL & 8) {
+    for (int j = 0; j < 4; ++j) {
+      r.hi[j] = (_Float16)a[j]; r.hi[4 + j] = (_Float16)b[j]; r.lo = r.hi;
+    }
+    return r;
+  }
   split4(a, sc, r.hi, r.lo, 0);
   split4(b, sc, r.hi, r.lo, 4);
   return r;
@@ -104,31 +119,115 @@ __device__ __forceinline__ float exp2i(int e) { return __builtin_amdgcn_ldexpf(1
 // other pass type (the window reaching back across a pass boundary) counts with that pass's
 // schedule; the unrolled tails between passes only add younger operations (not counted: a
 // lower bound only waits longer).
-template <int MB, int NB, int KS1, int KS2, int SPC, int ELOADS>
+// LDS-DMA through a buffer resource, lane l: 16 B from voff + soff to LDS at ldst + 16 l.
+// Out-of-range lanes (kOOB: padded columns) read 0, so padded columns stay exactly zero.  M0 is
+// compiler-reserved: saved and restored in the statement.
+__device__ __forceinline__ void blds16(i32x4 r, uint32_t voff, uint32_t soff, const void* ldst) {
+  unsigned keep;
+  const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ldst);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %3 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(r), "s"(soff), "s"(dst)
+      : "memory");
+}
+// Four consecutive 1 KiB fragments (sbase + 0..3 KiB -> ldst + 0..3 KiB) by LDS-DMA with one
+// M0 setup: the instruction offset advances the global source and the LDS destination alike
+// (tools/probe/ldsdma_offset.hip).
+__device__ __forceinline__ void glds16x4(const float* sbase, uint32_t voff, const void* ldst) {
+  unsigned keep;
+  const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ldst);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
+      "global_load_lds_dwordx4 %1, %2 offset:1024\n\t"
+      "global_load_lds_dwordx4 %1, %2 offset:2048\n\t"
+      "global_load_lds_dwordx4 %1, %2 offset:3072\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(dst)
+      : "memory");
+}
+__device__ __forceinline__ void bstore4(rsrc_t r, uint32_t voff, uint32_t soff, f32x4 v) {
+  if constexpr (!(X3_ABL & 4))
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), r, (int)voff, (int)soff,
+                                           DLADMM_STORE_AUX);
+}
+// m = max(m, |v|) in one v_max_f32 (fmaxf would canonicalise both inputs first)
+__device__ __forceinline__ float amax(float m, float v) {
+  float r;
+  asm("v_max_f32_e64 %0, %1, |%2|" : "=v"(r) : "v"(m), "v"(v));
+  return r;
+}
+__device__ __forceinline__ i32x4 mk_rsrc4(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));  // stride 0
+  r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
+  r[3] = 0x00020000;
+  return r;
+}
+
+// Chunk geometry.  The stream is the GEMM sequence A (prologue), -W_0, A, -W_1, ..., each ST
+// steps = NCH chunks of SPC steps.  A G1 chunk also carries, per wave, the NZB blocks of Z_{k-1}
+// (1 KiB each: 16 rows x the wave's 16 columns) that the epilogues of that chunk's steps read;
+// the block of the last G1 block's epilogue (run after the pass) rides on the next G2 chunk 0.
+template <int NB, int KS1, int SPC>
+struct ZChunks {
+  static constexpr int NZB = SPC / KS1;  // Z blocks per G1 chunk
+  // Z block carried in slot q of G1 chunk c (-1: none)
+  static constexpr int g1_block(int c, int q) {
+    const int b = c * NZB - 1 + q;
+    return (b >= 0 && b < NB) ? b : -1;
+  }
+  static constexpr int g1_blocks(int c) {
+    int n = 0;
+    for (int q = 0; q < NZB; ++q) n += g1_block(c, q) >= 0 ? 1 : 0;
+    return n;
+  }
+};
+
+// Static VM-operation windows of the ring barriers.  The barrier of chunk ch sits at position
+// SPC-D of the chunk and waits for chunk ch+1 (weights + Z blocks), whose DMA group was issued
+// at the barrier 3 chunks earlier; younger: the bodies of the 3*SPC steps since and the DMA
+// groups of chunks ch+2, ch+3.  Counted: what every step body issues unconditionally (the
+// epilogue stores) and the DMA instructions (Z blocks at one x4 instruction each; a tile
+// that loads them by dword issues more, which only waits longer).  A step or chunk of the
+// other pass type (the window reaching across a pass boundary) counts with that pass's
+// schedule; the unrolled tails between passes only add younger operations.
+template <int MB, int NB, int KS1, int KS2, int SPC>
 struct Win {
+  using Z = ZChunks<NB, KS1, SPC>;
   static constexpr int ST = NB * KS1;
-  static constexpr int DMA = (2 * SPC + 3) / 4;
+  static constexpr int NCH = ST / SPC;
+  static constexpr int DMA = (2 * SPC + 3) / 4;  // weight DMA instructions per chunk and wave
   static constexpr int row_step(int r, int KS) { return (r * KS) / 4; }
   static constexpr int rows_at(int s, int KS) {
     int c = 0;
     for (int r = 0; r < 4; ++r) c += row_step(r, KS) == s ? 1 : 0;
     return c;
   }
-  // G1 step body: rows of block ib-1 (Z store) + the re-read of block ib-1+kLA
+  // G1 step body: block ib-1's Z store (one dwordx4 per lane after its last row)
   static constexpr int ops1(int t) {
     const int ib = t / KS1, s = t % KS1;
-    if (ib == 0) return 0;
-    return rows_at(s, KS1) * (1 + (ib - 1 + kLA < NB ? 1 : 0));
+    return (ib == 0 || s != row_step(3, KS1)) ? 0 : 1;
   }
-  // G2 step body: rows of block ib-1 (E, L, T stores; V1: 3 beta loads)
+  // G2 step body: block ib-1's E, L, T stores
   static constexpr int ops2(int t) {
     const int ib = t / KS2, s = t % KS2;
-    if (ib == 0) return 0;
-    return rows_at(s, KS2) * (3 + ELOADS);
+    return (ib == 0 || s != row_step(3, KS2)) ? 0 : 3;
+  }
+  // DMA group of chunk c (c >= NCH: chunk c - NCH of the other pass)
+  static constexpr int group(int c, bool g1) {
+    if (c >= NCH) return group(c - NCH, !g1);
+    if (g1) return DMA + Z::g1_blocks(c);
+    return DMA + (c == 0 ? 1 : 0);  // G2 chunk 0 carries the last G1 block's Z
   }
   template <int T, bool G1>
   static constexpr int win() {
-    int n = 2 * DMA;
+    const int ch = T / SPC;
+    int n = group(ch + 2, G1) + group(ch + 3, G1);
     for (int u = T - 3 * SPC; u < T; ++u) {
       if (u >= 0) n += G1 ? ops1(u) : ops2(u);
       else if (ST + u >= 0) n += G1 ? ops2(ST + u) : ops1(ST + u);
@@ -147,19 +246,30 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
   static_assert(ST == MB * KS2, "both GEMMs have MP*NP/512 steps");
   static_assert(MB % 2 == 0 && NB % 2 == 0, "k-steps cover two 16-row blocks");
   constexpr int SPC = ST < 8 ? ST : 8;  // steps per ring chunk
-  static_assert(SPC >= 2 && ST % SPC == 0, "chunking");
+  static_assert(SPC >= 2 && ST % SPC == 0 && SPC % KS1 == 0, "chunking");
   constexpr int NCH = ST / SPC;
-  constexpr int D = ST >= 4 ? 2 : 1;  // fragment read-ahead (steps)
-  constexpr int R = 2 * D;            // fragment register rotation; divides ST, so every pass
-                                      // starts at rotation 0
+  // the DMA group issued at a barrier targets the chunk 4 ahead: it must lie in this pass or the
+  // next (the Z blocks a G1 chunk carries are only complete one pass ahead)
+  static_assert(NCH >= kSlots, "at least kSlots chunks per pass");
+#ifndef X3_ROT
+#define X3_ROT 4
+#endif
+  constexpr int R = ST % X3_ROT == 0 ? X3_ROT : 2;  // fragment register rotation; divides ST, so
+                                                    // every pass starts at rotation 0
+  constexpr int D = R - 1;                // fragment read-ahead (steps)
   static_assert(ST % R == 0 && SPC >= D + 1, "rotation");
-  constexpr int FPC = 2 * SPC;  // 1 KiB fragments per chunk
-  constexpr int RING_F4 = kSlots * FPC * 64;
+  using ZC = ZChunks<NB, KS1, SPC>;
+  constexpr int NZB = ZC::NZB;
+  constexpr int FPC = 2 * SPC;                 // 1 KiB weight fragments per chunk
+  constexpr int SLOT_F4 = (FPC + kWaves * NZB) * 64;  // + each wave's Z blocks
+  constexpr int RING_F4 = kSlots * SLOT_F4;
   constexpr int X_F4 = kWaves * MB * 64;
-  static_assert((RING_F4 + X_F4) * 16 <= 160 * 1024, "LDS budget");
+  constexpr int STG_F4 = kWaves * 4 * 64;  // per wave 4 output tiles of 16 x 16 floats
+  static_assert(FPC == 16, "DMA issue: 4 fragments per wave and chunk");
+  static_assert((RING_F4 + X_F4 + STG_F4) * 16 <= 160 * 1024, "LDS budget");
   static_assert(PKIND == PK_SCALAR || PKIND == PK_S1, "x3 path: scalar-parameter variants");
-  using W = Win<MB, NB, KS1, KS2, SPC, 0>;
-  __shared__ f32x4 smem[RING_F4 + X_F4];
+  using W = Win<MB, NB, KS1, KS2, SPC>;
+  __shared__ f32x4 smem[RING_F4 + X_F4 + STG_F4];
   f32x4* ring = smem;
   f32x4* xs = smem + RING_F4;  // xs[w][b][lane] = X rows 16b+4g+0..3 of this lane's column
 
@@ -175,11 +285,54 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
   auto lane_off = [&](int64_t ld) -> uint32_t {
     return cv ? (uint32_t)((col + (int64_t)(4 * g) * ld) * 4) : kOOB;
   };
-  constexpr bool kEState = EMODE != EM_V1;  // V1 never reads E_{k-1} (main_lena.py:87)
 
   float Er[MB][4], Lr[MB][4], Vr[MB][4];
   BOp Vpk[KS1], Zpk[KS2];
   float regsum = 0.f, fit1 = 0.f, fit2 = 0.f;
+
+  // ---------------------------------------------------------------- Z_{k-1} delivery
+  // Block b of the Z matrix the next G1 chunks need (set per pass): rows 16b + (l >> 2), the
+  // wave's columns c0 + 4 (l & 3) .. +3 -> LDS [16 rows][16 columns], 64 B rows.  The C ABI
+  // routes a batch that is not a multiple of 4, or unaligned rows, to the fp32 kernel, so a
+  // lane's 4 columns are all valid or all padding.
+  const int64_t c0 = (int64_t)blockIdx.x * kTileCols + w * 16;
+  auto off4 = [&](int64_t ld) -> uint32_t {  // lane offset of the 16-B-per-lane form
+    const int64_t c4 = c0 + 4 * (lane & 3);
+    return c4 < a.B ? (uint32_t)(((lane >> 2) * ld + c4) * 4) : kOOB;
+  };
+  struct ZSrc { i32x4 r; uint32_t v4; uint32_t ld4; };
+  auto zsrc = [&](const float* p, int64_t ld) -> ZSrc {
+    return ZSrc{mk_rsrc4(p, (uint32_t)(n * ld * 4)), off4(ld), (uint32_t)(ld * 4)};
+  };
+  ZSrc zd;  // source of the Z blocks the DMA groups issued during the current pass carry
+  auto zdma = [&](int b, const f32x4* dst) {
+    if constexpr (!(X3_ABL & 32)) blds16(zd.r, zd.v4, (uint32_t)(16 * b) * zd.ld4, dst);
+  };
+  // this wave's Z region of a ring slot: [NZB][1 KiB]
+  auto zreg = [&](int slot, int q) -> f32x4* {
+    return ring + slot * SLOT_F4 + (FPC + w * NZB + q) * 64;
+  };
+  // rows 4g + 0..3 of the lane's column from a Z block in LDS
+  auto zread = [&](const f32x4* blk, float (&v)[4]) {
+    const float* f = reinterpret_cast<const float*>(blk);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = f[(4 * g + r) * 16 + j];
+  };
+
+  // ---------------------------------------------------------------- output stores
+  // An epilogue row writes its value into this wave's 16 x 16 staging tile (LDS, ds_write_b32);
+  // once a block's 4 rows are done the tile goes out as ONE buffer_store_dwordx4 per lane (lane
+  // l: row l >> 2, columns 4 (l & 3) .. +3 of the wave's 16): 4x fewer store instructions than
+  // a dword per row (the store path is per-instruction bound).  Tiles whose rows are not
+  // 16-B aligned (or a batch not a multiple of 4) run on the fp32 kernel (C ABI plan).
+  f32x4* stg = smem + RING_F4 + X_F4 + w * 4 * 64;
+  auto stage = [&](int tile, int r, float v) {
+    reinterpret_cast<float*>(stg + tile * 64)[(4 * g + r) * 16 + j] = v;
+  };
+  // the finished tile -> rows 16b.. of the matrix (voff4: lane offset, soff: the block's rows)
+  auto flush = [&](int tile, rsrc_t rs, uint32_t voff4, uint32_t soff) {
+    bstore4(rs, voff4, soff, stg[tile * 64 + lane]);
+  };
 
   // ---------------------------------------------------------------- weight stream
   // GEMM gi: 0 = prologue A, 2k+1 = -W_k, 2k+2 = A; past the last GEMM, A again as filler.
@@ -193,18 +346,34 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     asm volatile("" : "+s"(sb));
     return (const float*)sb + (int64_t)(ch % NCH) * FPC * kFrag;
   };
-  auto issue = [&](const float* base, int slot) {
-    f32x4* dst = ring + slot * (FPC * 64);
-#pragma unroll
-    for (int i = 0; i < (FPC + 3) / 4; ++i) {
-      const int f = i * 4 + w;
-      if (FPC % 4 == 0 || f < FPC) glds16(base + f * kFrag, lane * 16, dst + f * 64);
+  // DMA group of chunk CH (relative to the pass: CH >= NCH = the next pass) into `slot`
+  auto issue = [&](auto G1_, auto CH_, int gi, int slot) {
+    constexpr bool G1 = decltype(G1_)::value;
+    constexpr int CH = decltype(CH_)::value;
+    const float* base = chunk_src(gi, CH);
+    f32x4* dst = ring + slot * SLOT_F4;
+    // wave w: fragments 4w .. 4w+3
+    if constexpr (!(X3_ABL & 1)) glds16x4(base + 4 * w * kFrag, lane * 16, dst + 4 * w * 64);
+    constexpr bool tg1 = (CH < NCH) == G1;  // the target chunk is a G1 chunk
+    constexpr int tc = CH < NCH ? CH : CH - NCH;
+    if constexpr (tg1) {
+      static_for<NZB>([&](auto Q_) {
+        constexpr int q = decltype(Q_)::value;
+        if constexpr (ZC::g1_block(tc, q) >= 0) zdma(ZC::g1_block(tc, q), zreg(slot, q));
+      });
+    } else if constexpr (tc == 0 && G1) {
+      zdma(NB - 1, zreg(slot, 0));  // the last G1 block, for the tail after the pass
     }
   };
   auto slot_add = [](int s, int d) -> int { s += d; return s >= kSlots ? s - kSlots : s; };
   int cur = 0;
   auto frag = [&](int slot, int f) -> f16x8 {
-    return __builtin_bit_cast(f16x8, ring[(slot * FPC + f) * 64 + lane]);
+    if constexpr (X3_ABL & 64) {
+      f16x8 v = {};
+      v[0] = (_Float16)(float)(slot * 16 + f);
+      return v;
+    }
+    return __builtin_bit_cast(f16x8, ring[slot * SLOT_F4 + f * 64 + lane]);
   };
 
   // ---------------------------------------------------------------- parameters
@@ -232,7 +401,8 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
 
   // ---------------------------------------------------------------- initial state
   const uint32_t oz0 = lane_off(a.ldz0), oo = lane_off(a.ldo), ozw = lane_off(a.ldzw);
-  float zmx = 0.f;       // lane max of |Z_k| of the layer being formed
+  const uint32_t ozw4 = off4(a.ldzw);
+  float zmx = 0.f;        // lane max of |Z_k| of the layer being formed
   float zmx_prev;         // column max of Z_{k-1} (Z0 first), exact
   int zexp;               // scale exponent the current Zpk was split with
   {
@@ -280,32 +450,41 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
   }
 
   const uint32_t mbytes = (uint32_t)(m * a.ldo * 4);
+  const uint32_t oo4 = off4(a.ldo);
   SWalk zw{0u, (uint32_t)(a.ldo * 4)}, mw{0u, (uint32_t)(a.ldo * 4)};
-  SWalk zr{0u, (uint32_t)(a.ldo * 4)};  // Z_{k-1} re-read walker (row stride set per layer)
 
   // ---------------------------------------------------------------- epilogues
   // G1 block b, row r of layer k: Z = S(Z_{k-1} + s1 * q, theta_z) with q = -W_k Var (the packed
   // weights are negated), main_lena.py:86 / main_syn_l1l1_scalar_tied.py:114
-  float zn[2][4];   // fp32 Z_k of the current block pair, split into Zpk when complete
-  float zo[kLA + 1][4];  // re-read Z_{k-1} of the next blocks (ring over blocks)
-  auto epi1_row = [&](const LayerP& P, rsrc_t rzo, uint32_t vzo, const SWalk& zs, int b, int r,
-                      float q) {
-    const float zp = zo[b % (kLA + 1)][r];
-    const float u = (PKIND == PK_S1) ? zp + P.s1 * q : zp + q;
+  float zn[2][4];        // fp32 Z_k of the current block pair, split into Zpk when complete
+  float zo[NZB][4];      // Z_{k-1} of the blocks whose epilogues run in the current chunk
+  // acc = the chain's raw sum; qs = 2^-(sW + sVar) (times s1 for V5): acc * qs is exactly the
+  // reference's fc(Var) (s1 * fc(Var)) up to the GEMM's rounding, so the fma is one rounding of
+  // Z_{k-1} - fc(Var) like the reference's subtraction
+  auto epi1_row = [&](const LayerP& P, int b, int r, float zp, float acc, float qs) {
+    if constexpr (X3_ABL & 2) { zn[b & 1][r] = acc; return; }
+    float u;
+    if constexpr (PKIND == PK_S1) u = zp + acc * qs;
+    else u = __builtin_fmaf(acc, qs, zp);
     const float z = shrink_u(u, P.thz);
     zn[b & 1][r] = z;
-    bstore_s(rzo, vzo, zs.at(r), z);
+    stage(0, r, z);
     regsum += fabsf(z);
-    zmx = fmaxf(zmx, fabsf(z));
+    zmx = amax(zmx, z);
     // materialise the running sums here: left alone, the scheduler sinks both serial chains
     // below the pass and keeps every row's z live (spills)
     asm volatile("" : "+v"(regsum), "+v"(zmx));
   };
   // G2 block b, row r of layer k (Pv = A Z_k, x = X).  pro: T0 = A Z0 + E0 - X, Var_0.
   struct OutR { rsrc_t e, l, t; };
+  auto flush2 = [&](const OutR& O, uint32_t soff) {
+    flush(1, O.e, oo4, soff);
+    flush(2, O.l, oo4, soff);
+    flush(3, O.t, oo4, soff);
+  };
   float vmx = 0.f;
-  auto epi2_row = [&](const LayerP& P, const OutR& O, bool pro, int b, int r, float Pv, float x,
-                      uint32_t so) {
+  auto epi2_row = [&](const LayerP& P, bool pro, int b, int r, float Pv, float x) {
+    if constexpr (X3_ABL & 2) { Vr[b][r] = Pv; pin_agpr(Vr[b][r]); return; }
     const float l0 = Lr[b][r];
     const float e0 = Er[b][r];
     float e;
@@ -323,14 +502,14 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     l = pro ? l0 : l;
     Er[b][r] = e;
     Lr[b][r] = l;
-    bstore_s(O.e, oo, so, e);
-    bstore_s(O.l, oo, so, l);
-    bstore_s(O.t, oo, so, t);
+    stage(1, r, e);
+    stage(2, r, l);
+    stage(3, r, t);
     const float res = x - Pv;
     fit1 += fabsf(res);
     fit2 = __builtin_fmaf(res, res, fit2);
     const float v = l + P.b1n * t;                                   // main_lena.py:85
-    vmx = fmaxf(vmx, fabsf(v));
+    vmx = amax(vmx, v);
     asm volatile("" : "+v"(fit1), "+v"(fit2), "+v"(vmx));
     Vr[b][r] = v;
     pin_agpr(Vr[b][r]);  // AGPRs: Vr, Zpk (G2) / Vpk, Zpk (G1); VGPRs: E, L, fragments
@@ -352,10 +531,11 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
 
   // ---------------------------------------------------------------- ring steps
   // Step t of a GEMM pass: head = read-ahead of step t+D's two fragments (at chunk position
-  // SPC-D: ring barrier, DMA of chunk ch+4 into the freed slot, first fragments of the next
-  // chunk), then the step body (epilogue rows / operand splits), then 3 MFMAs.
+  // SPC-D: ring barrier, DMA group of chunk ch+4 into the freed slot, first fragments of the
+  // next chunk), then the step body (epilogue rows / operand splits), then 3 MFMAs.
   f16x8 frh[R], frl[R];
-  auto step_head = [&](auto T_, int gi, auto WIN_) {
+  auto step_head = [&](auto G1_, auto T_, int gi) {
+    constexpr bool G1 = decltype(G1_)::value;
     constexpr int t = decltype(T_)::value;
     constexpr int c = t % SPC, ch = t / SPC;
     constexpr int tn = t + D;
@@ -363,10 +543,11 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
       frh[tn % R] = frag(cur, 2 * (c + D));
       frl[tn % R] = frag(cur, 2 * (c + D) + 1);
     } else {
-      // every wave has read all of chunk ch (its last fragments were read D steps ago)
+      // every wave has read all of chunk ch (its last fragments D steps ago, its Z blocks at
+      // the chunk's first step)
       if constexpr (c + D == SPC) {
-        ring_barrier_cnt<decltype(WIN_)::value>();
-        issue(chunk_src(gi, ch + kSlots), cur);
+        ring_barrier_cnt<(X3_ABL & 128) ? 63 : W::template win<t, G1>()>();
+        issue(G1_, std::integral_constant<int, ch + kSlots>{}, gi, cur);
       }
       const int nx = slot_add(cur, 1);
       frh[tn % R] = frag(nx, 2 * (c + D - SPC));
@@ -379,15 +560,19 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     if constexpr (t % SPC == SPC - 1) cur = slot_add(cur, 1);
   };
   auto mfma3 = [&](int tr, const BOp& bop, f32x4 acc) -> f32x4 {
+    if constexpr (X3_ABL & 16) {
+      acc[0] += (float)frh[tr][0] + (float)bop.hi[0] + (float)bop.lo[1] + (float)frl[tr][2];
+      return acc;
+    }
     acc = mfma(frh[tr], bop.hi, acc);
     acc = mfma(frh[tr], bop.lo, acc);
     return mfma(frl[tr], bop.hi, acc);
   };
 
-  // prime the ring: chunks 0..3 of the prologue GEMM, then steps 0 and 1's fragments
-#pragma unroll
-  for (int c = 0; c < kSlots; ++c) issue(chunk_src(0, c), c);
-  ring_barrier_cnt<(kSlots - 1) * W::DMA>();
+  // prime the ring: chunks 0..3 of the prologue GEMM (its following G1(0) chunks carry Z0)
+  zd = zsrc(a.Z0, a.ldz0);
+  static_for<kSlots>([&](auto C_) { issue(std::false_type{}, C_, 0, decltype(C_)::value); });
+  ring_barrier_cnt<0>();
 #pragma unroll
   for (int t = 0; t < D; ++t) {
     frh[t] = frag(0, 2 * t);
@@ -397,11 +582,11 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
 
   // ---------------------------------------------------------------- G1(k): -W_k Var -> Z_k
-  // Block ib's epilogue runs in block ib+1's steps (row r at step (r*KS1)/4) with the re-read
-  // of block ib-1+kLA of Z_{k-1}; Zpk[s] is split once blocks 2s, 2s+1 are complete; block 0's
-  // steps split Var into Vpk.  The last block's epilogue runs after the MFMAs.
-  auto g1_pass = [&](int k, const LayerP& P, rsrc_t rzo, uint32_t vzo, rsrc_t rzp,
-                     uint32_t vzp, float vsc, float vinv, float zsc) {
+  // Block ib's epilogue runs in block ib+1's steps (row r at step (r*KS1)/4) on the Z_{k-1}
+  // block its chunk carried; Zpk[s] is split once blocks 2s, 2s+1 are complete; block 0's steps
+  // split Var into Vpk.  The last block's epilogue runs after the MFMAs.
+  auto g1_pass = [&](int k, const LayerP& P, rsrc_t rzo, uint32_t vzo4, uint32_t vzo, float vsc,
+                     float qs, float zsc) {
     const int gi = 2 * k + 1;
     zw.reset();
     SWalk zs = zw;
@@ -412,8 +597,14 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
       static_for<KS1>([&](auto S_) {
         constexpr int s = decltype(S_)::value;
         constexpr int t = ib * KS1 + s;
-        step_head(std::integral_constant<int, t>{}, gi,
-                  std::integral_constant<int, W::template win<t, true>()>{});
+        // first step of a chunk: its Z_{k-1} blocks -> registers (before the slot is reused)
+        if constexpr (t % SPC == 0) {
+          static_for<NZB>([&](auto Q_) {
+            constexpr int q = decltype(Q_)::value;
+            if constexpr (ZC::g1_block(t / SPC, q) >= 0) zread(zreg(cur, q), zo[q]);
+          });
+        }
+        step_head(std::true_type{}, std::integral_constant<int, t>{}, gi);
         if constexpr (ib == 0) {
           Vpk[s] = split8(Vr[2 * s], Vr[2 * s + 1], vsc);
           pin_agpr_b(Vpk[s]);
@@ -421,11 +612,12 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
           static_for<4>([&](auto R_) {
             constexpr int r = decltype(R_)::value;
             if constexpr (W::row_step(r, KS1) == s) {
-              epi1_row(P, rzo, vzo, zs, ib - 1, r, qp[r] * vinv);
-              if constexpr (r == 3) zs.next();
-              if constexpr (ib - 1 + kLA < NB)
-                zo[(ib - 1 + kLA) % (kLA + 1)][r] =
-                    bload(rzp, vzp + zr.at(16 * (ib - 1 + kLA) + r));
+              constexpr int q = (ib - 1) + 1 - (t / SPC) * NZB;  // Z block slot in this chunk
+              epi1_row(P, ib - 1, r, zo[q][r], qp[r], qs);
+              if constexpr (r == 3) {
+                flush(0, rzo, vzo4, zs.at(0));
+                zs.next();
+              }
             }
           });
           // blocks 2s', 2s'+1 complete (the odd block's last row ran at this step or before)
@@ -440,9 +632,12 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
       });
       qp = acc;
     });
-    // tail: block NB-1
+    // tail: block NB-1 (its Z_{k-1} block rode on the next G2 chunk 0, now slot cur)
+    float zl[4];
+    zread(zreg(cur, 0), zl);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) epi1_row(P, rzo, vzo, zs, NB - 1, r, qp[r] * vinv);
+    for (int r = 0; r < 4; ++r) epi1_row(P, NB - 1, r, zl[r], qp[r], qs);
+    flush(0, rzo, vzo4, zs.at(0));
     Zpk[KS2 - 1] = split8(zn[0], zn[1], zsc);
     pin_agpr_b(Zpk[KS2 - 1]);
   };
@@ -461,14 +656,16 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
       static_for<KS2>([&](auto S_) {
         constexpr int s = decltype(S_)::value;
         constexpr int t = ib * KS2 + s;
-        step_head(std::integral_constant<int, t>{}, gi,
-                  std::integral_constant<int, W::template win<t, false>()>{});
+        step_head(std::false_type{}, std::integral_constant<int, t>{}, gi);
         if constexpr (ib > 0) {
           static_for<4>([&](auto R_) {
             constexpr int r = decltype(R_)::value;
             if constexpr (W::row_step(r, KS2) == s) {
-              epi2_row(P, O, PRO, ib - 1, r, qp[r] * zinv, xv[r], mw.at(r));
-              if constexpr (r == 3) mw.next();
+              epi2_row(P, PRO, ib - 1, r, qp[r] * zinv, xv[r]);
+              if constexpr (r == 3) {
+                flush2(O, mw.at(0));
+                mw.next();
+              }
             }
           });
         }
@@ -479,9 +676,8 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     });
     const f32x4 xv = xs[(w * MB + MB - 1) * 64 + lane];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      epi2_row(P, O, PRO, MB - 1, r, qp[r] * zinv, xv[r], mw.at(r));
-    }
+    for (int r = 0; r < 4; ++r) epi2_row(P, PRO, MB - 1, r, qp[r] * zinv, xv[r]);
+    flush2(O, mw.at(0));
   };
 
   // ---------------------------------------------------------------- prologue + K layers
@@ -500,38 +696,29 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     // Var_k (from G2(k-1) / the prologue): exact column scale for this layer's weight
     const int vexp = scale_exp(col_max(vmx), swk, 0);
     vmx = 0.f;
-    // Z_{k-1}: where it was written, and its lane offset / row stride
-    const bool zp_in = k == 0;
-    const float* zpp = zp_in ? a.Z0
-                             : (a.keep_all ? a.Zo + (int64_t)(k - 1) * n * a.ldo
-                                           : a.Zw + (int64_t)((k - 1) & 1) * n * a.ldzw);
-    const int64_t ldzp = zp_in ? a.ldz0 : (a.keep_all ? a.ldo : a.ldzw);
-    const rsrc_t rzp = mkrsrc(zpp, (uint32_t)(n * ldzp * 4));
-    const uint32_t vzp = zp_in ? oz0 : (a.keep_all ? oo : ozw);
-    zr = SWalk{0u, (uint32_t)(ldzp * 4)};
-    // Z_k goes to the output (keep_all or last layer) or to the lean-mode workspace
+    // Z_{k-1} -- the DMA source of this pass's groups (G1(k) chunks, G2(k) chunk 0) -- is set
+    // (previous pass); Z_k goes to the output (keep_all or last layer) or the lean workspace
     const bool zout = a.keep_all || last;
     const int64_t ldzo = zout ? a.ldo : a.ldzw;
     float* zop = zout ? a.Zo + (int64_t)(a.keep_all ? k : 0) * n * a.ldo
                       : a.Zw + (int64_t)(k & 1) * n * a.ldzw;
     const rsrc_t rzo = mkrsrc(zop, (uint32_t)(n * ldzo * 4));
     const uint32_t vzo = zout ? oo : ozw;
+    const uint32_t vzo4 = zout ? oo4 : ozw4;
     zw = SWalk{0u, (uint32_t)(ldzo * 4)};
-    // re-read the first kLA blocks of Z_{k-1}
-#pragma unroll
-    for (int b = 0; b < kLA; ++b)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) zo[b][r] = bload(rzp, vzp + zr.at(16 * b + r));
     // provisional scale of Z_k's split: the column max of Z_{k-1} with kHead bits of headroom
     const int zexp_p = scale_exp(zmx_prev, sw_a, kHead);
     zmx = 0.f;
-    g1_pass(k, P, rzo, vzo, rzp, vzp, exp2i(vexp), exp2i(-(vexp + swk)), exp2i(zexp_p));
+    const float qs = (PKIND == PK_S1 ? P.s1 : 1.0f) * exp2i(-(vexp + swk));
+    g1_pass(k, P, rzo, vzo4, vzo, exp2i(vexp), qs, exp2i(zexp_p));
+    // the groups issued during G2(k) carry Z_k for G1(k+1)
+    zd = zsrc(zop, ldzo);
     // exact column max of Z_k; re-split if a column outgrew the provisional scale
     const float zm = col_max(zmx);
     zmx_prev = zm;
     zexp = zexp_p;
     if (__any(zm * exp2i(zexp_p) >= 65504.0f)) {  // wave-uniform; rare (first layer)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // this wave's Z_k stores
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's Z_k stores
       zexp = scale_exp(zm, sw_a, 0);
       const float sc = exp2i(zexp);
       SWalk rw{0u, (uint32_t)(ldzo * 4)};
@@ -582,10 +769,11 @@ bool x3_supports(int variant) {
          variant == DLADMM_V6_LASSO;
 }
 
+// Shapes 1 and 2 only: shape 0 (32 x 32) has fewer than kSlots chunks per pass; the C ABI
+// runs those problems on shape 1 (zero padding is exact).
 hipError_t launch_fused_x3_shape(int shape, int variant, const FusedArgs& a, int grid,
                                  hipStream_t s) {
   switch (shape) {
-    case 0: return dispatch_x3_variant<kShapeMP[0], kShapeNP[0]>(variant, a, grid, s);
     case 1: return dispatch_x3_variant<kShapeMP[1], kShapeNP[1]>(variant, a, grid, s);
     case 2: return dispatch_x3_variant<kShapeMP[2], kShapeNP[2]>(variant, a, grid, s);
   }
