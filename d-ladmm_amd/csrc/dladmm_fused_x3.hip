@@ -46,7 +46,8 @@
 #define X3_ABL 0  // timing experiments only (tools/x3_ablate.py), every bit gives WRONG results:
                   // 1 no weight DMA, 2 no epilogue work, 4 no output stores, 8 no operand splits,
                   // 16 no MFMAs, 32 no Z re-read DMA, 64 no fragment LDS reads, 128 ring barriers
-                  // do not wait for the DMA (vmcnt(63))
+                  // do not wait for the DMA (vmcnt(63)), 256 no s_barrier, 512 no lgkmcnt(0)
+                  // drain at the ring barrier, 1024 every store to one 1 KiB block (L2-resident)
 #endif
 
 namespace dladmm {
@@ -148,10 +149,16 @@ __device__ __forceinline__ void glds16x4(const float* sbase, uint32_t voff, cons
       : "v"(voff), "s"(sbase), "s"(dst)
       : "memory");
 }
+// Store cache policy of the output tiles. Measured on the d=15 headline (tools/x3_ablate.py,
+// profiles/r02_x3_ablations.md): default policy 2.58 ms, sc0 2.59, nt 2.72, nt|sc1 2.73. The
+// fp32 kernels keep DLADMM_STORE_AUX (nt); here the full-line dwordx4 stores merge in L2 anyway.
+#ifndef X3_STORE_AUX
+#define X3_STORE_AUX 0
+#endif
 __device__ __forceinline__ void bstore4(rsrc_t r, uint32_t voff, uint32_t soff, f32x4 v) {
   if constexpr (!(X3_ABL & 4))
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), r, (int)voff, (int)soff,
-                                           DLADMM_STORE_AUX);
+                                           X3_STORE_AUX);
 }
 // m = max(m, |v|) in one v_max_f32 (fmaxf would canonicalise both inputs first)
 __device__ __forceinline__ float amax(float m, float v) {
@@ -331,6 +338,10 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
   };
   // the finished tile -> rows 16b.. of the matrix (voff4: lane offset, soff: the block's rows)
   auto flush = [&](int tile, rsrc_t rs, uint32_t voff4, uint32_t soff) {
+    if constexpr (X3_ABL & 1024) {
+      bstore4(rs, (uint32_t)(lane * 16), 0u, stg[tile * 64 + lane]);
+      return;
+    }
     bstore4(rs, voff4, soff, stg[tile * 64 + lane]);
   };
 
@@ -546,7 +557,12 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
       // every wave has read all of chunk ch (its last fragments D steps ago, its Z blocks at
       // the chunk's first step)
       if constexpr (c + D == SPC) {
-        ring_barrier_cnt<(X3_ABL & 128) ? 63 : W::template win<t, G1>()>();
+        if constexpr (X3_ABL & 256) {
+          if constexpr (X3_ABL & 512) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((X3_ABL & 128) ? 63 : W::template win<t, G1>()) : "memory");
+          else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((X3_ABL & 128) ? 63 : W::template win<t, G1>()) : "memory");
+        } else {
+          ring_barrier_cnt<(X3_ABL & 128) ? 63 : W::template win<t, G1>()>();
+        }
         issue(G1_, std::integral_constant<int, ch + kSlots>{}, gi, cur);
       }
       const int nx = slot_add(cur, 1);

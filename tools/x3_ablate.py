@@ -4,7 +4,7 @@ d-ladmm_amd/lib/abl/libdladmm_hip_x3abl<N>.so.  Run a variant with DLADMM_LIB=<t
 Every nonzero variant computes WRONG results: timing only.
 
     python tools/x3_ablate.py 1 2 4 8 16     # build (CPU)
-    python tools/x3_ablate.py X3_ABL=0,DLADMM_STORE_AUX=16   # arbitrary -D sets
+    python tools/x3_ablate.py X3_ABL=0,X3_STORE_AUX=16   # arbitrary -D sets
 """
 import os
 import subprocess
