@@ -464,6 +464,11 @@ inline int run_fused_x3(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipSt
   a.lossp = (float*)(ws + p.off_loss);
   a.wexp = wexp;
   a.Zw = (float*)(ws + p.off_zw); a.ldzw = p.ldzw;
+  static unsigned long long* const dbg = [] {  // diagnostic builds (X3_STAMP) write here
+    const char* e = getenv("DLADMM_DBG_PTR");
+    return e ? (unsigned long long*)strtoull(e, nullptr, 0) : nullptr;
+  }();
+  a.dbg = dbg;
   if (d->ev_kernel_start) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_start, s)) return (int)e;
   }

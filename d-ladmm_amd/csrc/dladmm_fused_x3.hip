@@ -47,7 +47,21 @@
                   // 1 no weight DMA, 2 no epilogue work, 4 no output stores, 8 no operand splits,
                   // 16 no MFMAs, 32 no Z re-read DMA, 64 no fragment LDS reads, 128 ring barriers
                   // do not wait for the DMA (vmcnt(63)), 256 no s_barrier, 512 no lgkmcnt(0)
-                  // drain at the ring barrier, 1024 every store to one 1 KiB block (L2-resident)
+                  // drain at the ring barrier, 1024 every store to one 1 KiB block (L2-resident),
+                  // 2048 each store instruction writes 1 KiB contiguous (same bytes)
+#endif
+#ifndef X3_OFF
+#define X3_OFF 0  // A/B knob: 1 immediate tile stores, 2 Z_{k-1} block read at the chunk start,
+                  // 4 X rows read at the block start (the earlier schedules; correct results)
+#endif
+#ifndef X3_STAMP
+#define X3_STAMP 0  // diagnostic build: per-wave cycle sums of the passes and ring barriers
+#endif
+#ifndef X3_SGB
+#define X3_SGB 0  // >0: interleave that many non-MFMA instructions between a step's 3 MFMAs
+#endif
+#ifndef X3_SGM
+#define X3_SGM 0x386  // instruction classes of those fillers (VALU | SALU | DS)
 #endif
 
 namespace dladmm {
@@ -113,13 +127,6 @@ __device__ __forceinline__ int scale_exp(float mx, int sw, int head) {
 }
 __device__ __forceinline__ float exp2i(int e) { return __builtin_amdgcn_ldexpf(1.0f, e); }
 
-// Static VM-operation windows of the ring barriers.  The barrier of chunk ch sits at position
-// SPC-D of the chunk (D = fragment read-ahead in steps) and waits for chunk ch+1, whose DMA was
-// issued at the barrier 3 chunks earlier; younger: the bodies of the 3*SPC steps since, and the DMAs of chunks ch+2, ch+3.
-// Counted here: the stores and loads every step body issues unconditionally.  A step of the
-// other pass type (the window reaching back across a pass boundary) counts with that pass's
-// schedule; the unrolled tails between passes only add younger operations (not counted: a
-// lower bound only waits longer).
 // LDS-DMA through a buffer resource, lane l: 16 B from voff + soff to LDS at ldst + 16 l.
 // Out-of-range lanes (kOOB: padded columns) read 0, so padded columns stay exactly zero.  M0 is
 // compiler-reserved: saved and restored in the statement.
@@ -215,16 +222,27 @@ struct Win {
     for (int r = 0; r < 4; ++r) c += row_step(r, KS) == s ? 1 : 0;
     return c;
   }
-  // G1 step body: block ib-1's Z store (one dwordx4 per lane after its last row)
-  static constexpr int ops1(int t) {
-    const int ib = t / KS1, s = t % KS1;
-    return (ib == 0 || s != row_step(3, KS1)) ? 0 : 1;
+  // Deferred tile stores: the staging tile of a finished block is read back (ds_read_b128) one
+  // step after its last row and stored one step after that, so neither the read nor the store
+  // waits on LDS latency.  Tile i (G2: E, L, T) is read at step s3 + 1 + i and stored at
+  // s3 + 2 + i of the block whose steps ran the rows; a store past the block's last step runs
+  // at the start of the next block.  Shapes too small for that flush at the last row.
+  static constexpr int s3(int KS) { return row_step(3, KS); }
+  static constexpr bool defer(int KS, int tiles) { return !(X3_OFF & 1) && s3(KS) + tiles < KS; }
+  static constexpr int stores_at(int ib, int s, int KS, int tiles) {
+    if (!defer(KS, tiles)) return (ib == 0 || s != s3(KS)) ? 0 : tiles;
+    int n = 0;
+    for (int i = 0; i < tiles; ++i) {
+      const int ss = s3(KS) + 2 + i;
+      if (ss < KS) n += (ib >= 1 && s == ss) ? 1 : 0;
+      else n += (ib >= 2 && s == ss - KS) ? 1 : 0;
+    }
+    return n;
   }
-  // G2 step body: block ib-1's E, L, T stores
-  static constexpr int ops2(int t) {
-    const int ib = t / KS2, s = t % KS2;
-    return (ib == 0 || s != row_step(3, KS2)) ? 0 : 3;
-  }
+  // G1 step body: the Z tile store (one dwordx4 per lane)
+  static constexpr int ops1(int t) { return stores_at(t / KS1, t % KS1, KS1, 1); }
+  // G2 step body: the E, L, T tile stores
+  static constexpr int ops2(int t) { return stores_at(t / KS2, t % KS2, KS2, 3); }
   // DMA group of chunk c (c >= NCH: chunk c - NCH of the other pass)
   static constexpr int group(int c, bool g1) {
     if (c >= NCH) return group(c - NCH, !g1);
@@ -337,13 +355,26 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     reinterpret_cast<float*>(stg + tile * 64)[(4 * g + r) * 16 + j] = v;
   };
   // the finished tile -> rows 16b.. of the matrix (voff4: lane offset, soff: the block's rows)
-  auto flush = [&](int tile, rsrc_t rs, uint32_t voff4, uint32_t soff) {
+  // v = the tile as read back (lane: its row segment)
+  auto flush_v = [&](int tile, rsrc_t rs, uint32_t voff4, uint32_t soff, f32x4 v) {
     if constexpr (X3_ABL & 1024) {
-      bstore4(rs, (uint32_t)(lane * 16), 0u, stg[tile * 64 + lane]);
+      bstore4(rs, (uint32_t)(lane * 16), 0u, v);
       return;
     }
-    bstore4(rs, voff4, soff, stg[tile * 64 + lane]);
+    if constexpr (X3_ABL & 2048) {  // same bytes, each wave-instruction 1 KiB contiguous
+      const uint32_t b = soff / (uint32_t)(64 * a.ldo);
+      const uint32_t nb = tile == 0 ? NB : MB;
+      bstore4(rs, (uint32_t)(lane * 16), ((blockIdx.x * kWaves + w) * nb + b) * 1024u, v);
+      return;
+    }
+    bstore4(rs, voff4, soff, v);
   };
+  auto flush = [&](int tile, rsrc_t rs, uint32_t voff4, uint32_t soff) {
+    flush_v(tile, rs, voff4, soff, stg[tile * 64 + lane]);
+  };
+  // deferred stores (Win::stores_at): the tile read back one step after the block's last row
+  f32x4 pst;
+  uint32_t pso = 0u;
 
   // ---------------------------------------------------------------- weight stream
   // GEMM gi: 0 = prologue A, 2k+1 = -W_k, 2k+2 = A; past the last GEMM, A again as filler.
@@ -545,6 +576,17 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
   // SPC-D: ring barrier, DMA group of chunk ch+4 into the freed slot, first fragments of the
   // next chunk), then the step body (epilogue rows / operand splits), then 3 MFMAs.
   f16x8 frh[R], frl[R];
+#if X3_STAMP
+  // diagnostic build: per-wave cycle sums (cdna_hip_programming.md, In-kernel stamps); read
+  // their shares only, never this build's run time
+  auto stamp = []() -> uint64_t {
+    uint64_t v;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");
+    return v;
+  };
+  uint64_t st_vm = 0, st_bar = 0, st_g1 = 0, st_g2 = 0, st_mid = 0;
+  const uint64_t st_0 = stamp();
+#endif
   auto step_head = [&](auto G1_, auto T_, int gi) {
     constexpr bool G1 = decltype(G1_)::value;
     constexpr int t = decltype(T_)::value;
@@ -561,7 +603,19 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
           if constexpr (X3_ABL & 512) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((X3_ABL & 128) ? 63 : W::template win<t, G1>()) : "memory");
           else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((X3_ABL & 128) ? 63 : W::template win<t, G1>()) : "memory");
         } else {
+#if X3_STAMP
+          __builtin_amdgcn_sched_barrier(0);
+          const uint64_t t0 = stamp();
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(W::template win<t, G1>()) : "memory");
+          const uint64_t t1 = stamp();
+          asm volatile("s_barrier" ::: "memory");
+          const uint64_t t2 = stamp();
+          __builtin_amdgcn_sched_barrier(0);
+          st_vm += t1 - t0;
+          st_bar += t2 - t1;
+#else
           ring_barrier_cnt<(X3_ABL & 128) ? 63 : W::template win<t, G1>()>();
+#endif
         }
         issue(G1_, std::integral_constant<int, ch + kSlots>{}, gi, cur);
       }
@@ -572,6 +626,14 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
   };
   auto step_tail = [&](auto T_) {
     constexpr int t = decltype(T_)::value;
+#if X3_SGB
+    // MFMA, X3_SGB fillers, MFMA, X3_SGB fillers, MFMA, rest (filler classes: X3_SGM)
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(X3_SGM, X3_SGB, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(X3_SGM, X3_SGB, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#endif
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (t % SPC == SPC - 1) cur = slot_add(cur, 1);
   };
@@ -601,6 +663,10 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
   // Block ib's epilogue runs in block ib+1's steps (row r at step (r*KS1)/4) on the Z_{k-1}
   // block its chunk carried; Zpk[s] is split once blocks 2s, 2s+1 are complete; block 0's steps
   // split Var into Vpk.  The last block's epilogue runs after the MFMAs.
+  constexpr int S31 = W::s3(KS1), S32 = W::s3(KS2);
+  constexpr bool DF1 = W::defer(KS1, 1), DF2 = W::defer(KS2, 3);
+  constexpr bool ZE = !(X3_OFF & 2) && NZB == 1 && S31 < SPC - 1;  // G1: Z_{k-1} read early
+  constexpr bool XE = !(X3_OFF & 4) && S32 + 1 < KS2;  // G2: X rows read after the last use
   auto g1_pass = [&](int k, const LayerP& P, rsrc_t rzo, uint32_t vzo4, uint32_t vzo, float vsc,
                      float qs, float zsc) {
     const int gi = 2 * k + 1;
@@ -613,8 +679,9 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
       static_for<KS1>([&](auto S_) {
         constexpr int s = decltype(S_)::value;
         constexpr int t = ib * KS1 + s;
-        // first step of a chunk: its Z_{k-1} blocks -> registers (before the slot is reused)
-        if constexpr (t % SPC == 0) {
+        // first step of a chunk: its Z_{k-1} blocks -> registers (before the slot is reused);
+        // with one Z block per chunk (ZE) that read runs one step early, below
+        if constexpr (!ZE && t % SPC == 0) {
           static_for<NZB>([&](auto Q_) {
             constexpr int q = decltype(Q_)::value;
             if constexpr (ZC::g1_block(t / SPC, q) >= 0) zread(zreg(cur, q), zo[q]);
@@ -630,12 +697,21 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
             if constexpr (W::row_step(r, KS1) == s) {
               constexpr int q = (ib - 1) + 1 - (t / SPC) * NZB;  // Z block slot in this chunk
               epi1_row(P, ib - 1, r, zo[q][r], qp[r], qs);
-              if constexpr (r == 3) {
+              if constexpr (r == 3 && !DF1) {
                 flush(0, rzo, vzo4, zs.at(0));
                 zs.next();
               }
             }
           });
+          if constexpr (DF1) {
+            if constexpr (s == S31 + 1) {
+              pso = zs.at(0);
+              zs.next();
+              pst = stg[lane];
+            }
+            if constexpr (S31 + 2 < KS1 ? s == S31 + 2 : (ib >= 2 && s == S31 + 2 - KS1))
+              flush_v(0, rzo, vzo4, pso, pst);
+          }
           // blocks 2s', 2s'+1 complete (the odd block's last row ran at this step or before)
           if constexpr (((ib - 1) & 1) && s == KS1 - 1) {
             constexpr int sp = (ib - 1) / 2;
@@ -643,12 +719,20 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
             pin_agpr_b(Zpk[sp]);
           }
         }
+        // ZE: the next chunk's Z_{k-1} block (slot cur+1, landed at this chunk's barrier), read
+        // at this chunk's last step -- after the last row that used zo -- so the next chunk's
+        // first row does not wait on LDS latency
+        if constexpr (ZE && t % SPC == SPC - 1 && t / SPC + 1 < NCH) {
+          if constexpr (ZC::g1_block(t / SPC + 1, 0) >= 0) zread(zreg(slot_add(cur, 1), 0), zo[0]);
+        }
         acc = mfma3(t % R, Vpk[s], acc);
         step_tail(std::integral_constant<int, t>{});
       });
       qp = acc;
     });
-    // tail: block NB-1 (its Z_{k-1} block rode on the next G2 chunk 0, now slot cur)
+    // tail: block NB-2's deferred store (if it wrapped), block NB-1 (its Z_{k-1} block rode on
+    // the next G2 chunk 0, now slot cur)
+    if constexpr (DF1 && S31 + 2 >= KS1) flush_v(0, rzo, vzo4, pso, pst);
     float zl[4];
     zread(zreg(cur, 0), zl);
 #pragma unroll
@@ -664,33 +748,54 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     const int gi = 2 * k + 2;
     mw.reset();
     f32x4 qp = zero4;
+    f32x4 xv;
     static_for<MB>([&](auto IB_) {
       constexpr int ib = decltype(IB_)::value;
       f32x4 acc = zero4;
-      f32x4 xv;
-      if constexpr (ib > 0) xv = xs[(w * MB + ib - 1) * 64 + lane];
+      if constexpr (!XE && ib > 0) xv = xs[(w * MB + ib - 1) * 64 + lane];
       static_for<KS2>([&](auto S_) {
         constexpr int s = decltype(S_)::value;
         constexpr int t = ib * KS2 + s;
         step_head(std::false_type{}, std::integral_constant<int, t>{}, gi);
+        // XE: X rows of block ib (for its epilogue rows in block ib+1's steps / the tail), read
+        // once block ib-1's last row has used xv
+        if constexpr (XE && s == (ib == 0 ? 0 : S32 + 1)) xv = xs[(w * MB + ib) * 64 + lane];
         if constexpr (ib > 0) {
           static_for<4>([&](auto R_) {
             constexpr int r = decltype(R_)::value;
             if constexpr (W::row_step(r, KS2) == s) {
               epi2_row(P, PRO, ib - 1, r, qp[r] * zinv, xv[r]);
-              if constexpr (r == 3) {
+              if constexpr (r == 3 && !DF2) {
                 flush2(O, mw.at(0));
                 mw.next();
               }
             }
           });
+          if constexpr (DF2) {
+            // tile i (E, L, T): stored one step after it was read back (tile i+1 is read in
+            // that same step, after the store consumed pst)
+            static_for<3>([&](auto I_) {
+              constexpr int i = decltype(I_)::value;
+              constexpr int ss = S32 + 2 + i;
+              if constexpr (ss < KS2 ? s == ss : (ib >= 2 && s == ss - KS2))
+                flush_v(1 + i, i == 0 ? O.e : (i == 1 ? O.l : O.t), oo4, pso, pst);
+              if constexpr (s == S32 + 1 + i) {
+                if constexpr (i == 0) {
+                  pso = mw.at(0);
+                  mw.next();
+                }
+                pst = stg[(1 + i) * 64 + lane];
+              }
+            });
+          }
         }
         acc = mfma3(t % R, Zpk[s], acc);
         step_tail(std::integral_constant<int, t>{});
       });
       qp = acc;
     });
-    const f32x4 xv = xs[(w * MB + MB - 1) * 64 + lane];
+    if constexpr (DF2 && S32 + 4 >= KS2) flush_v(3, O.t, oo4, pso, pst);  // block MB-2's T
+    if constexpr (!XE) xv = xs[(w * MB + MB - 1) * 64 + lane];
 #pragma unroll
     for (int r = 0; r < 4; ++r) epi2_row(P, PRO, MB - 1, r, qp[r] * zinv, xv[r]);
     flush2(O, mw.at(0));
@@ -726,7 +831,18 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     const int zexp_p = scale_exp(zmx_prev, sw_a, kHead);
     zmx = 0.f;
     const float qs = (PKIND == PK_S1 ? P.s1 : 1.0f) * exp2i(-(vexp + swk));
+#if X3_STAMP
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t ta = stamp();
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     g1_pass(k, P, rzo, vzo4, vzo, exp2i(vexp), qs, exp2i(zexp_p));
+#if X3_STAMP
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t tb = stamp();
+    __builtin_amdgcn_sched_barrier(0);
+    st_g1 += tb - ta;
+#endif
     // the groups issued during G2(k) carry Z_k for G1(k+1)
     zd = zsrc(zop, ldzo);
     // exact column max of Z_k; re-split if a column outgrew the provisional scale
@@ -757,11 +873,32 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
                  mkrsrc(a.Lo + (int64_t)ko * m * a.ldo, st ? mbytes : 0u),
                  mkrsrc(a.To ? a.To + (int64_t)(a.keep_all ? k + 1 : 0) * m * a.ldo : nullptr,
                         (a.To && st) ? mbytes : 0u)};
+#if X3_STAMP
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t tc = stamp();
+    __builtin_amdgcn_sched_barrier(0);
+    st_mid += tc - tb;
+#endif
     g2_pass(std::false_type{}, k, P, O, exp2i(-(zexp + sw_a)));
+#if X3_STAMP
+    __builtin_amdgcn_sched_barrier(0);
+    st_g2 += stamp() - tc;
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     flush_loss(k);
   }
   // drain: the ring's last LDS-DMAs must land before the workgroup's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if X3_STAMP
+  const uint64_t st_end = stamp();
+  if (a.dbg && lane < 8) {  // vector stores: lane i writes sum i
+    const uint64_t v[8] = {st_end - st_0, st_g1, st_g2, st_mid, st_vm, st_bar, 0, 0};
+    uint64_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x = lane == i ? v[i] : x;
+    a.dbg[((int64_t)blockIdx.x * kWaves + w) * 8 + lane] = x;
+  }
+#endif
 }
 
 template <int MP, int NP, int EM, int PK>

@@ -31,6 +31,8 @@ struct FusedArgs {
   // wexp[1 + k] = -W_k) and the lean-mode Z_k workspace [2][n][ldzw]
   const int* wexp;
   float* Zw; int64_t ldzw;
+  // diagnostic builds only (X3_STAMP): per-wave cycle sums; DLADMM_DBG_PTR (device address)
+  unsigned long long* dbg;
 };
 
 
