@@ -54,6 +54,9 @@
 #define X3_OFF 0  // A/B knob: 1 immediate tile stores, 2 Z_{k-1} block read at the chunk start,
                   // 4 X rows read at the block start (the earlier schedules; correct results)
 #endif
+#ifndef X3_SDLY
+#define X3_SDLY 2  // deferred tile stores: steps between the read-back and the store
+#endif
 #ifndef X3_STAMP
 #define X3_STAMP 0  // diagnostic build: per-wave cycle sums of the passes and ring barriers
 #endif
@@ -222,18 +225,21 @@ struct Win {
     for (int r = 0; r < 4; ++r) c += row_step(r, KS) == s ? 1 : 0;
     return c;
   }
-  // Deferred tile stores: the staging tile of a finished block is read back (ds_read_b128) one
-  // step after its last row and stored one step after that, so neither the read nor the store
-  // waits on LDS latency.  Tile i (G2: E, L, T) is read at step s3 + 1 + i and stored at
-  // s3 + 2 + i of the block whose steps ran the rows; a store past the block's last step runs
-  // at the start of the next block.  Shapes too small for that flush at the last row.
+  // Deferred tile stores: the staging tile of a finished block is read back (ds_read_b128) after
+  // its last row and stored X3_SDLY steps later, so neither the read nor the store waits on LDS
+  // latency.  Tile i (G2: E, L, T) is read at step s3 + 1 + i and stored at rd + X3_SDLY, steps
+  // of the block whose steps ran the rows; a store past the block's last step runs in the next
+  // block (or the pass tail).  Shapes too small for that flush at the last row.
   static constexpr int s3(int KS) { return row_step(3, KS); }
-  static constexpr bool defer(int KS, int tiles) { return !(X3_OFF & 1) && s3(KS) + tiles < KS; }
+  static constexpr bool defer(int KS, int tiles) {
+    return !(X3_OFF & 1) && s3(KS) + tiles < KS && X3_SDLY + tiles - 1 < KS;
+  }
+  static constexpr int st_step(int KS, int i) { return s3(KS) + 1 + i + X3_SDLY; }
   static constexpr int stores_at(int ib, int s, int KS, int tiles) {
     if (!defer(KS, tiles)) return (ib == 0 || s != s3(KS)) ? 0 : tiles;
     int n = 0;
     for (int i = 0; i < tiles; ++i) {
-      const int ss = s3(KS) + 2 + i;
+      const int ss = st_step(KS, i);
       if (ss < KS) n += (ib >= 1 && s == ss) ? 1 : 0;
       else n += (ib >= 2 && s == ss - KS) ? 1 : 0;
     }
@@ -373,7 +379,7 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     flush_v(tile, rs, voff4, soff, stg[tile * 64 + lane]);
   };
   // deferred stores (Win::stores_at): the tile read back one step after the block's last row
-  f32x4 pst;
+  f32x4 pst[3];
   uint32_t pso = 0u;
 
   // ---------------------------------------------------------------- weight stream
@@ -704,13 +710,14 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
             }
           });
           if constexpr (DF1) {
+            constexpr int ss = W::st_step(KS1, 0);
+            if constexpr (ss < KS1 ? s == ss : (ib >= 2 && s == ss - KS1))
+              flush_v(0, rzo, vzo4, pso, pst[0]);
             if constexpr (s == S31 + 1) {
               pso = zs.at(0);
               zs.next();
-              pst = stg[lane];
+              pst[0] = stg[lane];
             }
-            if constexpr (S31 + 2 < KS1 ? s == S31 + 2 : (ib >= 2 && s == S31 + 2 - KS1))
-              flush_v(0, rzo, vzo4, pso, pst);
           }
           // blocks 2s', 2s'+1 complete (the odd block's last row ran at this step or before)
           if constexpr (((ib - 1) & 1) && s == KS1 - 1) {
@@ -732,7 +739,7 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     });
     // tail: block NB-2's deferred store (if it wrapped), block NB-1 (its Z_{k-1} block rode on
     // the next G2 chunk 0, now slot cur)
-    if constexpr (DF1 && S31 + 2 >= KS1) flush_v(0, rzo, vzo4, pso, pst);
+    if constexpr (DF1 && W::st_step(KS1, 0) >= KS1) flush_v(0, rzo, vzo4, pso, pst[0]);
     float zl[4];
     zread(zreg(cur, 0), zl);
 #pragma unroll
@@ -772,19 +779,18 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
             }
           });
           if constexpr (DF2) {
-            // tile i (E, L, T): stored one step after it was read back (tile i+1 is read in
-            // that same step, after the store consumed pst)
+            // tile i (E, L, T): read back at step S32 + 1 + i, stored X3_SDLY steps later
             static_for<3>([&](auto I_) {
               constexpr int i = decltype(I_)::value;
-              constexpr int ss = S32 + 2 + i;
+              constexpr int ss = W::st_step(KS2, i);
               if constexpr (ss < KS2 ? s == ss : (ib >= 2 && s == ss - KS2))
-                flush_v(1 + i, i == 0 ? O.e : (i == 1 ? O.l : O.t), oo4, pso, pst);
+                flush_v(1 + i, i == 0 ? O.e : (i == 1 ? O.l : O.t), oo4, pso, pst[i]);
               if constexpr (s == S32 + 1 + i) {
                 if constexpr (i == 0) {
                   pso = mw.at(0);
                   mw.next();
                 }
-                pst = stg[(1 + i) * 64 + lane];
+                pst[i] = stg[(1 + i) * 64 + lane];
               }
             });
           }
@@ -794,7 +800,14 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
       });
       qp = acc;
     });
-    if constexpr (DF2 && S32 + 4 >= KS2) flush_v(3, O.t, oo4, pso, pst);  // block MB-2's T
+    // block MB-2's stores that wrapped past the pass
+    if constexpr (DF2) {
+      static_for<3>([&](auto I_) {
+        constexpr int i = decltype(I_)::value;
+        if constexpr (W::st_step(KS2, i) >= KS2)
+          flush_v(1 + i, i == 0 ? O.e : (i == 1 ? O.l : O.t), oo4, pso, pst[i]);
+      });
+    }
     if constexpr (!XE) xv = xs[(w * MB + MB - 1) * 64 + lane];
 #pragma unroll
     for (int r = 0; r < 4; ++r) epi2_row(P, PRO, MB - 1, r, qp[r] * zinv, xv[r]);
