@@ -67,6 +67,26 @@ __device__ __forceinline__ void glds16(const float* sbase, uint32_t voff, f32x4*
       : "memory");
 }
 
+#ifndef DLADMM_DMA4
+#define DLADMM_DMA4 1  // weight chunk DMA: 4 consecutive fragments per wave with one M0 setup
+#endif
+// Four consecutive 1 KiB fragments (sbase + 0..3 KiB -> ldst + 0..3 KiB) by LDS-DMA with one
+// M0 setup: the instruction offset advances the global source and the LDS destination alike
+// (tools/probe/ldsdma_offset.hip).
+__device__ __forceinline__ void glds16x4(const float* sbase, uint32_t voff, const void* ldst) {
+  unsigned keep;
+  const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ldst);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
+      "global_load_lds_dwordx4 %1, %2 offset:1024\n\t"
+      "global_load_lds_dwordx4 %1, %2 offset:2048\n\t"
+      "global_load_lds_dwordx4 %1, %2 offset:3072\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(dst)
+      : "memory");
+}
+
 // 4-byte variant: lane i's dword lands at ldst + 4 i (64 lanes = 256 consecutive bytes).
 __device__ __forceinline__ void glds4(const float* sbase, uint32_t voff, void* ldst) {
   unsigned keep;

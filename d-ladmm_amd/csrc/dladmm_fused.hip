@@ -33,6 +33,9 @@
 #ifndef DLADMM_ABLATE
 #define DLADMM_ABLATE 0  // timing experiments only, see tools/ablate.py
 #endif
+#ifndef DLADMM_CNT
+#define DLADMM_CNT 1  // ring barriers of every variant wait with counted vmcnt (else only V1)
+#endif
 #ifndef DLADMM_CHUNK
 #define DLADMM_CHUNK 16
 #endif
@@ -90,13 +93,14 @@ struct WinCount {
   }
   static constexpr int ops2(int t, bool pro) {
     const int p = t / NB, kb = t % NB;
-    if (p == 0) return (pro ? 0 : rows_in(kb, NB)) + 3 * parts_at(kb);  // G1 rows + prefetch
-    return 6 * rows_in(kb, NB);  // G2 rows (E, L, T stores) + one 3-load prefetch part each
+    constexpr int pf = PKIND == PK_ELEM ? 3 : 0;  // beta loads per prefetch part
+    if (p == 0) return (pro ? 0 : rows_in(kb, NB)) + pf * parts_at(kb);  // G1 rows + prefetch
+    return (3 + pf) * rows_in(kb, NB);  // G2 rows (E, L, T stores) + a prefetch part each
   }
   static constexpr int last1 = (NB / 2) * MB - 1, last2 = (MB / 2) * NB - 1;
   template <int S>
   static constexpr int g1() {
-    if constexpr (PKIND != PK_ELEM || S % SPC != SPC - 1) return 0;
+    if constexpr ((PKIND != PK_ELEM && !DLADMM_CNT) || S % SPC != SPC - 1) return 0;
     int n = 0;
     for (int t = S - SPC; t < S; ++t) {
       if (t >= 0) n += ops1(t);
@@ -106,7 +110,7 @@ struct WinCount {
   }
   template <int S, bool PRO>
   static constexpr int g2() {
-    if constexpr (PKIND != PK_ELEM || S % SPC != SPC - 1) return 0;
+    if constexpr ((PKIND != PK_ELEM && !DLADMM_CNT) || S % SPC != SPC - 1) return 0;
     int n = 0;
     for (int t = S - SPC; t < S; ++t) {
       if (t >= 0) n += ops2(t, PRO);
@@ -172,10 +176,17 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
 #if DLADMM_ABLATE & 1  // timing experiment: no weight stream (WRONG results)
     if (base != a.Ap) return;
 #endif
+    if constexpr (DLADMM_DMA4 && CF % 16 == 0) {
+      // wave w: fragments 16i + 4w .. +3, one M0 setup per 4 KiB
 #pragma unroll
-    for (int i = 0; i < (CF + 3) / 4; ++i) {
-      const int f = i * 4 + w;
-      if (CF % 4 == 0 || f < CF) glds16(base + f * kFrag, lane * 16, dst + f * 64);
+      for (int i = 0; i < CF / 16; ++i)
+        glds16x4(base + (16 * i + 4 * w) * kFrag, lane * 16, dst + (16 * i + 4 * w) * 64);
+    } else {
+#pragma unroll
+      for (int i = 0; i < (CF + 3) / 4; ++i) {
+        const int f = i * 4 + w;
+        if (CF % 4 == 0 || f < CF) glds16(base + f * kFrag, lane * 16, dst + f * 64);
+      }
     }
   };
   auto slot_add = [](int s, int d) -> int { s += d; return s >= 3 ? s - 3 : s; };

@@ -143,22 +143,6 @@ __device__ __forceinline__ void blds16(i32x4 r, uint32_t voff, uint32_t soff, co
       : "v"(voff), "s"(r), "s"(soff), "s"(dst)
       : "memory");
 }
-// Four consecutive 1 KiB fragments (sbase + 0..3 KiB -> ldst + 0..3 KiB) by LDS-DMA with one
-// M0 setup: the instruction offset advances the global source and the LDS destination alike
-// (tools/probe/ldsdma_offset.hip).
-__device__ __forceinline__ void glds16x4(const float* sbase, uint32_t voff, const void* ldst) {
-  unsigned keep;
-  const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ldst);
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, %2\n\t"
-      "global_load_lds_dwordx4 %1, %2 offset:1024\n\t"
-      "global_load_lds_dwordx4 %1, %2 offset:2048\n\t"
-      "global_load_lds_dwordx4 %1, %2 offset:3072\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(sbase), "s"(dst)
-      : "memory");
-}
 // Store cache policy of the output tiles. Measured on the d=15 headline (tools/x3_ablate.py,
 // profiles/r02_x3_ablations.md): default policy 2.58 ms, sc0 2.59, nt 2.72, nt|sc1 2.73. The
 // fp32 kernels keep DLADMM_STORE_AUX (nt); here the full-line dwordx4 stores merge in L2 anyway.

@@ -59,11 +59,16 @@ __device__ __forceinline__ void slice_gemm(f32x4* ring, const float* Wp, int MBp
     asm volatile("" : "+s"(sb));
     const float* base = (const float*)sb;
     f32x4* dst = ring + slot * (CF * 64);
+#if DLADMM_DMA4
+    // wave w: the chunk's fragments 4w .. 4w+3 (contiguous 4 KiB), one M0 setup
+    glds16x4(base + 4 * w * kFrag, lane * 16, dst + 4 * w * 64);
+#else
 #pragma unroll
     for (int i = 0; i < WPW; ++i) {
       const int f = i * NW + w;
       glds16(base + f * kFrag, lane * 16, dst + f * 64);
     }
+#endif
   };
   // B DMA lanes: column (l >> 2) of this wave's 16, row offset (l & 3) within each group of 4
   const int64_t colD = (int64_t)blockIdx.x * (16 * NW) + w * 16 + (lane >> 2);
