@@ -177,7 +177,26 @@ def main():
     if a.precision == "f32" and m <= 256 and n <= 512 and B % 4 == 0 and \
             os.environ.get("DLADMM_PATH", "")[:1] != "l" and not a.no_split:
         s_el, s_kern, s_obj = timed("f32_split")
-        split = (s_el, s_kern, float(s_obj.cpu().numpy()[-1]))
+        # untimed: per-layer norm-relative distance of the split path's Z/E/L/T from the fp32
+        # path's on this whole batch (max over layers and outputs)
+        with torch.no_grad():
+            net.precision = "f32"
+            rf = net.run(X, keep_all=keep_all, loss_kind=lk)
+            net.precision = "f32_split"
+            rs = net.run(X, keep_all=keep_all, loss_kind=lk)
+            dev_max = 0.0
+            for name in ("Z", "E", "L", "T"):
+                tf, ts = getattr(rf, name), getattr(rs, name)
+                if tf is None:
+                    continue
+                for k in range(tf.shape[0]):
+                    nf = torch.linalg.vector_norm(tf[k].double())
+                    if nf > 0:
+                        d = torch.linalg.vector_norm((ts[k] - tf[k]).double()) / nf
+                        dev_max = max(dev_max, float(d))
+            del rf, rs
+            net.precision = a.precision
+        split = (s_el, s_kern, float(s_obj.cpu().numpy()[-1]), dev_max)
     obj = obj.cpu().numpy()
 
     if rank == 0:
@@ -253,7 +272,7 @@ def main():
             "objective_last_layer": float(obj[-1]),
         }
         if split is not None:
-            s_el, s_kern, s_objl = split
+            s_el, s_kern, s_objl, s_dev = split
             s_peak = PEAK_BF16_MFMA / 3
             res["split_f16"] = {
                 "precision": "f32_split",
@@ -270,6 +289,9 @@ def main():
                                   "peak_note": "dense f16 MFMA peak / 3 products"},
                 "hbm_frac_algorithmic": bytes_launch / s_kern / PEAK_HBM,
                 "objective_last_layer": s_objl,
+                "max_rel_dev_vs_f32": s_dev,
+                "max_rel_dev_note": "max over layers of ||X_split - X_f32|| / ||X_f32|| for X in "
+                                    "Z, E, L, T on this batch (parity tolerance: 1e-5)",
             }
         if world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(m, n, K, a.cpu_batch, a.variant)

@@ -375,6 +375,16 @@ inline hipError_t pack(const float* const* srcs, int T, int R, int C, int64_t ld
   return hipSuccess;
 }
 
+// Device address of the per-wave cycle-sum buffer of the diagnostic stamp builds
+// (DLADMM_DBG_PTR, set by tools/x3_stamp.py); read once.  Regular builds never write it.
+inline unsigned long long* dbg_ptr() {
+  static unsigned long long* const p = [] {
+    const char* e = getenv("DLADMM_DBG_PTR");
+    return e ? (unsigned long long*)strtoull(e, nullptr, 0) : nullptr;
+  }();
+  return p;
+}
+
 inline int run_fused(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStream_t s) {
   float* Ap = (float*)(ws + p.off_ap);
   float* Wp = (float*)(ws + p.off_wp);
@@ -405,6 +415,7 @@ inline int run_fused(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStrea
     for (int k = 0; k < d->layers; ++k) { a.b1e[k] = d->beta1_elem[k]; a.b2e[k] = d->beta2_elem[k]; }
   a.Zo = d->Z; a.Eo = d->E; a.Lo = d->L; a.To = d->T; a.ldo = d->ld_out;
   a.lossp = lossp;
+  a.dbg = dbg_ptr();  // diagnostic builds (DLADMM_STAMP) write per-wave cycle sums here
   if (d->ev_kernel_start) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_start, s)) return (int)e;
   }
@@ -464,11 +475,7 @@ inline int run_fused_x3(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipSt
   a.lossp = (float*)(ws + p.off_loss);
   a.wexp = wexp;
   a.Zw = (float*)(ws + p.off_zw); a.ldzw = p.ldzw;
-  static unsigned long long* const dbg = [] {  // diagnostic builds (X3_STAMP) write here
-    const char* e = getenv("DLADMM_DBG_PTR");
-    return e ? (unsigned long long*)strtoull(e, nullptr, 0) : nullptr;
-  }();
-  a.dbg = dbg;
+  a.dbg = dbg_ptr();  // diagnostic builds (X3_STAMP) write per-wave cycle sums here
   if (d->ev_kernel_start) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_start, s)) return (int)e;
   }

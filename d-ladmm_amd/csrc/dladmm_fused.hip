@@ -33,6 +33,9 @@
 #ifndef DLADMM_ABLATE
 #define DLADMM_ABLATE 0  // timing experiments only, see tools/ablate.py
 #endif
+#ifndef DLADMM_STAMP
+#define DLADMM_STAMP 0  // diagnostic build: per-wave cycle sums of the passes and ring barriers
+#endif
 #ifndef DLADMM_CNT
 #define DLADMM_CNT 1  // ring barriers of every variant wait with counted vmcnt (else only V1)
 #endif
@@ -419,7 +422,17 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   // pins that order.  fr[] rotates over 4 registers (2 steps x 2 fragments).
   f32x4 fr[4];
   // WIN = VM operations (stores, V1 beta loads) definitely issued since the awaited chunk's DMA
-  // (PK_ELEM only, see window_ops): they stay in flight across the barrier
+  // (WinCount): they stay in flight across the barrier
+#if DLADMM_STAMP
+  // diagnostic build: per-wave cycle sums (read the shares, not this build's run time)
+  auto stamp = []() -> uint64_t {
+    uint64_t v;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");
+    return v;
+  };
+  uint64_t st_vm = 0, st_bar = 0, st_g1 = 0, st_g2 = 0;
+  const uint64_t st_0 = stamp();
+#endif
   auto step_head = [&](auto S_, int gi, auto WIN_) {
     constexpr int s = decltype(S_)::value;
     constexpr int WIN = decltype(WIN_)::value;
@@ -429,8 +442,20 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
       fr[(fi + 3) % 4] = frag(cur, fc + 3);
     } else {
       // chunk ch+1 landed for every wave; every wave is done with chunk ch-1
+#if DLADMM_STAMP
+      __builtin_amdgcn_sched_barrier(0);
+      const uint64_t t0 = stamp();
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(WIN) : "memory");
+      const uint64_t t1 = stamp();
+      asm volatile("s_barrier" ::: "memory");
+      const uint64_t t2 = stamp();
+      __builtin_amdgcn_sched_barrier(0);
+      st_vm += t1 - t0;
+      st_bar += t2 - t1;
+#else
       if constexpr (WIN > 0) ring_barrier_cnt<WIN>();
       else ring_barrier();
+#endif
       issue(chunk_src(gi, ch + 2), slot_add(cur, 2));
       const int nx = slot_add(cur, 1);
       fr[(fi + 2) % 4] = frag(nx, 0);
@@ -568,12 +593,28 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     const LayerP P = layer_params(k);
     // outputs of layer k; num_records 0 = not stored
     const rsrc_t rzo = mkrsrc(a.Zo + (int64_t)ko * n * a.ldo, st ? zbytes : 0u);
+#if DLADMM_STAMP
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t ta = stamp();
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     g1_pass(k, P, rzo, Pp, Op);
+#if DLADMM_STAMP
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t tb = stamp();
+    __builtin_amdgcn_sched_barrier(0);
+    st_g1 += tb - ta;
+#endif
     const OutR O{mkrsrc(a.Eo + (int64_t)ko * m * a.ldo, st ? mbytes : 0u),
                  mkrsrc(a.Lo + (int64_t)ko * m * a.ldo, st ? mbytes : 0u),
                  mkrsrc(a.To ? a.To + (int64_t)(a.keep_all ? k + 1 : 0) * m * a.ldo : nullptr,
                         (a.To && st) ? mbytes : 0u)};
     g2_pass(std::false_type{}, k, P, O, rzo);
+#if DLADMM_STAMP
+    __builtin_amdgcn_sched_barrier(0);
+    st_g2 += stamp() - tb;
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     Pp = P;
     Op = O;
   }
@@ -586,6 +627,16 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   flush_loss(K - 1);
   // drain: the ring's last LDS-DMA must land before the workgroup's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if DLADMM_STAMP
+  const uint64_t st_end = stamp();
+  if (a.dbg && lane < 8) {  // vector stores: lane i writes sum i
+    const uint64_t v[8] = {st_end - st_0, st_g1, st_g2, 0, st_vm, st_bar, 0, 0};
+    uint64_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x = lane == i ? v[i] : x;
+    a.dbg[((int64_t)blockIdx.x * kWaves + w) * 8 + lane] = x;
+  }
+#endif
 }
 
 

@@ -54,6 +54,9 @@
 #define X3_OFF 0  // A/B knob: 1 immediate tile stores, 2 Z_{k-1} block read at the chunk start,
                   // 4 X rows read at the block start (the earlier schedules; correct results)
 #endif
+#ifndef X3_BAR2
+#define X3_BAR2 0  // one ring barrier per two chunks (each refills two slots)
+#endif
 #ifndef X3_SDLY
 #define X3_SDLY 2  // deferred tile stores: steps between the read-back and the store
 #endif
@@ -249,6 +252,17 @@ struct Win {
     }
     return n < 63 ? n : 63;
   }
+  // X3_BAR2: a barrier every other chunk (odd ch) waits for chunks ch+1 and ch+2, issued (in
+  // that order) at the barrier two chunks earlier; younger: the bodies of the 2*SPC steps since
+  template <int T, bool G1>
+  static constexpr int win2() {
+    int n = 0;
+    for (int u = T - 2 * SPC; u < T; ++u) {
+      if (u >= 0) n += G1 ? ops1(u) : ops2(u);
+      else if (ST + u >= 0) n += G1 ? ops2(ST + u) : ops1(ST + u);
+    }
+    return n < 63 ? n : 63;
+  }
 };
 
 }  // namespace x3
@@ -266,6 +280,7 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
   // the DMA group issued at a barrier targets the chunk 4 ahead: it must lie in this pass or the
   // next (the Z blocks a G1 chunk carries are only complete one pass ahead)
   static_assert(NCH >= kSlots, "at least kSlots chunks per pass");
+  static_assert(!X3_BAR2 || (kSlots == 4 && NCH % 2 == 0), "paired barriers: 4 slots, even NCH");
 #ifndef X3_ROT
 #define X3_ROT 4
 #endif
@@ -588,15 +603,20 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     } else {
       // every wave has read all of chunk ch (its last fragments D steps ago, its Z blocks at
       // the chunk's first step)
-      if constexpr (c + D == SPC) {
+      // X3_BAR2: barriers at odd chunks only, each refilling two slots
+      constexpr bool BAR = !X3_BAR2 || ch % 2 == 1;
+      constexpr int WN = (X3_ABL & 128) ? 63
+                         : X3_BAR2     ? W::template win2<t, G1>()
+                                       : W::template win<t, G1>();
+      if constexpr (c + D == SPC && BAR) {
         if constexpr (X3_ABL & 256) {
-          if constexpr (X3_ABL & 512) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((X3_ABL & 128) ? 63 : W::template win<t, G1>()) : "memory");
-          else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((X3_ABL & 128) ? 63 : W::template win<t, G1>()) : "memory");
+          if constexpr (X3_ABL & 512) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WN) : "memory");
+          else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(WN) : "memory");
         } else {
 #if X3_STAMP
           __builtin_amdgcn_sched_barrier(0);
           const uint64_t t0 = stamp();
-          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(W::template win<t, G1>()) : "memory");
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(WN) : "memory");
           const uint64_t t1 = stamp();
           asm volatile("s_barrier" ::: "memory");
           const uint64_t t2 = stamp();
@@ -604,10 +624,16 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
           st_vm += t1 - t0;
           st_bar += t2 - t1;
 #else
-          ring_barrier_cnt<(X3_ABL & 128) ? 63 : W::template win<t, G1>()>();
+          ring_barrier_cnt<WN>();
 #endif
         }
-        issue(G1_, std::integral_constant<int, ch + kSlots>{}, gi, cur);
+        if constexpr (X3_BAR2) {
+          // slots of chunks ch-1 and ch are free: chunks ch+3, ch+4
+          issue(G1_, std::integral_constant<int, ch + 3>{}, gi, slot_add(cur, kSlots - 1));
+          issue(G1_, std::integral_constant<int, ch + 4>{}, gi, cur);
+        } else {
+          issue(G1_, std::integral_constant<int, ch + kSlots>{}, gi, cur);
+        }
       }
       const int nx = slot_add(cur, 1);
       frh[tn % R] = frag(nx, 2 * (c + D - SPC));

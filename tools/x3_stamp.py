@@ -1,7 +1,9 @@
-"""Per-wave cycle shares of the split-f16 kernel from its diagnostic stamp build (X3_STAMP=1).
+"""Per-wave cycle shares of a fused forward kernel from its diagnostic stamp build.
 
-    python tools/x3_ablate.py X3_STAMP=1                                    # build (CPU)
+    python tools/x3_ablate.py X3_STAMP=1                                    # split-f16 (CPU)
     DLADMM_LIB=d-ladmm_amd/lib/abl/libdladmm_hip_x3ablX3_STAMP1.so python tools/x3_stamp.py
+    python tools/ablate.py stamp=-DDLADMM_STAMP=1                           # fp32 kernel
+    DLADMM_LIB=d-ladmm_amd/lib/abl/stamp/libdladmm_hip.so python tools/x3_stamp.py f32
 
 Runs the headline workload (V4, m=256, n=512, K=15, B=65536, all layers written) a few times
 and prints the mean over waves of: total cycles, G1 passes, G2 passes, between passes, ring
@@ -27,7 +29,7 @@ def main():
     dl = importlib.import_module("d-ladmm_amd")
     A, X, Z0, E0, L0 = bench.synth(m, n, B, 0, dev)
     net = dl.DLADMMNetScalar(m=m, n=0, d=n, batch_size=B, A=A, Z0=Z0, E0=E0, L0=L0, layers=K)
-    net.precision = "f32_split"
+    net.precision = sys.argv[1] if len(sys.argv) > 1 else "f32_split"
     net.requires_grad_(False)
     with torch.no_grad():
         for _ in range(3):
