@@ -33,6 +33,9 @@
 #ifndef DLADMM_ABLATE
 #define DLADMM_ABLATE 0  // timing experiments only, see tools/ablate.py
 #endif
+#ifndef DLADMM_ABL_AUX
+#define DLADMM_ABL_AUX 0
+#endif
 #ifndef DLADMM_STAMP
 #define DLADMM_STAMP 0  // diagnostic build: per-wave cycle sums of the passes and ring barriers
 #endif
@@ -282,6 +285,16 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   SWalk zw{0u, (uint32_t)(a.ldo * 4)}, mw{0u, (uint32_t)(a.ldo * 4)};
   SWalk bw{0u, (uint32_t)(a.ldb * 4)};
 
+#if DLADMM_ABLATE & 16
+  float abq[4][4];
+  const int64_t c4 = (int64_t)blockIdx.x * kTileCols + w * 16 + 4 * (lane & 3);
+  const uint32_t vo4 = c4 < a.B ? (uint32_t)(((lane >> 2) * a.ldo + c4) * 4) : kOOB;
+  auto st4 = [&](rsrc_t r, uint32_t soff, const float (&v)[4]) {
+    const f32x4 x = {v[0], v[1], v[2], v[3]};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int __attribute__((ext_vector_type(4))), x),
+                                           r, (int)vo4, (int)soff, DLADMM_ABL_AUX);
+  };
+#endif
   // ---------------------------------------------------------------- per-row epilogues
   // G1 block b, row r of layer k: Z = S(Z - s1*(W_k Var), theta_z)  main_lena.py:86 / tied :114
   // (q = -W_k Var: the chain ran on the negated packed weights, so Z + s1*q is the reference's
@@ -299,7 +312,12 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     }
     Zr[b][r] = z;
     pin_agpr(Zr[b][r]);
+#if DLADMM_ABLATE & 16  // timing experiment: one dwordx4 store per block, same bytes (WRONG data)
+    abq[0][r] = z;
+    if (r == 3) st4(rzo, zw.at(0), abq[0]);
+#else
     bstore_s(rzo, vo, zw.at(r), z);
+#endif
     // no column mask: padded columns hold exactly zero state (X = Z0 = E0 = L0 = 0)
     regsum += fabsf(z);
     if (r == 3) zw.next();
@@ -354,10 +372,19 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     l = pro ? l0 : l;
     if constexpr (kEState) Er[b][r] = e;
     Lr[b][r] = l;
+#if DLADMM_ABLATE & 16
+    abq[1][r] = e; abq[2][r] = l; abq[3][r] = t;
+    if (r == 3) {
+      st4(O.e, mw.at(0), abq[1]);
+      st4(O.l, mw.at(0), abq[2]);
+      st4(O.t, mw.at(0), abq[3]);
+    }
+#else
     const uint32_t so = mw.at(r);
     bstore_s(O.e, vo, so, e);
     bstore_s(O.l, vo, so, l);
     bstore_s(O.t, vo, so, t);
+#endif
     const float res = x - Pv;
     fit1 += fabsf(res);                                      // |X - A Z|
     fit2 = __builtin_fmaf(res, res, fit2);                   // (X - A Z)^2

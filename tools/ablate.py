@@ -5,7 +5,8 @@
 Each variant recompiles dladmm_fused.hip with the extra flags and links it with the regular
 capi/layered objects into d-ladmm_amd/lib/abl/<name>/libdladmm_hip.so.  Time one with
     DLADMM_LIB=d-ladmm_amd/lib/abl/<name>/libdladmm_hip.so python bench.py --no-cpu-baseline
-Knobs: DLADMM_ABLATE (1 = no weight stream, 2 = no epilogue, 8 = no V1 beta loads),
+Knobs: DLADMM_ABLATE (1 = no weight stream, 2 = no epilogue, 8 = no V1 beta loads, 16 = one
+dwordx4 store per block with the same bytes; DLADMM_ABL_AUX its cache policy),
 DLADMM_ABLATE_NOSTORE, DLADMM_SYNC_MODE, DLADMM_CHUNK.
 """
 import os
