@@ -509,7 +509,11 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
   // reference's fc(Var) (s1 * fc(Var)) up to the GEMM's rounding, so the fma is one rounding of
   // Z_{k-1} - fc(Var) like the reference's subtraction
   auto epi1_row = [&](const LayerP& P, int b, int r, float zp, float acc, float qs) {
-    if constexpr (X3_ABL & 2) { zn[b & 1][r] = acc; return; }
+    if constexpr (X3_ABL & 2) {  // keep the MFMA chain alive
+      zn[b & 1][r] = acc;
+      asm volatile("" ::"v"(acc));
+      return;
+    }
     float u;
     if constexpr (PKIND == PK_S1) u = zp + acc * qs;
     else u = __builtin_fmaf(acc, qs, zp);
@@ -531,7 +535,12 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
   };
   float vmx = 0.f;
   auto epi2_row = [&](const LayerP& P, bool pro, int b, int r, float Pv, float x) {
-    if constexpr (X3_ABL & 2) { Vr[b][r] = Pv; pin_agpr(Vr[b][r]); return; }
+    if constexpr (X3_ABL & 2) {
+      Vr[b][r] = Pv;
+      pin_agpr(Vr[b][r]);
+      asm volatile("" ::"v"(Pv));
+      return;
+    }
     const float l0 = Lr[b][r];
     const float e0 = Er[b][r];
     float e;
