@@ -39,6 +39,10 @@
 #ifndef DLADMM_STAMP
 #define DLADMM_STAMP 0  // diagnostic build: per-wave cycle sums of the passes and ring barriers
 #endif
+#ifndef DLADMM_SLOTS
+#define DLADMM_SLOTS 4  // weight ring slots (chunks in flight: slots - 1); the per-row kinds
+                        // (their parameter tables take 24 KiB of LDS) use at most 4
+#endif
 #ifndef DLADMM_CNT
 #define DLADMM_CNT 1  // ring barriers of every variant wait with counted vmcnt (else only V1)
 #endif
@@ -57,7 +61,9 @@ struct Fused {
   static constexpr int NCH = GF / CF;               // chunks per GEMM
   static constexpr int TAB = ((6 * MP + NP + 63) / 64) * 64;  // per-row param table (floats,
                                                               // whole 64-entry DMA pieces)
-  static constexpr int RING_F4 = 3 * CF * 64;       // 3 slots
+  static constexpr int SLOTS = (PKIND == PK_ROW && DLADMM_SLOTS > 4) ? 4 : DLADMM_SLOTS;
+  static constexpr int RING_F4 = SLOTS * CF * 64;  // ring slots of CF fragments
+  static_assert(SLOTS >= 3, "the ring needs one slot being read, one landed, one in flight");
   static constexpr int TAB_F4 = (PKIND == PK_ROW) ? (3 * TAB) / 4 : 0;  // 3 layer buffers
   static constexpr int X_F4 = kWaves * MB * 64;     // the tile's X, resident in LDS
   static_assert(MB % 2 == 0 && NB % 2 == 0, "output blocks are processed in pairs");
@@ -103,24 +109,34 @@ struct WinCount {
     if (p == 0) return (pro ? 0 : rows_in(kb, NB)) + pf * parts_at(kb);  // G1 rows + prefetch
     return (3 + pf) * rows_in(kb, NB);  // G2 rows (E, L, T stores) + a prefetch part each
   }
-  static constexpr int last1 = (NB / 2) * MB - 1, last2 = (MB / 2) * NB - 1;
+  static constexpr int T1 = (NB / 2) * MB, T2 = (MB / 2) * NB;  // steps of a G1 / G2 pass
+  // With S slots the awaited chunk's DMA was issued S-2 barriers back: the bodies of the
+  // (S-2)*SPC steps since and the DMA groups of the S-3 chunks issued after it are newer.  A
+  // step before the pass counts with the previous pass's schedule (the smaller of the two
+  // possible previous passes before G1; nothing before the prologue).
+  static constexpr int SLOTS = (PKIND == PK_ROW && DLADMM_SLOTS > 4) ? 4 : DLADMM_SLOTS;
+  static constexpr int WSTEPS = (SLOTS - 2) * SPC;
+  static constexpr int DMAG = (SLOTS - 3) * ((CF + 3) / 4);
   template <int S>
   static constexpr int g1() {
     if constexpr ((PKIND != PK_ELEM && !DLADMM_CNT) || S % SPC != SPC - 1) return 0;
-    int n = 0;
-    for (int t = S - SPC; t < S; ++t) {
+    int n = DMAG;
+    for (int t = S - WSTEPS; t < S; ++t) {
       if (t >= 0) n += ops1(t);
-      else n += ops2(last2, true) < ops2(last2, false) ? ops2(last2, true) : ops2(last2, false);
+      else if (T2 + t >= 0) {
+        const int a = ops2(T2 + t, true), b = ops2(T2 + t, false);
+        n += a < b ? a : b;
+      }
     }
     return n < 63 ? n : 63;
   }
   template <int S, bool PRO>
   static constexpr int g2() {
     if constexpr ((PKIND != PK_ELEM && !DLADMM_CNT) || S % SPC != SPC - 1) return 0;
-    int n = 0;
-    for (int t = S - SPC; t < S; ++t) {
+    int n = DMAG;
+    for (int t = S - WSTEPS; t < S; ++t) {
       if (t >= 0) n += ops2(t, PRO);
-      else n += PRO ? 0 : ops1(last1);
+      else if (!PRO && T1 + t >= 0) n += ops1(T1 + t);
     }
     return n < 63 ? n : 63;
   }
@@ -195,7 +211,10 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
       }
     }
   };
-  auto slot_add = [](int s, int d) -> int { s += d; return s >= 3 ? s - 3 : s; };
+  auto slot_add = [](int s, int d) -> int {
+    s += d;
+    return s >= F::SLOTS ? s - F::SLOTS : s;
+  };
   int cur = 0;  // ring slot of the chunk being consumed
   auto frag = [&](int slot, int fc) -> f32x4 { return ring[(slot * CF + fc) * 64 + lane]; };
 
@@ -483,7 +502,7 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
       if constexpr (WIN > 0) ring_barrier_cnt<WIN>();
       else ring_barrier();
 #endif
-      issue(chunk_src(gi, ch + 2), slot_add(cur, 2));
+      issue(chunk_src(gi, ch + F::SLOTS - 1), slot_add(cur, F::SLOTS - 1));
       const int nx = slot_add(cur, 1);
       fr[(fi + 2) % 4] = frag(nx, 0);
       fr[(fi + 3) % 4] = frag(nx, 1);
@@ -496,9 +515,9 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     if constexpr (fc + 2 >= CF) cur = slot_add(cur, 1);
   };
 
-  // prime the ring: chunks 0 and 1, then the first step's fragments
-  issue(chunk_src(0, 0), 0);
-  issue(chunk_src(0, 1), 1);
+  // prime the ring: the first SLOTS - 1 chunks, then the first step's fragments
+#pragma unroll
+  for (int c = 0; c < F::SLOTS - 1; ++c) issue(chunk_src(0, c), c);
   ring_barrier();
   fr[0] = frag(0, 0);
   fr[1] = frag(0, 1);
