@@ -10,6 +10,7 @@ namespace dladmm {
 
 // ------------------------------------------------------------------------ weight packing
 constexpr int kPackBatch = 64;  // sources per pack launch (the struct is a kernel argument)
+constexpr bool kBf16NarrowDefault = true;  // bf16 tiles: 128 columns (2 % faster at config 5)
 
 struct PackArgs {
   const float* src[kPackBatch];
@@ -209,6 +210,7 @@ struct Plan {
   int nslots;  // loss partials per (layer, term): slices x ldl per-column entries
   int ldl;     // columns per slice
   int nbp;     // bf16 path: 16-column blocks of the packed state
+  bool narrow;  // bf16 path: 128-column tiles (two workgroups per CU)
   size_t off_ap, off_wp, off_v, off_zb, off_zw, off_ew, off_lw, off_loss, total;
   size_t off_wexp, off_umax;  // path 4
   int64_t ldzw;               // path 4: lean-mode Z_k workspace row stride
@@ -334,7 +336,10 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
   p->MBp2 = ceil_div(MB, p->SB2) * p->SB2;
   p->slices1 = p->MBp1 / p->SB1;
   p->slices2 = p->MBp2 / p->SB2;
-  const int cols = bf16 ? kBf16TileCols : kLayerCols;
+  // bf16 tile width: DLADMM_BF16_TILE=wide|narrow (A/B measurements), default below
+  const char* tw = getenv("DLADMM_BF16_TILE");
+  p->narrow = bf16 && (tw ? tw[0] == 'n' : kBf16NarrowDefault);
+  const int cols = bf16 ? bf16_tile_cols(p->narrow) : kLayerCols;
   p->gx = ceil_div(d->batch, cols);
   p->ldl = p->gx * cols;
   p->nbp = p->ldl / 16;
@@ -502,7 +507,7 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
   char* Vb = ws + p.off_v;   // bf16: packed Var_k (B operand of G1)
   char* Zb = ws + p.off_zb;  // bf16: packed Z_k / Z0 (B operand of G2)
   auto launch = [&](int phase, const LayerArgs& la, dim3 grid, int sb) -> hipError_t {
-    return bf ? launch_tile_bf16(phase, d->variant, la, grid, s)
+    return bf ? launch_tile_bf16(phase, d->variant, p.narrow, la, grid, s)
               : launch_layer(phase, d->variant, la, grid, sb, s);
   };
   // 1. pack A (rows m, contraction n) and every W_k (rows n, contraction m), k-major

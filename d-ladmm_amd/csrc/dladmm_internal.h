@@ -92,12 +92,15 @@ hipError_t launch_layer(int phase, int variant, const LayerArgs& a, dim3 grid, i
                         hipStream_t s);
 
 // ---- bf16 2-D tile kernels (dladmm_tile_bf16.hip), BASELINE config 5
-// A workgroup of 8 waves owns a 256 x 256 output tile (16 row blocks x 16 column blocks); both
-// operands are packed bf16 fragments streamed by LDS-DMA through a 4-stage ring.
-constexpr int kTileWaves = 8;
-constexpr int kTileBlocks = 16;                 // row and column blocks per tile
-constexpr int kBf16TileCols = 16 * kTileBlocks;  // batch columns per tile
-hipError_t launch_tile_bf16(int phase, int variant, const LayerArgs& a, dim3 grid, hipStream_t s);
+// A workgroup owns a 256-row output tile (16 row blocks); both operands are packed bf16
+// fragments streamed by LDS-DMA through a ring.  Two widths (wave tile 128 x 64 either way):
+//   wide   8 waves, 256 columns, 4-stage ring (128 KiB): one workgroup per CU;
+//   narrow 4 waves, 128 columns, 3-stage ring (72 KiB): two workgroups per CU, so one
+//          workgroup's HBM-bound epilogue runs beside the other's MFMA main loop.
+constexpr int kTileBlocks = 16;                 // row blocks per tile
+constexpr int bf16_tile_cols(bool narrow) { return narrow ? 128 : 256; }
+hipError_t launch_tile_bf16(int phase, int variant, bool narrow, const LayerArgs& a, dim3 grid,
+                            hipStream_t s);
 // Z0 [rows][ld] fp32 -> packed bf16 B operand [KB][nbp] (RNE, zero padding)
 hipError_t pack_state_bf16(const float* S, int64_t ld, int rows, int64_t cols, int KB, int nbp,
                            void* out, hipStream_t s);

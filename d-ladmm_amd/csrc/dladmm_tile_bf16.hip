@@ -13,12 +13,15 @@
 //     the state is packed by the PREVIOUS product's epilogue, which writes its output both as
 //     the fp32 tensor the API returns (Z_k) and as the next product's bf16 B operand (Z_k or
 //     Var_{k+1}) -- Var itself is never stored in fp32.
-//   * a workgroup of 8 waves owns a 256 x 256 output tile; wave (wr, wc) = (w >> 2, w & 3) owns
-//     128 rows x 64 columns = 8 x 4 accumulator blocks, so per k-block of 32 it reads 12
-//     fragments and issues 32 MFMAs (96 KiB of LDS reads per CU per 1024 MFMA cycles).
-//   * a stage (one k-block: 16 A + 16 B fragments = 32 KiB) is LDS-DMA'd by the 8 waves, 4
-//     fragments each; 4 stages are in the ring (128 KiB, one workgroup per CU), waited with a
-//     COUNTED vmcnt so two stages stay in flight across every barrier.
+//   * a workgroup owns a 256-row output tile; every wave owns 128 rows x 64 columns = 8 x 4
+//     accumulator blocks, so per k-block of 32 it reads 12 fragments and issues 32 MFMAs (96 KiB
+//     of LDS reads per CU per 1024 MFMA cycles).  Two widths (TileG):
+//       - wide: 8 waves, 256 columns; a stage (one k-block: 16 A + 16 B fragments = 32 KiB) is
+//         LDS-DMA'd 4 fragments per wave, 4 stages in the ring (128 KiB, one workgroup per CU);
+//       - narrow: 4 waves, 128 columns; 16 A + 8 B fragments = 24 KiB per stage, 6 per wave, 3
+//         stages (72 KiB), two workgroups per CU: while one streams its epilogue to HBM the
+//         other's main loop keeps the matrix cores busy;
+//     the ring barrier waits with a COUNTED vmcnt so the younger stages stay in flight.
 // Every output block is one accumulation chain over k-blocks in order, on the same packed
 // operands (weights RNE-rounded, state RNE-rounded) as the restated bf16 oracle.
 #include "dladmm_common.h"
@@ -31,35 +34,50 @@
 
 namespace dladmm {
 
-constexpr int kTileStages = 4;
-constexpr int kStageFrags = 2 * kTileBlocks;  // 16 A + 16 B fragments per stage (32 KiB)
-constexpr int kWaveRB = 8, kWaveCB = 4;       // blocks per wave: 128 rows x 64 columns
-static_assert(kTileWaves == 8 && kStageFrags == 4 * kTileWaves, "4 fragments per wave per stage");
-static_assert(2 * kWaveRB == kTileBlocks && 4 * kWaveCB == kTileBlocks, "2 x 4 wave grid");
+// Tile geometry by workgroup width NW (8 waves: 256 columns, 4: 128 columns).  Every wave owns
+// 128 rows x 64 columns; a stage is one k-block of the tile's 16 A and NW/2*4 B fragments, each
+// wave LDS-DMAs FPW of them; the ring holds NST stages and the barrier's counted vmcnt keeps the
+// NST - 2 stages issued after the awaited one in flight.
+template <int NW>
+struct TileG {
+  static constexpr int NWC = NW / 2;                // wave columns (2 wave rows)
+  static constexpr int CBT = 4 * NWC;               // column blocks per tile
+  static constexpr int SF = kTileBlocks + CBT;      // fragments per stage
+  static constexpr int FPW = SF / NW;               // fragments per wave per stage
+  static constexpr int NST = NW == 8 ? 4 : 3;       // ring stages (128 KiB / 72 KiB)
+  static constexpr int VMC = FPW * (NST - 2);       // younger DMA pieces at the barrier
+  static constexpr int H1 = FPW / 2;                // pieces issued before the first MFMA half
+  static_assert(SF % NW == 0 && FPW % 2 == 0, "even share of every stage per wave");
+  static_assert(NST * SF * 1024 <= (NW == 8 ? 160 : 80) * 1024, "LDS: 1 (8 waves) / 2 per CU");
+};
+constexpr int kWaveRB = 8, kWaveCB = 4;  // blocks per wave: 128 rows x 64 columns
+static_assert(2 * kWaveRB == kTileBlocks, "2 wave rows");
 
-template <int EMODE, int PKIND, int PH>
-__global__ __launch_bounds__(kTileWaves * 64, 1) void tile_bf16_kernel(const LayerArgs a) {
-  __shared__ f32x4 ring[kTileStages * kStageFrags * 64];  // 128 KiB
+template <int EMODE, int PKIND, int PH, int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void tile_bf16_kernel(const LayerArgs a) {
+  using G = TileG<NW>;
+  constexpr int SF = G::SF, FPW = G::FPW, NST = G::NST;
+  __shared__ f32x4 ring[NST * SF * 64];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = w >> 2, wc = w & 3;
+  const int wr = w / G::NWC, wc = w % G::NWC;
   const int g = lane >> 4;
   const int ib0 = blockIdx.y * kTileBlocks;  // first output row block of the tile
-  const int cb0 = blockIdx.x * kTileBlocks;  // first column block
+  const int cb0 = blockIdx.x * G::CBT;       // first column block
   const int KB = a.KB;
 
-  // wave w DMAs fragments 4w .. 4w+3 of every stage: waves 0-3 the weights' row blocks
-  // ib0 + 4w .., waves 4-7 the state's column blocks cb0 + 4(w - 4) ..
-  const float* src0 = w < 4 ? a.Wp + (int64_t)(ib0 + 4 * w) * kFrag
-                            : a.S + (int64_t)(cb0 + 4 * (w - 4)) * kFrag;
-  const int64_t kstride = (int64_t)(w < 4 ? a.MBp : a.nbp) * kFrag;  // floats per k-block
-  // piece q (0..3) of this wave's share of stage kb
+  // piece q (0..FPW-1) of wave w is stage fragment f = FPW w + q: f < 16 the weights' row block
+  // ib0 + f, else the state's column block cb0 + f - 16 (wave-uniform either way)
   auto issue = [&](int kb, int slot, int q) {
-    uint64_t sb = (uint64_t)(src0 + kb * kstride + q * kFrag);
+    const int f = FPW * w + q;
+    const float* src = f < kTileBlocks
+        ? a.Wp + ((int64_t)kb * a.MBp + ib0 + f) * kFrag
+        : a.S + ((int64_t)kb * a.nbp + cb0 + f - kTileBlocks) * kFrag;
+    uint64_t sb = (uint64_t)src;
     asm volatile("" : "+s"(sb));
-    glds16((const float*)sb, lane * 16, ring + (slot * kStageFrags + 4 * w + q) * 64);
+    glds16((const float*)sb, lane * 16, ring + (slot * SF + f) * 64);
   };
 
   f32x4 acc[kWaveRB][kWaveCB];
@@ -68,18 +86,20 @@ __global__ __launch_bounds__(kTileWaves * 64, 1) void tile_bf16_kernel(const Lay
 #pragma unroll
     for (int j = 0; j < kWaveCB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: stages 0, 1, 2 (past the end: re-read k-block 0, never consumed)
+  // prologue: stages 0 .. NST-2 (past the end: re-read k-block 0, never consumed)
 #pragma unroll
-  for (int st = 0; st < kTileStages - 1; ++st)
+  for (int st = 0; st < NST - 1; ++st)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) issue(KB > st ? st : 0, st, q);
+    for (int q = 0; q < FPW; ++q) issue(KB > st ? st : 0, st, q);
+  int slot = 0;                 // ring slot of stage kb
+  int nslot = NST - 1;          // slot of stage kb + NST - 1 (= the slot of stage kb - 1)
   for (int kb = 0; kb < KB; ++kb) {
-    // this wave's pieces of stage kb have landed (the 8 DMAs of stages kb+1, kb+2 may still be
-    // in flight), every wave is past its reads of stage kb-1; then the barrier publishes stage
-    // kb to all waves and frees slot (kb+3) & 3 = (kb-1) & 3
-    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    const int nkb = kb + 3 < KB ? kb + 3 : 0, nslot = (kb + 3) & 3;
-    const bf16x8* st = reinterpret_cast<const bf16x8*>(ring + (kb & 3) * kStageFrags * 64);
+    // this wave's pieces of stage kb have landed (those of the NST-2 younger stages may still
+    // be in flight), every wave is past its reads of stage kb-1; then the barrier publishes
+    // stage kb to all waves and frees the slot of stage kb-1
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(G::VMC) : "memory");
+    const int nkb = kb + NST - 1 < KB ? kb + NST - 1 : 0;
+    const bf16x8* st = reinterpret_cast<const bf16x8*>(ring + slot * SF * 64);
     // two halves of 4 row blocks x 4 column blocks (16 MFMAs each); the second half's A
     // fragments are read before the first half's MFMAs, the next stage's DMA pieces are spread
     // over the two halves
@@ -88,7 +108,10 @@ __global__ __launch_bounds__(kTileWaves * 64, 1) void tile_bf16_kernel(const Lay
     for (int j = 0; j < kWaveCB; ++j) bfr[j] = st[(kTileBlocks + kWaveCB * wc + j) * 64 + lane];
 #pragma unroll
     for (int i = 0; i < 4; ++i) a0[i] = st[(kWaveRB * wr + i) * 64 + lane];
-    if (DLADMM_TILE_EXP != 1) { issue(nkb, nslot, 0); issue(nkb, nslot, 1); }
+    if (DLADMM_TILE_EXP != 1) {
+#pragma unroll
+      for (int q = 0; q < G::H1; ++q) issue(nkb, nslot, q);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) a1[i] = st[(kWaveRB * wr + 4 + i) * 64 + lane];
     if (DLADMM_TILE_EXP == 2) continue;
@@ -98,13 +121,18 @@ __global__ __launch_bounds__(kTileWaves * 64, 1) void tile_bf16_kernel(const Lay
 #pragma unroll
       for (int j = 0; j < kWaveCB; ++j) acc[i][j] = mfma_bf16(a0[i], bfr[j], acc[i][j]);
     __builtin_amdgcn_s_setprio(0);
-    if (DLADMM_TILE_EXP != 1) { issue(nkb, nslot, 2); issue(nkb, nslot, 3); }
+    if (DLADMM_TILE_EXP != 1) {
+#pragma unroll
+      for (int q = G::H1; q < FPW; ++q) issue(nkb, nslot, q);
+    }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < kWaveCB; ++j) acc[4 + i][j] = mfma_bf16(a1[i], bfr[j], acc[4 + i][j]);
     __builtin_amdgcn_s_setprio(0);
+    slot = slot + 1 == NST ? 0 : slot + 1;
+    nslot = nslot + 1 == NST ? 0 : nslot + 1;
   }
   // drain the speculative stages before the workgroup's LDS can be handed to another
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
@@ -194,31 +222,35 @@ __global__ __launch_bounds__(kTileWaves * 64, 1) void tile_bf16_kernel(const Lay
   }
 }
 
-template <int PH>
+template <int PH, int NW>
 hipError_t launch_tile_ph(int variant, const LayerArgs& a, dim3 grid, hipStream_t s) {
-  const dim3 blk(kTileWaves * 64);
+  const dim3 blk(NW * 64);
   switch (variant) {
     case DLADMM_V1_LENA:
-      hipLaunchKernelGGL((tile_bf16_kernel<EM_V1, PK_ELEM, PH>), grid, blk, 0, s, a); break;
+      hipLaunchKernelGGL((tile_bf16_kernel<EM_V1, PK_ELEM, PH, NW>), grid, blk, 0, s, a); break;
     case DLADMM_V2_LTHETA:
-      hipLaunchKernelGGL((tile_bf16_kernel<EM_V1, PK_ROW, PH>), grid, blk, 0, s, a); break;
+      hipLaunchKernelGGL((tile_bf16_kernel<EM_V1, PK_ROW, PH, NW>), grid, blk, 0, s, a); break;
     case DLADMM_V3_FULL:
-      hipLaunchKernelGGL((tile_bf16_kernel<EM_VVAR, PK_ROW, PH>), grid, blk, 0, s, a); break;
+      hipLaunchKernelGGL((tile_bf16_kernel<EM_VVAR, PK_ROW, PH, NW>), grid, blk, 0, s, a); break;
     case DLADMM_V4_SCALAR:
     case DLADMM_V5_TIED:
-      hipLaunchKernelGGL((tile_bf16_kernel<EM_VVAR, PK_SCALAR, PH>), grid, blk, 0, s, a); break;
+      hipLaunchKernelGGL((tile_bf16_kernel<EM_VVAR, PK_SCALAR, PH, NW>), grid, blk, 0, s, a); break;
     case DLADMM_V6_LASSO:
-      hipLaunchKernelGGL((tile_bf16_kernel<EM_LASSO, PK_SCALAR, PH>), grid, blk, 0, s, a); break;
+      hipLaunchKernelGGL((tile_bf16_kernel<EM_LASSO, PK_SCALAR, PH, NW>), grid, blk, 0, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-hipError_t launch_tile_bf16(int phase, int variant, const LayerArgs& a, dim3 grid, hipStream_t s) {
-  switch (phase) {
-    case 0: return launch_tile_ph<0>(variant, a, grid, s);
-    case 1: return launch_tile_ph<1>(variant, a, grid, s);
-    case 2: return launch_tile_ph<2>(variant, a, grid, s);
+hipError_t launch_tile_bf16(int phase, int variant, bool narrow, const LayerArgs& a, dim3 grid,
+                            hipStream_t s) {
+  switch (phase * 2 + (narrow ? 1 : 0)) {
+    case 0: return launch_tile_ph<0, 8>(variant, a, grid, s);
+    case 1: return launch_tile_ph<0, 4>(variant, a, grid, s);
+    case 2: return launch_tile_ph<1, 8>(variant, a, grid, s);
+    case 3: return launch_tile_ph<1, 4>(variant, a, grid, s);
+    case 4: return launch_tile_ph<2, 8>(variant, a, grid, s);
+    case 5: return launch_tile_ph<2, 4>(variant, a, grid, s);
   }
   return hipErrorInvalidValue;
 }

@@ -19,6 +19,14 @@ import problems as P
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["wide", "narrow"])
+def tile(request, monkeypatch):
+    """Every test runs on both tile widths (256 columns / 8 waves, 128 columns / 4 waves with
+    two workgroups per CU; DLADMM_BF16_TILE is read by the C ABI at every call)."""
+    monkeypatch.setenv("DLADMM_BF16_TILE", request.param)
+    return request.param
+
+
 def nrel(a, b):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
@@ -128,3 +136,29 @@ def test_bf16_loss_lean_and_determinism(dl):
         res = (full.E[k] - full.T[k + 1]).double().cpu().numpy()   # X - A Z_k = E_k - T_{k+1}
         assert abs(ls[k, 0] - np.abs(z).sum()) <= 1e-6 * np.abs(z).sum(), k
         assert abs(ls[k, 1] - np.abs(res).sum()) <= 1e-4 * np.abs(res).sum(), k
+
+
+def test_bf16_tile_widths_bit_identical(dl, monkeypatch):
+    """Both tile widths compute every output element as the same chain (k-blocks in order, same
+    packed operands, same epilogue code): the outputs and fused sums are bitwise equal."""
+    m, n, B, K = 300, 530, 600, 3
+    inp = P.make_inputs(m, n, B, 9304)
+    sd = P.make_state_dict("v4", m, n, B, K, inp["A"], 9304, perturb=0.1)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+    net = dl.VARIANTS["v4"](m=m, n=0, d=n, batch_size=B, A=t(inp["A"]), Z0=t(inp["Z0"]),
+                            E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K)
+    net.load_state_dict({k: t(v) for k, v in sd.items()})
+    net.requires_grad_(False)
+    net.cuda()
+    net.precision = "bf16"
+    X = t(inp["X"]).cuda()
+    res = {}
+    for wd in ("wide", "narrow"):
+        monkeypatch.setenv("DLADMM_BF16_TILE", wd)
+        with torch.no_grad():
+            res[wd] = net.run(X, keep_all=True, loss_kind=1)
+    a, b = res["wide"], res["narrow"]
+    for x, y in ((a.Z, b.Z), (a.E, b.E), (a.L, b.L), (a.T, b.T)):
+        assert torch.equal(x, y)
+    # the per-column partials are summed in a fixed order per slot; the slot layout is the same
+    np.testing.assert_allclose(a.loss_sums.cpu().numpy(), b.loss_sums.cpu().numpy(), rtol=1e-6)
