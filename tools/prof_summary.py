@@ -70,6 +70,21 @@ def main():
         if "SQ_VALU_MFMA_BUSY_CYCLES" in sq:
             # SIMD-cycles of MFMA / (1024 SIMDs x per-XCD active cycles)
             res["mfma_busy_frac"] = sq["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * sq["GRBM_GUI_ACTIVE"] / 8)
+    # kernel-trace durations (the first launch is a cold warmup: bench.py's timed region excludes
+    # it) beside the bench line of the same profiled run, whose kernel_ms is measured with HIP
+    # events on the launch stream
+    import statistics
+    kt = durations(os.path.join(src, "kt"))
+    if kt:
+        res["trace"] = {"launches": len(kt), "mean_ms_all": 1e3 * statistics.mean(kt),
+                        "mean_ms_excl_first": 1e3 * statistics.mean(kt[1:] or kt),
+                        "median_ms": 1e3 * statistics.median(kt)}
+    for line in open(os.path.join(src, "kt.log"), errors="replace") if os.path.exists(
+            os.path.join(src, "kt.log")) else []:
+        if line.startswith('{"metric"'):
+            b = json.loads(line)
+            res["bench_line_same_run"] = {"value": b["value"], "kernel_ms_hip_events":
+                                          b["roofline"]["kernel_ms"], "frac": b["roofline"]["frac"]}
     json.dump(res, open(out + "_pmc.json", "w"), indent=1)
     tr = {k: res[k] for k in ("workload", "hbm_bytes_per_launch", "hbm_bytes_per_launch_upper",
                               "hbm_read_bytes_raw", "hbm_write_bytes") if k in res}
