@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DLADMM_LIB") or os.path.join(HERE, "lib", "libdladmm_hip.so")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 PREC_F32, PREC_BF16, PREC_F32_SPLIT = 0, 1, 2
 MAX_LAYERS = 65536
 MAX_LAYERS_V1 = 64
@@ -60,6 +60,7 @@ class FwdDesc(ctypes.Structure):
         ("ev_kernel_start", _fp), ("ev_kernel_stop", _fp),
         ("col_loss", _fp),
         ("precision", _i32), ("pad1", _i32),
+        ("P", _fp),
     ]
 
 

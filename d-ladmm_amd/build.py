@@ -16,9 +16,10 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-UNITS = ("dladmm_capi.hip", "dladmm_fused.hip", "dladmm_fused_x3.hip", "dladmm_layered.hip",
+UNITS = ("dladmm_capi.hip", "dladmm_fused.hip", "dladmm_fused_savep.hip", "dladmm_fused_x3.hip", "dladmm_layered.hip",
          "dladmm_backward.hip", "dladmm_lskm.hip", "dladmm_eval.hip", "dladmm_tile_bf16.hip")
 HEADERS = (os.path.join(ROOT, "include", "dladmm.h"), os.path.join(CSRC, "dladmm_common.h"),
+           os.path.join(CSRC, "dladmm_fused_kernel.h"),
            os.path.join(CSRC, "dladmm_internal.h"), os.path.join(CSRC, "dladmm_slice.h"),
            os.path.join(CSRC, "dladmm_layer_epi.h"))
 OUT = os.path.join(HERE, "lib", "libdladmm_hip.so")
@@ -74,7 +75,7 @@ def build(force: bool = False, verbose: bool = True, extra_flags=()) -> str:
             print("[dladmm build]", " ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
 
-    with ThreadPoolExecutor(max_workers=max(1, min(len(jobs), 4))) as ex:
+    with ThreadPoolExecutor(max_workers=max(1, min(len(jobs), 6))) as ex:
         list(ex.map(run, jobs))
     tmp = OUT + ".tmp"
     run([cc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs)

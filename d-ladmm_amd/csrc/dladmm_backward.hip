@@ -51,11 +51,15 @@ __device__ __forceinline__ float col16_sum(float v) {
 #define BWD_MIN_WG 2
 #endif
 
+// PH: 1 = BK1, 2 = BK2, 3 = BK3, 4 = BK1 on the forward's saved P_k = A Z_k (a.Pk; no GEMM:
+// an elementwise pass over the m x B adjoints)
 template <int EMODE, int PKIND, int PH, int NW, int SB>
 __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs a) {
+  constexpr bool BK1 = PH == 1 || PH == 4;
+  constexpr bool PSV = PH == 4;
   // BK1 keeps 4 workgroups per CU (its latency-bound epilogue needs them): a 2-deep B ring
   constexpr int NSB = PH == 1 ? 2 : 3;
-  __shared__ f32x4 ring[slice_lds_f4<NW, NSB>()];
+  __shared__ f32x4 ring[PSV ? 1 : slice_lds_f4<NW, NSB>()];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -67,8 +71,11 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
   const int ib0 = blockIdx.y * SB;
   const int k = a.k;
 
-  f32x4 acc[SB];
-  slice_gemm<NW, SB, NSB>(ring, a.Wp, a.MBp, ib0, a.KB, a.S, a.ldS, a.Krows, a.B, acc);
+  f32x4 acc[PSV ? 1 : SB];
+  if constexpr (!PSV)
+    slice_gemm<NW, SB, NSB>(ring, a.Wp, a.MBp, ib0, a.KB, a.S, a.ldS, a.Krows, a.B, acc);
+  else
+    (void)ring;
   f32x4 acc2[PH == 2 ? SB : 1];
   if constexpr (PH == 2)
     slice_gemm<NW, SB, NSB>(ring, a.Wp2, a.MBp, ib0, a.KB, a.S2, a.ldS2, a.Krows, a.B, acc2);
@@ -113,6 +120,7 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
   const BView vEp = make_view(a.Ep, m, a.ldep, g, col, cv);
   const BView vLp = make_view(a.Lp, m, a.ldlp, g, col, cv);
   const BView vTk = make_view(a.Tk, m, a.ldt, g, col, cv);
+  const BView vPk = make_view(PSV ? a.Pk : nullptr, m, a.ldt, g, col, cv);
   const BView vZp = make_view(a.Zp, n, a.ldzp, g, col, cv);
   const BView vgZ = make_view(a.gZ, n, a.ldg, g, col, cv);
   const BView vgE = make_view(a.gE, m, a.ldg, g, col, cv);
@@ -132,12 +140,13 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
   // The epilogue is software-pipelined over output blocks: pass 1 (bload) issues every load of
   // block i + 1 before pass 2 (bfinish) computes and stores block i -- the compiler cannot move a
   // load above a store it may alias, so element order would pay one memory round trip per block.
-  struct BIn { float x, ep, lp, tk, b1, b2, AL, gL, AT, gT, AE, gE, zp, AZ, gZ, gb1; };
+  struct BIn { float x, ep, lp, tk, b1, b2, AL, gL, AT, gT, AE, gE, zp, AZ, gZ, gb1, P; };
   auto bload_row = [&](int i, int r) {
     const uint32_t ru = (uint32_t)(16 * (ib0 + i) + r);  // uniform part of the row
     BIn v;
-    if constexpr (PH == 1) {
+    if constexpr (BK1) {
       v.x = vX.ld(ru); v.ep = vEp.ld(ru); v.lp = vLp.ld(ru); v.tk = vTk.ld(ru);
+      if constexpr (PSV) v.P = vPk.ld(ru);
       if constexpr (PKIND == PK_ELEM) { v.b1 = vb1.ld(ru); v.b2 = vb2.ld(ru); }
       v.AL = vAL.ld(ru); v.gL = vgL.ld(ru);
       v.AT = vAT.ld(ru); v.gT = vgT.ld(ru);
@@ -161,12 +170,14 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
       const int row = 16 * (ib0 + i) + 4 * g + r;
       const uint32_t ru = (uint32_t)(16 * (ib0 + i) + r);  // uniform part of the row
       float pv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if constexpr (PH == 1) {
-        // ---------------- BK1: rows of m.  acc = P = A Z_k
+      if constexpr (BK1) {
+        // ---------------- BK1: rows of m.  P = A Z_k (acc, or the forward's saved product)
         const bool rok = row < m;
         const bool ok = cv && rok;
         const int rowc = rok ? row : 0;
-        const float P = acc[i][r];
+        float P;
+        if constexpr (PSV) P = v.P;
+        else P = acc[i][r];
         const float x = v.x;
         const float ep = v.ep;
         const float lp = v.lp;
@@ -322,7 +333,7 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
   };
   // BK1 loads up to 12 operands per element: pipelined it needs > 128 registers and loses the
   // 4-workgroups-per-CU occupancy that hides its latency better, so it runs block by block
-  constexpr bool kPipe = PH != 1;
+  constexpr bool kPipe = !BK1;
   std::array<BIn, 4> cur;
   if constexpr (kPipe) cur = bload(std::integral_constant<int, 0>{});
   static_for<SB>([&](auto I_) {
@@ -351,7 +362,7 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
       const float s = wave_sum(ps[sl]);
       if (lane == 0) a.part[(int64_t)sl * a.nslots + slot] = s;
     };
-    if constexpr (PH == 1) {
+    if constexpr (BK1) {
       flush(DLADMM_P_BETA3);
       if constexpr (EMODE == EM_VVAR) { flush(DLADMM_P_BETA2); flush(DLADMM_P_SS2); flush(DLADMM_P_THETA_E); }
       if constexpr (EMODE == EM_V1) { flush(DLADMM_P_BETA2); flush(DLADMM_P_THETA_E); }
@@ -477,6 +488,7 @@ hipError_t launch_bwd(int phase, int variant, const BwdArgs& a, dim3 grid, int s
                       hipStream_t s) {
   switch (phase) {
     case 1: return launch_bwd_ph<1>(variant, a, grid, sb, s);
+    case 4: return launch_bwd_ph<4>(variant, a, grid, sb, s);
     case 2: return launch_bwd_ph<2>(variant, a, grid, sb, s);
     case 3: return launch_bwd_ph<3>(variant, a, grid, sb, s);
   }

@@ -421,10 +421,15 @@ inline int run_fused(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStrea
   a.Zo = d->Z; a.Eo = d->E; a.Lo = d->L; a.To = d->T; a.ldo = d->ld_out;
   a.lossp = lossp;
   a.dbg = dbg_ptr();  // diagnostic builds (DLADMM_STAMP) write per-wave cycle sums here
+  // training forwards also store P_k = A Z_k for the backward (fwd_desc.P, keep_all only)
+  const bool savep = d->P != nullptr && d->keep_all;
+  a.Po = savep ? d->P : nullptr;
   if (d->ev_kernel_start) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_start, s)) return (int)e;
   }
-  if (hipError_t e = launch_fused_shape(p.shape, d->variant, a, p.tiles, s)) return (int)e;
+  if (hipError_t e = (savep ? launch_fused_shape_savep : launch_fused_shape)(p.shape, d->variant,
+                                                                          a, p.tiles, s))
+    return (int)e;
   if (d->ev_kernel_stop) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_stop, s)) return (int)e;
   }
@@ -606,6 +611,7 @@ struct BwdPlan {
   int64_t Bpad, Rn, Rm;           // padded batch; padded rows of the gU / Var buffers
   int nslots, ncg;
   int wtiles, nchunks; int64_t chunk;
+  bool saved_p;                   // BK1 reads the forward's A Z_k (fwd_desc.P)
   size_t off_a1, off_at, off_m, off_mt, off_az, off_ae, off_al, off_at_, off_gp, off_var,
       off_part, off_wpart, total;
 };
@@ -645,6 +651,8 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   *p = BwdPlan{};
   const dladmm_fwd_desc& f = d->fwd;
   if (int e = make_plan(&f, &p->fwd)) return e;
+  // the forward stored A Z_k only on the fused fp32 path (fwd_desc.P)
+  p->saved_p = f.P != nullptr && f.keep_all && p->fwd.path == 1;
   const int m = f.m, n = f.n;
   const int64_t B = f.batch;
   p->MB = ceil_div(m, 16);
@@ -759,11 +767,13 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
       a.b1e = f.beta1_elem[k]; a.b2e = f.beta2_elem[k];
       a.gb1e = d->g_beta1_elem[k]; a.gb2e = d->g_beta2_elem[k];
     }
-    // BK1: P = A Z_k
+    // BK1: P = A Z_k, recomputed -- or (phase 4) read from the forward's saved P_k, the same
+    // values bit for bit (the forward's own product), which leaves BK1 without a GEMM
     BwdArgs b1 = a;
     b1.KB = p.NB; b1.MBp = p.MBpm; b1.Krows = n; b1.Wp = A1;
     b1.S = f.Z + k * zl; b1.ldS = ldo;
-    if (hipError_t e = launch_bwd(1, v, b1, gm, p.SBm, s)) return (int)e;
+    b1.Pk = p.saved_p ? f.P + k * ml : nullptr;
+    if (hipError_t e = launch_bwd(p.saved_p ? 4 : 1, v, b1, gm, p.SBm, s)) return (int)e;
     // BK2: R = A^T gP, q = M_k Var_k
     BwdArgs b2 = a;
     b2.KB = p.MB; b2.MBp = p.NBpn; b2.Krows = m;

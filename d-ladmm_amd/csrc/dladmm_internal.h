@@ -26,6 +26,7 @@ struct FusedArgs {
   const float* b1e[DLADMM_MAX_LAYERS_V1];
   const float* b2e[DLADMM_MAX_LAYERS_V1];
   float* Zo; float* Eo; float* Lo; float* To; int64_t ldo;
+  float* Po;         // training: A Z_k of every layer [K][m][ldo] (the SAVEP instantiations)
   float* lossp;      // [K][2][ldl] per-column objective terms
   // split-f16 path (dladmm_fused_x3.hip): per-tensor weight scale exponents (wexp[0] = A,
   // wexp[1 + k] = -W_k) and the lean-mode Z_k workspace [2][n][ldzw]
@@ -43,6 +44,9 @@ constexpr int kShapeNP[kNumShapes] = {32, 256, 512};
 
 hipError_t launch_fused_shape(int shape, int variant, const FusedArgs& a, int grid,
                               hipStream_t s);
+// the same kernels that also store P_k = A Z_k (a.Po) for the backward (dladmm_fused_savep.hip)
+hipError_t launch_fused_shape_savep(int shape, int variant, const FusedArgs& a, int grid,
+                                    hipStream_t s);
 // split-f16 fused kernel (DLADMM_PREC_F32_SPLIT); Ap / Wp hold [step][hi|lo] f16 fragments
 bool x3_supports(int variant);
 hipError_t launch_fused_x3_shape(int shape, int variant, const FusedArgs& a, int grid,
@@ -125,6 +129,7 @@ struct BwdArgs {
   const float* Lp; int64_t ldlp;   // L_{k-1}
   const float* Zp; int64_t ldzp;   // Z_{k-1}
   const float* Tk; int64_t ldt;    // T_k
+  const float* Pk;                 // BK1 with the forward's saved A Z_k (row stride ldt)
   const float* gZ; const float* gE; const float* gL; const float* gT; int64_t ldg;  // upstream
   int loss_kind; const float* lcoef;  // fused training objective: device [K][2] (cz_k, cf_k)
   float* AZ; float* AE; float* AL; float* AT; float* GP; float* VAR; int64_t ldw;   // workspace

@@ -317,12 +317,12 @@ class _DLADMMFunction(torch.autograd.Function):
         tables = _slice_tables(mod._tables(dev), nl)
         W = [w.detach() for w in mod._weights()[:nl]]
         r = dladmm_forward(mod.VARIANT, x, mod.A, W, mod.Z0, mod.E0, mod.L0, keep_all=True,
-                           want_T=True, **tables)
+                           want_T=True, want_P=True, **tables)
         ctx.mod = mod
         ctx.nl = nl
         ctx.tables = tables
         ctx.W = W
-        ctx.save_for_backward(x, r.Z, r.E, r.L, r.T)
+        ctx.save_for_backward(x, r.Z, r.E, r.L, r.T, r.P)
         ctx.set_materialize_grads(False)
         K = nl
         outs = tuple(r.Z[k] for k in range(K)) + tuple(r.E[k] for k in range(K)) + \
@@ -333,10 +333,10 @@ class _DLADMMFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *g):
-        x, Z, E, L, T = ctx.saved_tensors
+        x, Z, E, L, T, P = ctx.saved_tensors
         mod = ctx.mod
         K = ctx.nl
-        saved = ForwardResult(Z, E, L, T, None)
+        saved = ForwardResult(Z, E, L, T, None, P=P)
         res = dladmm_backward(mod.VARIANT, x, mod.A, ctx.W, mod.Z0, mod.E0, mod.L0, saved,
                               g[:K], g[K:2 * K], g[2 * K:3 * K],
                               g[3 * K:] if mod.RETURNS_T else None,
@@ -363,27 +363,28 @@ class _DLADMMLossFunction(torch.autograd.Function):
         Z0, E0, L0 = mod._init_state(cols)
         lk = {"l1l1": _lib.LOSS_L1L1, "lasso": _lib.LOSS_LASSO}[kind]
         r = dladmm_forward(mod.VARIANT, x, mod.A, W, Z0, E0, L0, keep_all=True, want_T=True,
-                           loss_kind=lk, **tables)
+                           loss_kind=lk, want_P=True, **tables)
         per_layer = (alpha * r.loss_sums[:, 0] + r.loss_sums[:, 1]) / denom  # fp64 [K]
         c = torch.as_tensor(coeffs, dtype=torch.float64, device=dev)
         total = (c * per_layer).sum().to(torch.float32)
         ctx.mod, ctx.tables, ctx.W, ctx.lk, ctx.cols = mod, tables, W, lk, cols
         # (cz_k, cf_k) per unit upstream gradient
         ctx.base = torch.stack([c * alpha / denom, c / denom], 1).to(torch.float32)
-        ctx.save_for_backward(x, r.Z, r.E, r.L, r.T)
+        ctx.save_for_backward(x, r.Z, r.E, r.L, r.T, r.P)
         per_layer = per_layer.to(torch.float32)
         ctx.mark_non_differentiable(per_layer)
         return total, per_layer
 
     @staticmethod
     def backward(ctx, g_total, g_layers):
-        x, Z, E, L, T = ctx.saved_tensors
+        x, Z, E, L, T, P = ctx.saved_tensors
         mod = ctx.mod
         K = mod.layers
         coef = (ctx.base * g_total).contiguous()  # device-side scale, no host sync
         Z0, E0, L0 = mod._init_state(ctx.cols)
         res = dladmm_backward(mod.VARIANT, x, mod.A, ctx.W, Z0, E0, L0,
-                              ForwardResult(Z, E, L, T, None), loss_kind=ctx.lk, loss_coef=coef,
+                              ForwardResult(Z, E, L, T, None, P=P), loss_kind=ctx.lk,
+                              loss_coef=coef,
                               tied=mod._shared_weight(), **ctx.tables)
         # the objective reads Z_0..Z_{K-1} only: the last layer's E/L steps feed nothing
         reach = {"z": [True] * K, "e": [k < K - 1 for k in range(K)],

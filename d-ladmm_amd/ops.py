@@ -24,6 +24,7 @@ class ForwardResult:
     T: Optional[torch.Tensor]  # [K+1 | 1, m, B] or None
     loss_sums: Optional[torch.Tensor]  # [K, 2] fp64: (sum|Z_k|, fit_k)
     col_loss: Optional[torch.Tensor] = None  # [K, 2, B] fp32 per-column terms (want_col_loss)
+    P: Optional[torch.Tensor] = None  # [K, m, B] A Z_k per layer (want_P: training forwards)
 
 
 def _f32_dev(t: torch.Tensor, name: str) -> torch.Tensor:
@@ -107,6 +108,7 @@ def _fill_fwd_desc(d, variant, X, A, W, Z0, E0, L0, scalar_params, row_params, b
     d.T = out.T.data_ptr() if out.T is not None else None
     d.ld_out = B
     d.loss_sums = out.loss_sums.data_ptr() if out.loss_sums is not None else None
+    d.P = out.P.data_ptr() if out.P is not None else None
     return keep
 
 
@@ -126,13 +128,17 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
                    keep_all: bool = True, want_T: bool = True, loss_kind: int = 0,
                    out: Optional[ForwardResult] = None,
                    kernel_events: Optional[tuple] = None,
-                   want_col_loss: bool = False, precision: str = "f32") -> ForwardResult:
+                   want_col_loss: bool = False, precision: str = "f32",
+                   want_P: bool = False) -> ForwardResult:
     """Run the whole K-layer forward of `variant` (dladmm_variant) on X's device.
 
     X: (m, B); A: (m, n); W: K tensors (n, m) (fc[k].weight; V5 passes the shared one K times);
     Z0: (n, B); E0, L0: (m, B).  scalar_params: (K, 8) device fp32 (V1, V4-V6);
     row_params: (K, 8, max(m, n)) (V2, V3); beta{1,2}_elem: K tensors (m, B) (V1).
     Returns views-ready stacked outputs and, if loss_kind, the per-layer (sum|Z|, fit) sums.
+    want_P (training): also keep P_k = A Z_k of every layer (result.P) when the call runs on the
+    fused fp32 kernel, so the backward reads the product instead of recomputing it; on every
+    other path result.P stays None and the backward recomputes it.
     """
     L = _lib.lib()
     _f32_dev(X, "X")
@@ -158,6 +164,9 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
         raise ValueError(f"dladmm: precision must be one of {sorted(_PRECISIONS)}, "
                          f"got {precision!r}")
     d.precision = _PRECISIONS[precision]
+    if want_P and keep_all and out.P is None and L.dladmm_fwd_path(ctypes.byref(d)) == 1:
+        out.P = torch.empty((K, m, B), device=dev, dtype=torch.float32)
+        d.P = out.P.data_ptr()
     if want_col_loss:
         if not loss_kind:
             raise ValueError("dladmm: per-column objectives need loss_kind")

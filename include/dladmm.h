@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DLADMM_ABI_VERSION 4
+#define DLADMM_ABI_VERSION 5
 #define DLADMM_MAX_LAYERS 65536   /* K limit (V4-V6; e.g. the K=2000 KM ground-truth iteration) */
 #define DLADMM_MAX_LAYERS_V1 64   /* V1: per-layer per-sample beta pointer tables */
 
@@ -154,6 +154,12 @@ typedef struct dladmm_fwd_desc {
          fp32).  bf16 runs on the per-layer kernels (path 3). */
   int32_t precision;
   int32_t pad1;
+
+  /* optional (training): P [K][m][ld_out] receives A Z_k of every layer, exactly the product the
+     E/L/T updates consumed (main_syn_l1l1_scalar.py:114-117).  Written only on path 1 (fused
+     fp32 kernel, keep_all = 1; dladmm_fwd_path() tells); ignored on every other path.  A backward
+     whose fwd.P is set reads it instead of recomputing the product (one GEMM per layer less). */
+  float* P;
 } dladmm_fwd_desc;
 
 enum dladmm_precision { DLADMM_PREC_F32 = 0, DLADMM_PREC_BF16 = 1, DLADMM_PREC_F32_SPLIT = 2 };

@@ -239,3 +239,52 @@ def test_fused_training_loss(name, dl):
         assert e <= max(GTOL, 3.0 * gap), (key, e, gap)
         e2 = nrel(p.grad.cpu().numpy(), p2[key].grad.cpu().numpy())
         assert e2 <= max(GTOL, 3.0 * gap), (key, e2, gap)
+
+
+@pytest.mark.parametrize("variant", ["v4", "v1", "v2", "v3", "v5", "v6"])
+@pytest.mark.parametrize("lossy", [False, True])
+def test_saved_product_backward_bit_identical(variant, lossy, dl):
+    """A training forward on the fused kernel keeps P_k = A Z_k (fwd_desc.P) and BK1 reads it
+    instead of recomputing the product: the forward's own product, so every gradient equals the
+    recomputing backward's bit for bit (the same epilogue on the same values); the saved P is
+    A Z_k of the returned Z_k."""
+    from importlib import import_module
+    ops = import_module("d-ladmm_amd.ops")
+    m, n, B, K = 96, 200, 70, 4
+    d = dict(variant=variant, m=m, n=n, B=B, K=K, seed=9500, perturb=0.1,
+             wscale=0.4 if variant in ("v1", "v2") else None)
+    inp, sd = P.build_problem(d)
+    net = make_train_net(dl, variant, inp, sd, K)
+    net.cuda()
+    X = torch.from_numpy(inp["X"]).cuda()
+    with torch.no_grad():
+        tables = net._tables(X.device)
+    W = [w.detach() for w in net._weights()]
+    lk = dl._lib.LOSS_LASSO if variant == "v6" else dl._lib.LOSS_L1L1
+    args = (net.VARIANT, X, net.A, W, net.Z0, net.E0, net.L0)
+    with torch.no_grad():
+        r1 = ops.dladmm_forward(*args, keep_all=True, want_T=True, want_P=True,
+                                loss_kind=lk if lossy else 0, **tables)
+        r0 = ops.dladmm_forward(*args, keep_all=True, want_T=True,
+                                loss_kind=lk if lossy else 0, **tables)
+    assert r1.P is not None and r0.P is None
+    for a, b in ((r1.Z, r0.Z), (r1.E, r0.E), (r1.L, r0.L), (r1.T, r0.T)):
+        assert torch.equal(a, b)  # the extra store changes nothing else
+    Pref = torch.einsum("mn,knb->kmb", net.A.double(), r1.Z.double())
+    assert float((r1.P.double() - Pref).norm() / Pref.norm()) < 1e-6
+    g = torch.Generator(device="cuda").manual_seed(5)
+    gz = [torch.randn(n, B, device="cuda", generator=g) for _ in range(K)]
+    ge = [torch.randn(m, B, device="cuda", generator=g) for _ in range(K)]
+    gl = [torch.randn(m, B, device="cuda", generator=g) for _ in range(K)]
+    gt = [torch.randn(m, B, device="cuda", generator=g) for _ in range(K + 1)]
+    kw = dict(tied=net._shared_weight(), **tables)
+    if lossy:
+        kw.update(loss_kind=lk, loss_coef=torch.tensor([[1e-3, 1.0]] * K, device="cuda"))
+    res = [ops.dladmm_backward(*args, r, gz, ge, gl, gt, **kw) for r in (r1, r0)]
+    for f in ("gW", "g_scalar", "g_row"):
+        a, b = getattr(res[0], f), getattr(res[1], f)
+        assert (a is None) == (b is None)
+        if a is not None:
+            assert torch.equal(a, b), f
+    for a, b in zip(res[0].g_beta1 + res[0].g_beta2, res[1].g_beta1 + res[1].g_beta2):
+        assert torch.equal(a, b)
