@@ -113,10 +113,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU over RCCL ("nccl" on ROCm).  DLADMM_BENCH_BACKEND=gloo rehearses the N > 1
+    # control path with several ranks on fewer GPUs (rank r on GPU r % count); never for numbers
+    backend = os.environ.get("DLADMM_BENCH_BACKEND", "nccl")
+    gpu = local if backend == "nccl" else local % max(torch.cuda.device_count(), 1)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")  # RCCL on ROCm
-    dev = torch.device("cuda", local if world > 1 else 0)
+        torch.cuda.set_device(gpu)
+        dist.init_process_group(backend)
+    dev = torch.device("cuda", gpu if world > 1 else 0)
     torch.cuda.set_device(dev)
     dl = importlib.import_module("d-ladmm_amd")
 
