@@ -44,7 +44,8 @@ def build(dl, variant, m, n, K, B, A, Z0, E0, L0, dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=65536)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--m", type=int, default=256)
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--layers", type=int, default=15)
@@ -62,8 +63,9 @@ def main():
         for e in ev:
             e.record()  # torch creates the hipEvent lazily; make the handles exist
         with torch.no_grad():
-            r = net.run(X, keep_all=True, loss_kind=lk)  # warmup (tables, workspace)
-            del r
+            for _ in range(a.warmup):  # tables, workspace, clocks (as bench.py)
+                r = net.run(X, keep_all=True, loss_kind=lk)
+                del r
             torch.cuda.synchronize()
             for i in range(a.steps):
                 r = net.run(X, keep_all=True, loss_kind=lk, kernel_events=(ev[2 * i], ev[2 * i + 1]))
