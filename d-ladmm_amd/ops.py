@@ -35,7 +35,7 @@ def _f32_dev(t: torch.Tensor, name: str) -> torch.Tensor:
                            "device only (no CPU fallback)")
     if t.dtype != torch.float32:
         raise TypeError(f"dladmm: {name} must be float32, got {t.dtype}")
-    if t.dim() != 2 or t.stride(1) != 1:
+    if t.dim() != 2 or (t.stride(1) != 1 and t.numel() > 0):  # empty: strides are moot
         raise ValueError(f"dladmm: {name} must be a 2-D row-major matrix (batch contiguous)")
     return t
 
@@ -157,6 +157,18 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
         ls = torch.empty((K, 2), device=dev, dtype=torch.float64) if loss_kind else None
         out = ForwardResult(Zo, Eo, Lo, To, ls)
 
+    if B == 0:
+        # an empty batch: the reference's ops return empty (rows, 0) tensors and zero sums; no
+        # kernel runs (shapes are still checked)
+        _fill_fwd_desc(_lib.FwdDesc(), variant, X, A, W, Z0, E0, L0, scalar_params, row_params,
+                       beta1_elem, beta2_elem, keep_all, loss_kind, out)
+        if out.loss_sums is not None:
+            out.loss_sums.zero_()
+        if want_col_loss:
+            out.col_loss = torch.zeros((K, 2, 0), device=dev, dtype=torch.float32)
+        if want_P and keep_all:
+            out.P = torch.empty((K, m, 0), device=dev, dtype=torch.float32)
+        return out
     d = _lib.FwdDesc()
     keep = _fill_fwd_desc(d, variant, X, A, W, Z0, E0, L0, scalar_params, row_params, beta1_elem,
                           beta2_elem, keep_all, loss_kind, out)
@@ -222,6 +234,15 @@ def dladmm_backward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[
     n = A.shape[1]
     K = len(W)
     dev = X.device
+    if B == 0:  # an empty batch contributes nothing to any gradient
+        gs = torch.zeros((K, _lib.NSCALAR), device=dev, dtype=torch.float64) \
+            if variant >= _lib.V4_SCALAR else None
+        gr = torch.zeros((K, _lib.NSCALAR, row_params.shape[2]), device=dev,
+                         dtype=torch.float64) if variant in (_lib.V2_LTHETA, _lib.V3_FULL) else None
+        gb = [torch.zeros((m, 0), device=dev) for _ in range(K)] if variant == _lib.V1_LENA \
+            else []
+        return BackwardResult(torch.zeros((1 if tied else K, n, m), device=dev), gs, gr, gb,
+                              [t.clone() for t in gb])
     d = _lib.BwdDesc()
     keep = _fill_fwd_desc(d.fwd, variant, X, A, W, Z0, E0, L0, scalar_params, row_params,
                           beta1_elem, beta2_elem, True, 0, saved)

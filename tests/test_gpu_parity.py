@@ -310,3 +310,35 @@ def test_strided_views_per_layer_paths(precision, dl):
     for a, b in zip(out_v, out_c):
         for x, y in zip(a, b):
             assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("variant", ["v1", "v4", "v6"])
+def test_empty_batch(variant, dl, oracle):
+    """batch_size = 0: the reference's ops return K empty (rows, 0) tensors (and T), so does the
+    drop-in (no kernel runs); the fused objective sums are zero and a training step leaves zero
+    gradients."""
+    m, n, K = 24, 40, 3
+    inp = P.make_inputs(m, n, 0, 3)
+    sd = P.make_state_dict(variant, m, n, 0, K, inp["A"], 3)
+    t = torch.from_numpy
+    net = dl.VARIANTS[variant](m=m, n=0, d=n, batch_size=0, A=t(inp["A"]), Z0=t(inp["Z0"]),
+                               E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K)
+    net.load_state_dict({k: t(v) for k, v in sd.items()})
+    ref = oracle.forward(variant, inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd, K)
+    X = t(inp["X"]).cuda()
+    with torch.no_grad():
+        out = net(X)
+    assert len(out) == (4 if variant != "v1" else 3)
+    for i, nm in enumerate("ZELT"[:len(out)]):
+        assert len(out[i]) == len(ref[nm])
+        for a, b in zip(out[i], ref[nm]):
+            assert tuple(a.shape) == b.shape
+    with torch.no_grad():
+        r = net.run(X, keep_all=True, loss_kind=1)
+    assert torch.count_nonzero(r.loss_sums) == 0
+    if variant == "v4":
+        net.requires_grad_(True)
+        total, _ = net.training_loss(X, 0.001, [1.0] * K, "l1l1")
+        total.backward()
+        for p in net.parameters():
+            assert p.grad is None or torch.count_nonzero(p.grad) == 0
