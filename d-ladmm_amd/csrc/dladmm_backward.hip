@@ -76,9 +76,22 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
     slice_gemm<NW, SB, NSB>(ring, a.Wp, a.MBp, ib0, a.KB, a.S, a.ldS, a.Krows, a.B, acc);
   else
     (void)ring;
+  // BK2: with a uniform theta_z >= 0 the shrink S(U, theta_z) is nonzero exactly where
+  // |U| > theta_z, so the forward's own Z_k gives S'(U) (and the objective's sign(Z_k)); then
+  // q = W_k Var_k is needed only for a trainable step s1 (V5) -- host: zk_mask -- and for
+  // theta_z < 0 (both relus open), where the second GEMM still runs
+  bool zmask = false;
+  if constexpr (PH == 2 && PKIND != PK_ROW)
+    zmask = a.zk_mask && ((cfloat_p)a.scal)[k * DLADMM_NSCALAR + DLADMM_P_THETA_Z] >= 0.0f;
   f32x4 acc2[PH == 2 ? SB : 1];
-  if constexpr (PH == 2)
-    slice_gemm<NW, SB, NSB>(ring, a.Wp2, a.MBp, ib0, a.KB, a.S2, a.ldS2, a.Krows, a.B, acc2);
+  if constexpr (PH == 2) {
+    if (!zmask) {
+      slice_gemm<NW, SB, NSB>(ring, a.Wp2, a.MBp, ib0, a.KB, a.S2, a.ldS2, a.Krows, a.B, acc2);
+    } else {
+#pragma unroll
+      for (int i = 0; i < SB; ++i) acc2[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
 
   cfloat_p sp = (cfloat_p)a.scal + k * DLADMM_NSCALAR;
   const float* rp = a.rowp ? a.rowp + (int64_t)k * 8 * a.rstride : nullptr;
@@ -122,6 +135,7 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
   const BView vTk = make_view(a.Tk, m, a.ldt, g, col, cv);
   const BView vPk = make_view(PSV ? a.Pk : nullptr, m, a.ldt, g, col, cv);
   const BView vZp = make_view(a.Zp, n, a.ldzp, g, col, cv);
+  const BView vZk = make_view(PH == 2 && zmask ? a.Zk : nullptr, n, a.ldzk, g, col, cv);
   const BView vgZ = make_view(a.gZ, n, a.ldg, g, col, cv);
   const BView vgE = make_view(a.gE, m, a.ldg, g, col, cv);
   const BView vgL = make_view(a.gL, m, a.ldg, g, col, cv);
@@ -140,7 +154,7 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
   // The epilogue is software-pipelined over output blocks: pass 1 (bload) issues every load of
   // block i + 1 before pass 2 (bfinish) computes and stores block i -- the compiler cannot move a
   // load above a store it may alias, so element order would pay one memory round trip per block.
-  struct BIn { float x, ep, lp, tk, b1, b2, AL, gL, AT, gT, AE, gE, zp, AZ, gZ, gb1, P; };
+  struct BIn { float x, ep, lp, tk, b1, b2, AL, gL, AT, gT, AE, gE, zp, AZ, gZ, gb1, P, zk; };
   auto bload_row = [&](int i, int r) {
     const uint32_t ru = (uint32_t)(16 * (ib0 + i) + r);  // uniform part of the row
     BIn v;
@@ -152,7 +166,7 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
       v.AT = vAT.ld(ru); v.gT = vgT.ld(ru);
       v.AE = vAE.ld(ru); v.gE = vgE.ld(ru);
     } else if constexpr (PH == 2) {
-      v.zp = vZp.ld(ru); v.AZ = vAZ.ld(ru); v.gZ = vgZ.ld(ru);
+      v.zp = vZp.ld(ru); v.AZ = vAZ.ld(ru); v.gZ = vgZ.ld(ru); v.zk = vZk.ld(ru);
     } else {
       v.tk = vTk.ld(ru);
       if constexpr (PKIND == PK_ELEM) { v.b1 = vb1.ld(ru); v.gb1 = vgb1.ld(ru); }
@@ -283,12 +297,15 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
         const float U = zp - ((PKIND == PK_SCALAR) ? s1 * q : q);
         const float thz = pm(DLADMM_P_THETA_Z, rowc);
         float gZt = (v.AZ + v.gZ) + R;
-        {
-          // d/dZ_k of cz_k * sum|Z_k|, Z_k = S(U, theta_z) recomputed as the forward formed it
-          const float z = shrink(U, thz);
-          gZt = gZt + czk * (z > 0.f ? 1.f : (z < 0.f ? -1.f : 0.f));
+        // Z_k = S(U, theta_z): the forward's (zmask) or recomputed as the forward formed it
+        const float z = zmask ? v.zk : shrink(U, thz);
+        // d/dZ_k of cz_k * sum|Z_k|
+        gZt = gZt + czk * (z > 0.f ? 1.f : (z < 0.f ? -1.f : 0.f));
+        SD d = shrink_d(U, thz);
+        if (zmask) {  // theta_z >= 0: [U - th > 0] = [Z_k > 0], [-U - th > 0] = [Z_k < 0]
+          const float zp1 = z > 0.f ? 1.f : 0.f, zn1 = z < 0.f ? 1.f : 0.f;
+          d = SD{zp1 + zn1, zn1 - zp1};
         }
-        const SD d = shrink_d(U, thz);
         const float gU = gZt * d.dx;
         pv[DLADMM_P_THETA_Z] = gZt * d.dth;
         if constexpr (PKIND == PK_SCALAR) {

@@ -779,6 +779,10 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
     b2.KB = p.MB; b2.MBp = p.NBpn; b2.Krows = m;
     b2.Wp = At; b2.S = GP; b2.ldS = ldw;
     b2.Wp2 = Mp; b2.S2 = VAR; b2.ldS2 = ldw;
+    // S'(U_k) from the saved Z_k unless a parameter scales W_k Var_k (V5's ss1) or theta_z is
+    // per row (V2, V3); the kernel also checks theta_z >= 0
+    b2.Zk = f.Z + k * zl; b2.ldzk = ldo;
+    b2.zk_mask = (v == DLADMM_V1_LENA || v == DLADMM_V4_SCALAR || v == DLADMM_V6_LASSO) ? 1 : 0;
     if (hipError_t e = launch_bwd(2, v, b2, gn, 16, s)) return (int)e;
     // BK3: gVar = M_k^T gU
     BwdArgs b3 = a;

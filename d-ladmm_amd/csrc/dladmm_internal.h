@@ -130,6 +130,9 @@ struct BwdArgs {
   const float* Zp; int64_t ldzp;   // Z_{k-1}
   const float* Tk; int64_t ldt;    // T_k
   const float* Pk;                 // BK1 with the forward's saved A Z_k (row stride ldt)
+  const float* Zk; int64_t ldzk;   // BK2: the forward's Z_k (its shrink mask, zk_mask)
+  int zk_mask;                     // BK2: 1 = no parameter scales W_k Var_k (s1), so with
+                                   // theta_z >= 0 the mask comes from Z_k and q is not formed
   const float* gZ; const float* gE; const float* gL; const float* gT; int64_t ldg;  // upstream
   int loss_kind; const float* lcoef;  // fused training objective: device [K][2] (cz_k, cf_k)
   float* AZ; float* AE; float* AL; float* AT; float* GP; float* VAR; int64_t ldw;   // workspace
