@@ -163,6 +163,12 @@ __device__ __forceinline__ float amax(float m, float v) {
   asm("v_max_f32_e64 %0, %1, |%2|" : "=v"(r) : "v"(m), "v"(v));
   return r;
 }
+// m = max(m, |u|, |v|) in one v_max3_f32
+__device__ __forceinline__ float amax2(float m, float u, float v) {
+  float r;
+  asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(u), "v"(v));
+  return r;
+}
 __device__ __forceinline__ i32x4 mk_rsrc4(const void* p, uint32_t bytes) {
   const uint64_t a = (uint64_t)p;
   i32x4 r;
@@ -267,7 +273,9 @@ struct Win {
 
 }  // namespace x3
 
-template <int MP, int NP, int EMODE, int PKIND>
+// LQ: the fused objective's fit term is 0.5 (X - A Z)^2 (LASSO) instead of |X - A Z| -- a
+// compile-time choice, so each element accumulates only the term the call reduces
+template <int MP, int NP, int EMODE, int PKIND, bool LQ>
 __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
   using namespace x3;
   constexpr int MB = MP / 16, NB = NP / 16, KS1 = MP / 32, KS2 = NP / 32;
@@ -311,14 +319,13 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
   const bool cv = col < a.B;
   const int m = a.m, n = a.n, K = a.K;
   const bool lossz = a.loss_kind != 0;
-  const bool lasso = __builtin_amdgcn_readfirstlane(a.loss_kind) == DLADMM_LOSS_LASSO;
   auto lane_off = [&](int64_t ld) -> uint32_t {
     return cv ? (uint32_t)((col + (int64_t)(4 * g) * ld) * 4) : kOOB;
   };
 
   float Er[MB][4], Lr[MB][4], Vr[MB][4];
   BOp Vpk[KS1], Zpk[KS2];
-  float regsum = 0.f, fit1 = 0.f, fit2 = 0.f;
+  float regsum = 0.f, fit = 0.f;
 
   // ---------------------------------------------------------------- Z_{k-1} delivery
   // Block b of the Z matrix the next G1 chunks need (set per pass): rows 16b + (l >> 2), the
@@ -521,7 +528,7 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     zn[b & 1][r] = z;
     stage(0, r, z);
     regsum += fabsf(z);
-    zmx = amax(zmx, z);
+    if (r & 1) zmx = amax2(zmx, zn[b & 1][(r - 1) & 3], z);  // rows in pairs: one v_max3
     // materialise the running sums here: left alone, the scheduler sinks both serial chains
     // below the pass and keeps every row's z live (spills)
     asm volatile("" : "+v"(regsum), "+v"(zmx));
@@ -533,7 +540,7 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     flush(2, O.l, oo4, soff);
     flush(3, O.t, oo4, soff);
   };
-  float vmx = 0.f;
+  float vmx = 0.f, vpend = 0.f;
   auto epi2_row = [&](const LayerP& P, bool pro, int b, int r, float Pv, float x) {
     if constexpr (X3_ABL & 2) {
       Vr[b][r] = Pv;
@@ -562,18 +569,19 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     stage(2, r, l);
     stage(3, r, t);
     const float res = x - Pv;
-    fit1 += fabsf(res);
-    fit2 = __builtin_fmaf(res, res, fit2);
+    if constexpr (LQ) fit = __builtin_fmaf(res, res, fit);
+    else fit += fabsf(res);
     const float v = l + P.b1n * t;                                   // main_lena.py:85
-    vmx = amax(vmx, v);
-    asm volatile("" : "+v"(fit1), "+v"(fit2), "+v"(vmx));
+    if (r & 1) vmx = amax2(vmx, vpend, v);  // rows in pairs: one v_max3
+    else vpend = v;
+    asm volatile("" : "+v"(fit), "+v"(vmx));
     Vr[b][r] = v;
     pin_agpr(Vr[b][r]);  // AGPRs: Vr, Zpk (G2) / Vpk, Zpk (G1); VGPRs: E, L, fragments
   };
   auto flush_loss = [&](int k) {
     if (lossz && k >= 0) {
       const float rs = col_sum(regsum);
-      const float fs = lasso ? 0.5f * col_sum(fit2) : col_sum(fit1);
+      const float fs = LQ ? 0.5f * col_sum(fit) : col_sum(fit);
       if (g == 0) {
         const int64_t c = (int64_t)blockIdx.x * kTileCols + w * 16 + j;
         a.lossp[(int64_t)(2 * k + 0) * a.ldl + c] = rs;
@@ -581,8 +589,7 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
       }
     }
     regsum = 0.f;
-    fit1 = 0.f;
-    fit2 = 0.f;
+    fit = 0.f;
   };
 
   // ---------------------------------------------------------------- ring steps
@@ -935,7 +942,10 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
 
 template <int MP, int NP, int EM, int PK>
 hipError_t launch_x3(const FusedArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((fused_x3_kernel<MP, NP, EM, PK>), dim3(grid), dim3(256), 0, s, a);
+  if (a.loss_kind == DLADMM_LOSS_LASSO)
+    hipLaunchKernelGGL((fused_x3_kernel<MP, NP, EM, PK, true>), dim3(grid), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((fused_x3_kernel<MP, NP, EM, PK, false>), dim3(grid), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
