@@ -28,10 +28,12 @@ def global_objectives(local_sums: torch.Tensor, alpha: float, total_batch: int,
     (sum|Z_k|, fit_k): one all-reduce(SUM), then (alpha*sum|Z| + fit) / B_total, i.e. the
     reference's alpha*sum(|Z|,0).mean() + sum(|X-AZ|,0).mean() (main_syn_l1l1_scalar.py:290-294)
     over all ranks' columns."""
-    s = local_sums.clone()
+    s = local_sums
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        s = s.clone()  # the caller's sums stay its shard's
         dist.all_reduce(s, op=dist.ReduceOp.SUM, group=group)
-    return (alpha * s[:, 0] + s[:, 1]) / total_batch
+    # (alpha * sum|Z| + fit) / B in two small kernels
+    return torch.add(s[:, 1], s[:, 0], alpha=alpha).div_(total_batch)
 
 
 def allreduce_grads(module: torch.nn.Module, group: Optional[dist.ProcessGroup] = None,
