@@ -52,11 +52,20 @@ __device__ __forceinline__ float col16_sum(float v) {
 #endif
 
 // PH: 1 = BK1, 2 = BK2, 3 = BK3, 4 = BK1 on the forward's saved P_k = A Z_k (a.Pk; no GEMM:
-// an elementwise pass over the m x B adjoints)
+// an elementwise pass over the m x B adjoints), 5 = BK2 on the saved Z_k mask only (one GEMM,
+// 32-block slices; launched beside a PH 2 launch, each exits unless theta_z's sign is its case)
 template <int EMODE, int PKIND, int PH, int NW, int SB>
 __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs a) {
   constexpr bool BK1 = PH == 1 || PH == 4;
+  constexpr bool BK2 = PH == 2 || PH == 5;
   constexpr bool PSV = PH == 4;
+  if constexpr (BK2 && PKIND != PK_ROW) {
+    // zk_mask 2: the PH 5 launch covers theta_z >= 0 and the PH 2 launch theta_z < 0
+    if (a.zk_mask == 2) {
+      const bool pos = ((cfloat_p)a.scal)[a.k * DLADMM_NSCALAR + DLADMM_P_THETA_Z] >= 0.0f;
+      if (pos != (PH == 5)) return;  // uniform: the whole grid exits
+    }
+  }
   // BK1 keeps 4 workgroups per CU (its latency-bound epilogue needs them): a 2-deep B ring
   constexpr int NSB = PH == 1 ? 2 : 3;
   __shared__ f32x4 ring[PSV ? 1 : slice_lds_f4<NW, NSB>()];
@@ -80,11 +89,13 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
   // |U| > theta_z, so the forward's own Z_k gives S'(U) (and the objective's sign(Z_k)); then
   // q = W_k Var_k is needed only for a trainable step s1 (V5) -- host: zk_mask -- and for
   // theta_z < 0 (both relus open), where the second GEMM still runs
-  bool zmask = false;
+  bool zmask = PH == 5;
   if constexpr (PH == 2 && PKIND != PK_ROW)
     zmask = a.zk_mask && ((cfloat_p)a.scal)[k * DLADMM_NSCALAR + DLADMM_P_THETA_Z] >= 0.0f;
   f32x4 acc2[PH == 2 ? SB : 1];
-  if constexpr (PH == 2) {
+  if constexpr (PH == 5) {
+    acc2[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+  } else if constexpr (PH == 2) {
     if (!zmask) {
       slice_gemm<NW, SB, NSB>(ring, a.Wp2, a.MBp, ib0, a.KB, a.S2, a.ldS2, a.Krows, a.B, acc2);
     } else {
@@ -135,7 +146,7 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
   const BView vTk = make_view(a.Tk, m, a.ldt, g, col, cv);
   const BView vPk = make_view(PSV ? a.Pk : nullptr, m, a.ldt, g, col, cv);
   const BView vZp = make_view(a.Zp, n, a.ldzp, g, col, cv);
-  const BView vZk = make_view(PH == 2 && zmask ? a.Zk : nullptr, n, a.ldzk, g, col, cv);
+  const BView vZk = make_view(BK2 && zmask ? a.Zk : nullptr, n, a.ldzk, g, col, cv);
   const BView vgZ = make_view(a.gZ, n, a.ldg, g, col, cv);
   const BView vgE = make_view(a.gE, m, a.ldg, g, col, cv);
   const BView vgL = make_view(a.gL, m, a.ldg, g, col, cv);
@@ -165,7 +176,7 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
       v.AL = vAL.ld(ru); v.gL = vgL.ld(ru);
       v.AT = vAT.ld(ru); v.gT = vgT.ld(ru);
       v.AE = vAE.ld(ru); v.gE = vgE.ld(ru);
-    } else if constexpr (PH == 2) {
+    } else if constexpr (BK2) {
       v.zp = vZp.ld(ru); v.AZ = vAZ.ld(ru); v.gZ = vgZ.ld(ru); v.zk = vZk.ld(ru);
     } else {
       v.tk = vTk.ld(ru);
@@ -283,13 +294,13 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
         row_flush(row, rok, pv, (1u << DLADMM_P_BETA3) | (1u << DLADMM_P_BETA2) |
                                     (1u << DLADMM_P_THETA_E) | (1u << DLADMM_P_SS2) |
                                     (1u << DLADMM_P_SS2B));
-      } else if constexpr (PH == 2) {
+      } else if constexpr (BK2) {
         // ---------------- BK2: rows of n.  acc = R = A^T gP, acc2 = q = W_k Var_k
         const bool rok = row < n;
         const bool ok = cv && rok;
         const int rowc = rok ? row : 0;
         const float R = acc[i][r];
-        const float q = acc2[i][r];
+        const float q = PH == 5 ? 0.0f : acc2[PH == 5 ? 0 : i][r];
         const float zp = v.zp;
         float s1 = 1.0f;
         if constexpr (PKIND == PK_SCALAR) s1 = spv[DLADMM_P_S1];
@@ -374,17 +385,23 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
     if constexpr (BWD_EPI_FENCE) __builtin_amdgcn_sched_barrier(0);
   });
   if constexpr (PKIND == PK_SCALAR) {
-    const int slot = blockIdx.y * gridDim.x * NW + cg;
+    // PH 5 slices span two 16-block slices: the partial goes to the first one's slot and the
+    // second one's slot is zeroed (the reduction sums the 16-block slot count)
+    const int sy = PH == 5 ? 2 * (int)blockIdx.y : (int)blockIdx.y;
+    const int slot = sy * gridDim.x * NW + cg;
     auto flush = [&](int sl) {
       const float s = wave_sum(ps[sl]);
-      if (lane == 0) a.part[(int64_t)sl * a.nslots + slot] = s;
+      if (lane == 0) {
+        a.part[(int64_t)sl * a.nslots + slot] = s;
+        if (PH == 5) a.part[(int64_t)sl * a.nslots + slot + gridDim.x * NW] = 0.0f;
+      }
     };
     if constexpr (BK1) {
       flush(DLADMM_P_BETA3);
       if constexpr (EMODE == EM_VVAR) { flush(DLADMM_P_BETA2); flush(DLADMM_P_SS2); flush(DLADMM_P_THETA_E); }
       if constexpr (EMODE == EM_V1) { flush(DLADMM_P_BETA2); flush(DLADMM_P_THETA_E); }
       if constexpr (EMODE == EM_LASSO) { flush(DLADMM_P_SS2); flush(DLADMM_P_SS2B); }
-    } else if constexpr (PH == 2) {
+    } else if constexpr (BK2) {
       flush(DLADMM_P_THETA_Z);
       flush(DLADMM_P_S1);
     } else {
@@ -482,10 +499,16 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* part, in
 template <int EM, int PK, int PH>
 hipError_t launch_bwd_v(const BwdArgs& a, dim3 grid, int sb, hipStream_t s) {
   constexpr int NW = kBwdWaves;
-  // 16 output blocks per slice: with 32 the epilogue's operand loads spill (PH 1, scalar kind)
-  if (sb != 16) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((bwd_kernel<EM, PK, PH, NW, 16>), grid, dim3(NW * 64), 0, s, a);
-  return hipGetLastError();
+  // 16 output blocks per slice (with 32 the epilogue's operand loads spill: PH 1, scalar kind);
+  // PH 5 (one GEMM, light epilogue) runs 32
+  constexpr int SB = PH == 5 ? 32 : 16;
+  if (sb != SB) return hipErrorInvalidValue;
+  if constexpr (PH == 5 && PK == PK_ROW) {
+    return hipErrorInvalidValue;
+  } else {
+    hipLaunchKernelGGL((bwd_kernel<EM, PK, PH, NW, SB>), grid, dim3(NW * 64), 0, s, a);
+    return hipGetLastError();
+  }
 }
 
 template <int PH>
@@ -506,6 +529,7 @@ hipError_t launch_bwd(int phase, int variant, const BwdArgs& a, dim3 grid, int s
   switch (phase) {
     case 1: return launch_bwd_ph<1>(variant, a, grid, sb, s);
     case 4: return launch_bwd_ph<4>(variant, a, grid, sb, s);
+    case 5: return launch_bwd_ph<5>(variant, a, grid, sb, s);
     case 2: return launch_bwd_ph<2>(variant, a, grid, sb, s);
     case 3: return launch_bwd_ph<3>(variant, a, grid, sb, s);
   }

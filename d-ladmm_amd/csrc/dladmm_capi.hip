@@ -659,7 +659,8 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   p->NB = ceil_div(n, 16);
   p->SBm = 16;                          // BK1 / BK3 output rows: m (SB = 32 spills registers)
   p->MBpm = ceil_div(p->MB, p->SBm) * p->SBm;
-  p->NBpn = ceil_div(p->NB, 16) * 16;   // BK2 output rows: n (two accumulator sets: 16 blocks)
+  p->NBpn = ceil_div(p->NB, 32) * 32;   // BK2 output rows: n (16-block slices with two
+                                        // accumulator sets, 32-block ones with one: PH 5)
   p->slices_m = p->MBpm / p->SBm;
   p->slices_n = p->NBpn / 16;
   p->gx = ceil_div(f.batch, kBwdCols);
@@ -782,7 +783,13 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
     // S'(U_k) from the saved Z_k unless a parameter scales W_k Var_k (V5's ss1) or theta_z is
     // per row (V2, V3); the kernel also checks theta_z >= 0
     b2.Zk = f.Z + k * zl; b2.ldzk = ldo;
-    b2.zk_mask = (v == DLADMM_V1_LENA || v == DLADMM_V4_SCALAR || v == DLADMM_V6_LASSO) ? 1 : 0;
+    const bool zm = v == DLADMM_V1_LENA || v == DLADMM_V4_SCALAR || v == DLADMM_V6_LASSO;
+    // mask variants: a PH 5 launch (32-block slices, one GEMM) does the layer when theta_z >= 0,
+    // the PH 2 launch when theta_z < 0; the other exits at once (the sign is read on the device)
+    b2.zk_mask = zm ? 2 : 0;
+    if (zm) {
+      if (hipError_t e = launch_bwd(5, v, b2, dim3(p.gx, p.slices_n / 2), 32, s)) return (int)e;
+    }
     if (hipError_t e = launch_bwd(2, v, b2, gn, 16, s)) return (int)e;
     // BK3: gVar = M_k^T gU
     BwdArgs b3 = a;
