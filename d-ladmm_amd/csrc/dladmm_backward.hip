@@ -73,8 +73,12 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4;
-  const int64_t col = (int64_t)blockIdx.x * (16 * NW) + w * 16 + (lane & 15);
+  // GEMM phases: the MFMA C/D layout (lane: column l & 15, rows 16b + 4(l >> 4) + r).  PH 4 has
+  // no GEMM, so a lane owns one column and a wave 64 consecutive ones: every operand access of a
+  // row is one 256-byte piece (the C/D layout touches four 64-byte pieces per instruction)
+  const int g = PSV ? 0 : lane >> 4;
+  const int64_t col = PSV ? (int64_t)blockIdx.x * (64 * NW) + w * 64 + lane
+                          : (int64_t)blockIdx.x * (16 * NW) + w * 16 + (lane & 15);
   const bool cv = col < a.B;
   const int64_t colc = cv ? col : 0;
   const int ib0 = blockIdx.y * SB;
@@ -131,8 +135,8 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
 #pragma unroll
       for (int sl = 0; sl < 8; ++sl) {
         if (!(mask & (1u << sl))) continue;
-        const float s = col16_sum(v[sl]);
-        if ((lane & 15) == 0 && rok)
+        const float s = PSV ? wave_sum(v[sl]) : col16_sum(v[sl]);
+        if ((PSV ? lane == 0 : (lane & 15) == 0) && rok)
           a.part[((int64_t)sl * a.rstride + row) * a.ncg + cg] = s;
       }
     }
@@ -368,7 +372,7 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
     constexpr int i = decltype(I_)::value;
     if constexpr (!kPipe) {
 #pragma unroll
-      for (int r = 0; r < 4; r += 2) {  // two rows' loads, then their stores
+      for (int r = 0; r < (PSV ? 16 : 4); r += 2) {  // two rows' loads, then their stores
         const BIn v0 = bload_row(i, r), v1 = bload_row(i, r + 1);
         bfinish_row(i, r, v0);
         bfinish_row(i, r + 1, v1);

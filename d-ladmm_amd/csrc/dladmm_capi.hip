@@ -774,7 +774,10 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
     b1.KB = p.NB; b1.MBp = p.MBpm; b1.Krows = n; b1.Wp = A1;
     b1.S = f.Z + k * zl; b1.ldS = ldo;
     b1.Pk = p.saved_p ? f.P + k * ml : nullptr;
-    if (hipError_t e = launch_bwd(p.saved_p ? 4 : 1, v, b1, gm, p.SBm, s)) return (int)e;
+    // phase 4: a wave covers 64 columns (one per lane), so its grid has a quarter of the tiles
+    const dim3 gm4(ceil_div((int)B, 64 * kBwdWaves), p.slices_m);
+    if (hipError_t e = launch_bwd(p.saved_p ? 4 : 1, v, b1, p.saved_p ? gm4 : gm, p.SBm, s))
+      return (int)e;
     // BK2: R = A^T gP, q = M_k Var_k
     BwdArgs b2 = a;
     b2.KB = p.MB; b2.MBp = p.NBpn; b2.Krows = m;

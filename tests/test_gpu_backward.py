@@ -245,9 +245,10 @@ def test_fused_training_loss(name, dl):
 @pytest.mark.parametrize("lossy", [False, True])
 def test_saved_product_backward_bit_identical(variant, lossy, dl):
     """A training forward on the fused kernel keeps P_k = A Z_k (fwd_desc.P) and BK1 reads it
-    instead of recomputing the product: the forward's own product, so every gradient equals the
-    recomputing backward's bit for bit (the same epilogue on the same values); the saved P is
-    A Z_k of the returned Z_k."""
+    instead of recomputing the product: the forward's own product, so every elementwise adjoint
+    and the weight and per-sample gradients equal the recomputing backward's bit for bit; the
+    parameter-slot sums agree to their fp32 partials' rounding; the saved P is A Z_k of the
+    returned Z_k."""
     from importlib import import_module
     ops = import_module("d-ladmm_amd.ops")
     m, n, B, K = 96, 200, 70, 4
@@ -284,7 +285,13 @@ def test_saved_product_backward_bit_identical(variant, lossy, dl):
     for f in ("gW", "g_scalar", "g_row"):
         a, b = getattr(res[0], f), getattr(res[1], f)
         assert (a is None) == (b is None)
-        if a is not None:
+        if a is None:
+            continue
+        if f == "gW":
             assert torch.equal(a, b), f
+        else:
+            # the GEMM-free BK1 maps a lane to one column (the recomputing one to the MFMA
+            # layout), so its per-wave partial sums group the same terms differently
+            assert nrel(a.cpu().numpy(), b.cpu().numpy()) <= 2e-6, f
     for a, b in zip(res[0].g_beta1 + res[0].g_beta2, res[1].g_beta1 + res[1].g_beta2):
         assert torch.equal(a, b)
