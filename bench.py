@@ -5,9 +5,15 @@ Workload (BASELINE.json configs[1]/north_star): the reference's V4 model
 with the gen_syn_data.py distribution generated on device, reference-init parameters.  One "step"
 = one complete forward with every layer's Z, E, L and T written (the reference's return lists),
 the per-layer L1L1 objective of the training loop fused in, and (N > 1) one RCCL all-reduce of
-the [K, 2] objective sums.  Batch is sharded across ranks (weak scaling: B per GPU fixed).
+the [K, 2] objective sums.  Batch is sharded across ranks: the headline is weak scaling (B per GPU
+fixed); `--global-batch G` makes it strong scaling instead (BASELINE config 3: G = 262,144 columns
+split by dist.shard_columns over the ranks).  The default run also times config 3's strong-scaling
+workload beside the headline (`cfg3_strong`), so every driver run at N = 1/2/4/8 records both
+curves.  The model is built after torch.manual_seed(1126), so the objective is
+reproducible.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B | --global-batch G]
+                    [--no-cpu-baseline] [--no-split] [--no-cfg3]
 
 Prints ONE JSON line (rank 0).  Roofline of the dominant kernel (the fused K-layer kernel):
 algorithmic FLOP per launch (4K+2)*m*n*B over its average duration measured here with
@@ -40,7 +46,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=65536, help="columns per GPU")
+    ap.add_argument("--batch", type=int, default=65536, help="columns per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling: this many columns in total, split over the ranks by "
+                         "dist.shard_columns (BASELINE config 3: 262144)")
+    ap.add_argument("--no-cfg3", action="store_true",
+                    help="skip the secondary config-3 strong-scaling measurement (262,144 "
+                         "global columns)")
     ap.add_argument("--m", type=int, default=256)
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--layers", type=int, default=15)
@@ -56,14 +68,18 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-split", action="store_true",
                     help="skip the secondary f32_split measurement of the f32 headline run")
-    ap.add_argument("--cpu-batch", type=int, default=8192, help="columns of the CPU sample")
+    ap.add_argument("--cpu-batch", type=int, default=10000,
+                    help="columns of the CPU sample (SURVEY 8d: B = 10,000)")
+    ap.add_argument("--cpu-runs", type=int, default=5, help="timed CPU forwards (median)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return ap.parse_args()
 
 
-def synth(m, n, B, seed, dev):
+def synth(m, n, B, seed, dev, cols=None):
     """gen_syn_data.py:14-47 distribution on device: A column-normalised N(0,1) (same on every
-    rank), Z*, E* Bernoulli(0.1)*N(0,1), X = A Z* + E*; Z0 = U(0,1)/n, E0 = L0 = 0."""
+    rank), Z*, E* Bernoulli(0.1)*N(0,1), X = A Z* + E*; Z0 = U(0,1)/n, E0 = L0 = 0.
+    cols = (c0, c1): keep only that column shard of the B-column batch (strong scaling: every rank
+    generates the same global batch and keeps its own columns)."""
     g = torch.Generator(device=dev)
     g.manual_seed(1126)
     A = torch.randn(m, n, generator=g, device=dev)
@@ -75,15 +91,43 @@ def synth(m, n, B, seed, dev):
                                                                         device=dev)
     X = (A @ zs + es).contiguous()
     Z0 = torch.rand(n, B, generator=g, device=dev) / n
+    del zs, es
+    if cols is not None:
+        c0, c1 = cols
+        X, Z0 = X[:, c0:c1].contiguous(), Z0[:, c0:c1].contiguous()
+        B = c1 - c0
     E0 = torch.zeros(m, B, device=dev)
     L0 = torch.zeros(m, B, device=dev)
-    del zs, es
     return A, X, Z0, E0, L0
 
 
-def cpu_baseline(m, n, K, B, variant="v4"):
-    """The oracle (CPU restatement of the reference forward, numpy fp32 + BLAS) on a bounded
-    sample of the same workload: B columns, median of 3 forwards after 1 warmup."""
+def host_info():
+    """CPU model, physical cores and the CPUs this process may run on (GPU box: a share)."""
+    model, phys = "unknown", set()
+    try:
+        cur = {}
+        for line in open("/proc/cpuinfo"):
+            if ":" not in line:
+                if cur:
+                    phys.add((cur.get("physical id"), cur.get("core id")))
+                cur = {}
+                continue
+            k, v = (x.strip() for x in line.split(":", 1))
+            cur[k] = v
+            if k == "model name":
+                model = v
+        if cur:
+            phys.add((cur.get("physical id"), cur.get("core id")))
+    except OSError:  # pragma: no cover
+        pass
+    return dict(cpu_model=model, physical_cores=len(phys), logical_cpus=os.cpu_count(),
+                cpus_allowed=len(os.sched_getaffinity(0)))
+
+
+def cpu_baseline(m, n, K, B, runs, variant="v4"):
+    """The oracle (CPU restatement of the reference forward, numpy fp32 + BLAS; the reference's
+    op sequence) on a bounded sample of the same workload: B columns (10,000), median
+    of `runs` forwards after 1 warmup.  `cores` = the BLAS threads that ran it."""
     from oracle import dladmm_oracle as oracle
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     import problems
@@ -98,14 +142,53 @@ def cpu_baseline(m, n, K, B, variant="v4"):
     args = (variant, inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd, K)
     oracle.forward(*args)
     ts = []
-    for _ in range(3):
+    for _ in range(runs):
         t0 = time.perf_counter()
         oracle.forward(*args)
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
+    h = host_info()
     return {"value": B / t, "unit": "samples/s", "cores": int(cores), "kind": "port",
-            "sample": f"oracle/dladmm_oracle.py {variant.upper()} forward, m={m} n={n} K={K}, B={B} columns, "
-                      f"fp32 numpy+BLAS, median of 3 after 1 warmup ({t*1e3:.0f} ms/forward)"}
+            "sample": f"oracle/dladmm_oracle.py {variant.upper()} forward, m={m} n={n} K={K}, "
+                      f"B={B} columns, fp32 numpy+BLAS ({cores} threads), median of {runs} after "
+                      f"1 warmup ({t*1e3:.0f} ms/forward)",
+            "host": h}
+
+
+def reduce_timing(elapsed, kern, world, dev):
+    """Max over ranks of the wall seconds and of the mean kernel seconds, plus every rank's mean
+    kernel seconds in rank order (one MAX all-reduce + one all-gather; nothing at N = 1)."""
+    if world == 1:
+        return elapsed, kern, [kern]
+    tt = torch.tensor([elapsed, kern], device=dev, dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    allk = [torch.zeros(1, device=dev, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(allk, torch.tensor([kern], device=dev, dtype=torch.float64))
+    return float(tt[0]), float(tt[1]), [float(x) for x in allk]
+
+
+class Workload:
+    """One benchmark workload on this rank: the model, its (shard of the) synthetic batch and the
+    timed step (forward + the [K, 2] all-reduce)."""
+
+    def __init__(self, dl, a, m, n, K, B_rank, B_global, cols, rank, dev, seed):
+        self.dl, self.a = dl, a
+        self.B, self.B_global = B_rank, B_global
+        gen_B = B_global if cols is not None else B_rank
+        A, X, Z0, E0, L0 = synth(m, n, gen_B, seed, dev, cols)
+        self.X = X
+        cls = {"v4": dl.DLADMMNetScalar, "v6": dl.DLADMMNetLasso}[a.variant]
+        torch.manual_seed(1126)   # SURVEY 8d: params seeded -> reproducible objective
+        self.net = cls(m=m, n=0, d=n, batch_size=B_rank, A=A, Z0=Z0, E0=E0, L0=L0, layers=K)
+        self.net.requires_grad_(False)
+        self.lk = dl._lib.LOSS_L1L1 if a.variant == "v4" else dl._lib.LOSS_LASSO
+        self.ddist = importlib.import_module("d-ladmm_amd.dist")
+
+    def step(self, keep_all, evpair=None):
+        r = self.net.run(self.X, keep_all=keep_all, loss_kind=self.lk, kernel_events=evpair)
+        # one RCCL all-reduce of the [K, 2] objective sums over xGMI (no-op at N = 1)
+        obj = self.ddist.global_objectives(r.loss_sums, self.a.alpha, self.B_global)
+        return r, obj
 
 
 def main():
@@ -123,35 +206,31 @@ def main():
     dev = torch.device("cuda", gpu if world > 1 else 0)
     torch.cuda.set_device(dev)
     dl = importlib.import_module("d-ladmm_amd")
+    ddist = importlib.import_module("d-ladmm_amd.dist")
 
-    m, n, K, B = a.m, a.n, a.layers, a.batch
-    A, X, Z0, E0, L0 = synth(m, n, B, rank, dev)
-    cls = {"v4": dl.DLADMMNetScalar, "v6": dl.DLADMMNetLasso}[a.variant]
-    net = cls(m=m, n=0, d=n, batch_size=B, A=A, Z0=Z0, E0=E0, L0=L0, layers=K)
-    net.precision = a.precision
-    lk = dl._lib.LOSS_L1L1 if a.variant == "v4" else dl._lib.LOSS_LASSO
-    net.requires_grad_(False)
+    m, n, K = a.m, a.n, a.layers
+    strong = a.global_batch > 0
     keep_all = not a.lean
+
+    def make(strong_b):
+        if strong_b:
+            c0, c1 = ddist.shard_columns(strong_b, rank, world)
+            return Workload(dl, a, m, n, K, c1 - c0, strong_b, (c0, c1), rank, dev, 0)
+        return Workload(dl, a, m, n, K, a.batch, a.batch * world, None, rank, dev, rank)
+
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.steps)]
     for e in ev:
         e.record()  # torch creates the hipEvent lazily; make the handles exist
     torch.cuda.synchronize()
 
-    ddist = importlib.import_module("d-ladmm_amd.dist")
-
-    def step(evpair=None):
-        r = net.run(X, keep_all=keep_all, loss_kind=lk, kernel_events=evpair)
-        # one RCCL all-reduce of the [K, 2] objective sums over xGMI (no-op at N = 1)
-        obj = ddist.global_objectives(r.loss_sums, a.alpha, B * world)
-        return r, obj
-
-    def timed(precision):
+    def timed(w, precision):
         """W untimed warmup steps, then exactly K timed steps between barrier + synchronize;
-        (max-over-ranks wall seconds, mean kernel seconds, objective)."""
-        net.precision = precision
+        (max-over-ranks wall seconds, max-over-ranks mean kernel seconds, every rank's mean
+        kernel seconds, objective)."""
+        w.net.precision = precision
         with torch.no_grad():
             for _ in range(a.warmup):
-                r, obj = step()
+                r, obj = w.step(keep_all)
                 del r
             torch.cuda.synchronize()
             if world > 1:
@@ -159,7 +238,7 @@ def main():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for i in range(a.steps):
-                r, obj = step((ev[2 * i], ev[2 * i + 1]))
+                r, obj = w.step(keep_all, (ev[2 * i], ev[2 * i + 1]))
                 del r
             torch.cuda.synchronize()
             if world > 1:
@@ -168,26 +247,26 @@ def main():
         elapsed = t1 - t0
         kern = float(np.mean([ev[2 * i].elapsed_time(ev[2 * i + 1])
                               for i in range(a.steps)])) * 1e-3
-        if world > 1:
-            tt = torch.tensor([elapsed, kern], device=dev, dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            elapsed, kern = float(tt[0]), float(tt[1])
-        return elapsed, kern, obj
+        elapsed, kern, kerns = reduce_timing(elapsed, kern, world, dev)
+        return elapsed, kern, kerns, obj
 
-    elapsed, kern_avg, obj = timed(a.precision)
+    w = make(a.global_batch if strong else 0)
+    B = w.B
+    elapsed, kern_avg, kerns, obj = timed(w, a.precision)
     # the same workload with the fp32 GEMMs on the f16 matrix cores (split-f16, same fp32
     # tolerance tests; tests/test_gpu_split.py), timed the same way beside the headline
     split = None
     if a.precision == "f32" and m <= 256 and n <= 512 and B % 4 == 0 and \
             os.environ.get("DLADMM_PATH", "")[:1] != "l" and not a.no_split:
-        s_el, s_kern, s_obj = timed("f32_split")
+        s_el, s_kern, _, s_obj = timed(w, "f32_split")
         # untimed: per-layer norm-relative distance of the split path's Z/E/L/T from the fp32
         # path's on this whole batch (max over layers and outputs)
         with torch.no_grad():
+            net = w.net
             net.precision = "f32"
-            rf = net.run(X, keep_all=keep_all, loss_kind=lk)
+            rf = net.run(w.X, keep_all=keep_all, loss_kind=w.lk)
             net.precision = "f32_split"
-            rs = net.run(X, keep_all=keep_all, loss_kind=lk)
+            rs = net.run(w.X, keep_all=keep_all, loss_kind=w.lk)
             dev_max = 0.0
             for name in ("Z", "E", "L", "T"):
                 tf, ts = getattr(rf, name), getattr(rs, name)
@@ -202,6 +281,17 @@ def main():
             net.precision = a.precision
         split = (s_el, s_kern, float(s_obj.cpu().numpy()[-1]), dev_max)
     obj = obj.cpu().numpy()
+    del w
+    # BASELINE config 3 (V4, 262,144 columns in total, batch-sharded) beside the weak headline
+    cfg3 = None
+    if not strong and not a.no_cfg3 and a.variant == "v4" and a.precision == "f32" and \
+            (m, n, K) == (256, 512, 15):
+        w3 = make(262144)
+        c_el, c_kern, c_kerns, c_obj = timed(w3, "f32")
+        cfg3 = dict(value=262144 * a.steps / c_el, ms_per_step=c_el / a.steps * 1e3,
+                    kern=c_kern, kerns=c_kerns, B=w3.B, obj=float(c_obj.cpu().numpy()[-1]))
+        del w3
+    torch.cuda.synchronize()
 
     if rank == 0:
         fused = (m <= 256 and n <= 512 and os.environ.get("DLADMM_PATH", "")[:1] != "l"
@@ -215,9 +305,10 @@ def main():
         kname = ({"fused": "dladmm::fused_kernel (one launch)",
                   "fused-split-f16": "dladmm::fused_x3_kernel (one launch)"}.get(path) or
                  f"dladmm::layer_kernel x {2 * K + 1} launches (timed together)")
-        total = B * world * a.steps
+        B_global = w_global = (a.global_batch if strong else B * world)
+        total = B_global * a.steps
         value = total / elapsed
-        flop = (4 * K + 2) * m * n * B                      # per launch (one rank's shard)
+        flop = (4 * K + 2) * m * n * B                      # per launch (rank 0's shard)
         achieved = flop / kern_avg  # noqa
         # algorithmic HBM bytes per sample (SURVEY 8d, V4 API-parity): inputs X,Z0,E0,L0 +
         # outputs Z,E,L (K layers) + T (K+1); weights (K+1)*m*n*4 per launch
@@ -233,6 +324,7 @@ def main():
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        scal = "strong" if strong else "weak"
         res = {
             "metric": METRIC,
             "value": value,
@@ -242,22 +334,25 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": elapsed / a.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scal,
             "vs_baseline": None,
             "dtype": {"f32": "f32",
                       "f32_split": "f32 (GEMMs: exact hi/lo f16 split, 3 f16 MFMA products, "
                                    "f32 accumulate)",
                       "bf16": "bf16 operands / f32 state"}[a.precision],
             "data": "synthetic (gen_syn_data.py distribution generated on device; reference-init "
-                    "V4 parameters, random W = 0.4(A^T + 1e-3 N))",
+                    f"{a.variant.upper()} parameters after torch.manual_seed(1126), "
+                    "W = 0.4(A^T + 1e-3 N))",
             "config": {
-                "workload": f"{net.name()} ({a.variant.upper()}) forward m={m} n={n} K={K} "
-                            f"B={B}/GPU, all layers' Z/E/L/T written"
+                "workload": f"{w_net_name(dl, a)} ({a.variant.upper()}) forward m={m} n={n} "
+                            f"K={K} " + (f"B={B_global} global, {B}/GPU (strong scaling)"
+                                         if strong else f"B={B}/GPU")
+                            + f", all layers' Z/E/L/T written"
                             f"{'' if keep_all else ' (lean: last only)'} + fused per-layer "
                             f"{'L1L1' if a.variant == 'v4' else 'LASSO'} objective",
                 "variant": a.variant, "m": m, "n": n, "layers": K, "batch_per_gpu": B,
                 "path": path,
-                "global_batch": B * world, "keep_all": keep_all,
+                "global_batch": w_global, "keep_all": keep_all,
                 "parallelism": f"batch-shard dp{world} (one RCCL all-reduce of [K,2] sums)",
             },
             "roofline": {
@@ -275,6 +370,8 @@ def main():
             },
             "objective_last_layer": float(obj[-1]),
         }
+        if world > 1:
+            res["per_rank_kernel_ms"] = [k * 1e3 for k in kerns]
         if split is not None:
             s_el, s_kern, s_objl, s_dev = split
             s_peak = PEAK_BF16_MFMA / 3
@@ -297,11 +394,35 @@ def main():
                 "max_rel_dev_note": "max over layers of ||X_split - X_f32|| / ||X_f32|| for X in "
                                     "Z, E, L, T on this batch (parity tolerance: 1e-5)",
             }
+        if cfg3 is not None:
+            f3 = (4 * K + 2) * m * n * cfg3["B"]
+            res["cfg3_strong"] = {
+                "workload": f"BASELINE config 3: V4 forward m={m} n={n} K={K}, B=262144 global "
+                            f"batch-sharded over {world} GPU(s) ({cfg3['B']}/GPU), all layers "
+                            "written + fused L1L1 objective, one RCCL all-reduce of [K,2] sums",
+                "scaling": "strong",
+                "value": cfg3["value"],
+                "unit": "samples/s",
+                "ms_per_step": cfg3["ms_per_step"],
+                "kernel_ms_max_over_ranks": cfg3["kern"] * 1e3,
+                "per_rank_kernel_ms": [k * 1e3 for k in cfg3["kerns"]],
+                "efficiency_within_run": (sum(cfg3["kerns"]) / world) / (cfg3["ms_per_step"]
+                                                                         * 1e-3),
+                "efficiency_note": "mean per-rank kernel time / wall time per step (1.0 = the "
+                                   "step is all kernel; the driver computes scaling efficiency "
+                                   "across N itself)",
+                "roofline_frac": f3 / cfg3["kern"] / PEAK_F32_MFMA,
+                "objective_last_layer": cfg3["obj"],
+            }
         if world == 1 and not a.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(m, n, K, a.cpu_batch, a.variant)
+            res["cpu_baseline"] = cpu_baseline(m, n, K, a.cpu_batch, a.cpu_runs, a.variant)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def w_net_name(dl, a):
+    return {"v4": dl.DLADMMNetScalar, "v6": dl.DLADMMNetLasso}[a.variant].NAME
 
 
 if __name__ == "__main__":

@@ -6,12 +6,14 @@ identifier) or put the repo root on sys.path and use the same call.
 from . import _lib  # noqa: F401
 from . import dist  # noqa: F401
 from .model import (DLADMMNet, DLADMMNetFull, DLADMMNetLasso, DLADMMNetLTheta,  # noqa: F401
-                    DLADMMNetScalar, DLADMMNetScalarTied, VARIANTS, load_checkpoint)
+                    DLADMMNetScalar, DLADMMNetScalarSl2, DLADMMNetScalarTied,
+                    DLADMMNetScalarZ0, VARIANTS, load_checkpoint)
 from .model import DLADMMNetNewS, DLADMMNetPTiedNewS, DLADMMNetTiedNewS  # noqa: F401
 from .lskm import DLADMMNetLSKM  # noqa: F401
 from .ops import BackwardResult, ForwardResult, dladmm_backward, dladmm_forward  # noqa: F401
 
 __all__ = ["DLADMMNet", "DLADMMNetLTheta", "DLADMMNetFull", "DLADMMNetScalar",
+           "DLADMMNetScalarSl2", "DLADMMNetScalarZ0",
            "DLADMMNetScalarTied", "DLADMMNetLasso", "DLADMMNetNewS", "DLADMMNetTiedNewS",
            "DLADMMNetPTiedNewS", "DLADMMNetLSKM", "VARIANTS", "load_checkpoint",
            "dladmm_forward", "dladmm_backward", "ForwardResult", "BackwardResult"]

@@ -15,7 +15,6 @@ LIB_PATH = os.environ.get("DLADMM_LIB") or os.path.join(HERE, "lib", "libdladmm_
 ABI_VERSION = 5
 PREC_F32, PREC_BF16, PREC_F32_SPLIT = 0, 1, 2
 MAX_LAYERS = 65536
-MAX_LAYERS_V1 = 64
 NSCALAR = 8
 
 # enum dladmm_variant

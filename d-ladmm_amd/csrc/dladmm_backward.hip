@@ -93,19 +93,13 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
   // |U| > theta_z, so the forward's own Z_k gives S'(U) (and the objective's sign(Z_k)); then
   // q = W_k Var_k is needed only for a trainable step s1 (V5) -- host: zk_mask -- and for
   // theta_z < 0 (both relus open), where the second GEMM still runs
-  bool zmask = PH == 5;
-  if constexpr (PH == 2 && PKIND != PK_ROW)
-    zmask = a.zk_mask && ((cfloat_p)a.scal)[k * DLADMM_NSCALAR + DLADMM_P_THETA_Z] >= 0.0f;
+  // (the PH 2 launch of a zk_mask layer reaches here only with theta_z < 0: it forms q)
+  constexpr bool zmask = PH == 5;
   f32x4 acc2[PH == 2 ? SB : 1];
   if constexpr (PH == 5) {
     acc2[0] = f32x4{0.f, 0.f, 0.f, 0.f};
   } else if constexpr (PH == 2) {
-    if (!zmask) {
-      slice_gemm<NW, SB, NSB>(ring, a.Wp2, a.MBp, ib0, a.KB, a.S2, a.ldS2, a.Krows, a.B, acc2);
-    } else {
-#pragma unroll
-      for (int i = 0; i < SB; ++i) acc2[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    slice_gemm<NW, SB, NSB>(ring, a.Wp2, a.MBp, ib0, a.KB, a.S2, a.ldS2, a.Krows, a.B, acc2);
   }
 
   cfloat_p sp = (cfloat_p)a.scal + k * DLADMM_NSCALAR;

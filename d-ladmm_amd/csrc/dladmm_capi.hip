@@ -212,6 +212,7 @@ struct Plan {
   int nbp;     // bf16 path: 16-column blocks of the packed state
   bool narrow;  // bf16 path: 128-column tiles (two workgroups per CU)
   size_t off_ap, off_wp, off_v, off_zb, off_zw, off_ew, off_lw, off_loss, total;
+  size_t off_btab;            // path 1, V1: device tables of the per-layer beta pointers
   size_t off_wexp, off_umax;  // path 4
   int64_t ldzw;               // path 4: lean-mode Z_k workspace row stride
 };
@@ -222,7 +223,6 @@ inline int validate(const dladmm_fwd_desc* d) {
   if (d->variant < DLADMM_V1_LENA || d->variant > DLADMM_V6_LASSO) return DLADMM_E_VARIANT;
   if (d->m < 1 || d->n < 1 || d->batch < 1) return DLADMM_E_SHAPE;
   if (d->layers < 1 || d->layers > DLADMM_MAX_LAYERS) return DLADMM_E_LAYERS;
-  if (d->variant == DLADMM_V1_LENA && d->layers > DLADMM_MAX_LAYERS_V1) return DLADMM_E_LAYERS;
   if (d->loss_kind < 0 || d->loss_kind > 2) return DLADMM_E_UNSUPPORTED;
   if (!d->X || !d->A || !d->Z0 || !d->E0 || !d->L0 || !d->W || !d->Z || !d->E || !d->L)
     return DLADMM_E_NULL;
@@ -322,7 +322,9 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
     p->off_ap = 0;
     p->off_wp = align256(frag_bytes);
     p->off_loss = p->off_wp + align256(frag_bytes * (shared_weight(d) ? 1 : K));
-    p->total = p->off_loss + align256((size_t)2 * K * p->nslots * sizeof(float));
+    p->off_btab = p->off_loss + align256((size_t)2 * K * p->nslots * sizeof(float));
+    p->total = p->off_btab +
+               (d->variant == DLADMM_V1_LENA ? align256((size_t)2 * K * sizeof(void*)) : 0);
     return 0;
   }
   // per-layer path; path 3 = bf16 operands: 2-D tiles of 256 x 256, k-blocks of 32
@@ -416,8 +418,20 @@ inline int run_fused(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStrea
   a.scal = d->scalar_params;
   a.rowp = d->row_params; a.rstride = d->row_stride;
   a.ldb = d->ld_beta;
-  if (d->variant == DLADMM_V1_LENA)
-    for (int k = 0; k < d->layers; ++k) { a.b1e[k] = d->beta1_elem[k]; a.b2e[k] = d->beta2_elem[k]; }
+  if (d->variant == DLADMM_V1_LENA) {
+    // the K per-layer beta pointers of each table go to the workspace (no depth limit); the
+    // host array is staged by the runtime before hipMemcpyAsync returns
+    const float** tab = (const float**)(ws + p.off_btab);
+    const size_t K = (size_t)d->layers;
+    if (hipError_t e = hipMemcpyAsync(tab, d->beta1_elem, K * sizeof(void*),
+                                      hipMemcpyHostToDevice, s))
+      return (int)e;
+    if (hipError_t e = hipMemcpyAsync(tab + K, d->beta2_elem, K * sizeof(void*),
+                                      hipMemcpyHostToDevice, s))
+      return (int)e;
+    a.b1t = tab;
+    a.b2t = tab + K;
+  }
   a.Zo = d->Z; a.Eo = d->E; a.Lo = d->L; a.To = d->T; a.ldo = d->ld_out;
   a.lossp = lossp;
   a.dbg = dbg_ptr();  // diagnostic builds (DLADMM_STAMP) write per-wave cycle sums here

@@ -453,9 +453,9 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
 #endif
     if constexpr (PKIND == PK_ELEM) {
       const uint32_t eb = (uint32_t)(m * a.ldb * 4);
-      const rsrc_t r1 = mkrsrc(pro ? nullptr : a.b1e[k], pro ? 0u : eb);
-      const rsrc_t r2 = pro ? mkrsrc(a.E0, (uint32_t)(m * a.lde0 * 4)) : mkrsrc(a.b2e[k], eb);
-      const rsrc_t rn = mkrsrc(k + 1 < K ? a.b1e[k + 1] : nullptr, k + 1 < K ? eb : 0u);
+      const rsrc_t r1 = mkrsrc(pro ? nullptr : a.b1t[k], pro ? 0u : eb);
+      const rsrc_t r2 = pro ? mkrsrc(a.E0, (uint32_t)(m * a.lde0 * 4)) : mkrsrc(a.b2t[k], eb);
+      const rsrc_t rn = mkrsrc(k + 1 < K ? a.b1t[k + 1] : nullptr, k + 1 < K ? eb : 0u);
       const uint32_t so = bw.at(r);
       pb[h][0][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r1, (int)vb, (int)so, 0));
       pb[h][1][r] = pro ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r2, (int)ve, (int)ew.at(r), 0))

@@ -23,8 +23,9 @@ struct FusedArgs {
   const float* scal; // [K][8]
   const float* rowp; int64_t rstride;  // [K][8][rstride]
   int64_t ldb;
-  const float* b1e[DLADMM_MAX_LAYERS_V1];
-  const float* b2e[DLADMM_MAX_LAYERS_V1];
+  // V1 per-sample betas: device tables of the K layer pointers (workspace), any depth
+  const float* const* b1t;
+  const float* const* b2t;
   float* Zo; float* Eo; float* Lo; float* To; int64_t ldo;
   float* Po;         // training: A Z_k of every layer [K][m][ldo] (the SAVEP instantiations)
   float* lossp;      // [K][2][ldl] per-column objective terms
@@ -131,8 +132,11 @@ struct BwdArgs {
   const float* Tk; int64_t ldt;    // T_k
   const float* Pk;                 // BK1 with the forward's saved A Z_k (row stride ldt)
   const float* Zk; int64_t ldzk;   // BK2: the forward's Z_k (its shrink mask, zk_mask)
-  int zk_mask;                     // BK2: 1 = no parameter scales W_k Var_k (s1), so with
-                                   // theta_z >= 0 the mask comes from Z_k and q is not formed
+  int zk_mask;                     // BK2: 2 = no parameter scales W_k Var_k (s1): the layer
+                                   // runs a PH 5 launch (theta_z >= 0: the mask comes from Z_k,
+                                   // q = W_k Var_k is not formed) beside a PH 2 launch (theta_z
+                                   // < 0), each exiting unless theta_z's sign is its case; 0 =
+                                   // PH 2 only
   const float* gZ; const float* gE; const float* gL; const float* gT; int64_t ldg;  // upstream
   int loss_kind; const float* lcoef;  // fused training objective: device [K][2] (cz_k, cf_k)
   float* AZ; float* AE; float* AL; float* AT; float* GP; float* VAR; int64_t ldw;   // workspace

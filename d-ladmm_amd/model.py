@@ -8,6 +8,8 @@ each script):
   DLADMMNetLTheta      V2  main_syn_l1l1_ltheta.py:16-95  beta (m,1), thetas (d,1)/(m,1)
   DLADMMNetFull        V3  main_syn_l1l1_full.py:16-96    per-row beta1/2/3, ss2, thetas
   DLADMMNetScalar      V4  main_syn_l1l1_scalar.py:34-131 all (1,1); returns (Z, E, L, T)
+  DLADMMNetScalarSl2 / DLADMMNetScalarZ0: V4 of main_syn_l1l1-sl2_scalar.py / _scalar_z0.py
+                           (same body; name() "DLADMMNet")
   DLADMMNetScalarTied  V5  main_syn_l1l1_scalar_tied.py:34-104 one shared fc + ss1[k]
   DLADMMNetLasso       V6  main_syn_lasso_scalar.py:17-118 linear LASSO E-step
 
@@ -202,7 +204,9 @@ class _DLADMMBase(nn.Module):
             raise ValueError(f"dladmm: unknown loss kind {kind!r}")
         if cols is not None:
             cols = (int(cols[0]), int(cols[1]))
-            if not (0 <= cols[0] < cols[1] <= self.Z0.shape[1]) or \
+            # an empty shard (c0 == c1: dist.shard_columns when the batch has fewer columns
+            # than ranks) is valid: it contributes zero, and its rank still joins the collectives
+            if not (0 <= cols[0] <= cols[1] <= self.Z0.shape[1]) or \
                     x.shape[1] != cols[1] - cols[0]:
                 raise ValueError(f"dladmm: cols {cols} do not match x {tuple(x.shape)} and the "
                                  f"model's batch of {self.Z0.shape[1]} columns")
@@ -227,10 +231,12 @@ class _DLADMMBase(nn.Module):
         return self.Z0[:, c0:c1], self.E0[:, c0:c1], self.L0[:, c0:c1]
 
     def _run_shard(self, x, cols, **kw):
-        """Forward of every layer on the column shard `cols` (None: the whole batch)."""
+        """Forward of every layer on the column shard `cols` (None: the whole batch), at the
+        module's precision unless `precision=` is given."""
         dev = self.A.device
         Z0, E0, L0 = self._init_state(cols)
         W = [w.detach() for w in self._weights()]
+        kw.setdefault("precision", self.precision)
         return dladmm_forward(self.VARIANT, x, self.A, W, Z0, E0, L0, keep_all=True,
                               **kw, **self._tables(dev, cols))
 
@@ -578,6 +584,17 @@ class DLADMMNetScalar(_DLADMMBase):
                                the=self.active_para1, thz=self.active_para, s1=1.0)}
 
 
+class DLADMMNetScalarSl2(DLADMMNetScalar):
+    """V4 as main_syn_l1l1-sl2_scalar.py:17-114 carries it: the same body, but name() returns
+    "DLADMMNet" (:113-114), the stem of that script's checkpoints."""
+    NAME = "DLADMMNet"
+
+
+class DLADMMNetScalarZ0(DLADMMNetScalar):
+    """V4 as main_syn_l1l1_scalar_z0.py:17-114 carries it (name() "DLADMMNet", :113-114)."""
+    NAME = "DLADMMNet"
+
+
 class DLADMMNetScalarTied(DLADMMNetScalar):
     """V5, main_syn_l1l1_scalar_tied.py:34-104: one shared fc scaled by ss1[k]."""
     VARIANT = _lib.V5_TIED
@@ -707,7 +724,8 @@ class DLADMMNetPTiedNewS(DLADMMNetTiedNewS):
 
 VARIANTS = {
     "v1": DLADMMNet, "v2": DLADMMNetLTheta, "v3": DLADMMNetFull,
-    "v4": DLADMMNetScalar, "v5": DLADMMNetScalarTied, "v6": DLADMMNetLasso,
+    "v4": DLADMMNetScalar, "v4_sl2": DLADMMNetScalarSl2, "v4_z0": DLADMMNetScalarZ0,
+    "v5": DLADMMNetScalarTied, "v6": DLADMMNetLasso,
     "v7": DLADMMNetNewS, "v7t": DLADMMNetTiedNewS, "v7p": DLADMMNetPTiedNewS,
 }
 

@@ -56,9 +56,8 @@ def _fill_fwd_desc(d, variant, X, A, W, Z0, E0, L0, scalar_params, row_params, b
         raise RuntimeError(
             "dladmm: Z0/E0/L0 shapes do not broadcast with X: "
             f"Z0 {tuple(Z0.shape)}, E0 {tuple(E0.shape)}, L0 {tuple(L0.shape)}, X {tuple(X.shape)}")
-    kmax = _lib.MAX_LAYERS_V1 if variant == _lib.V1_LENA else _lib.MAX_LAYERS
-    if not 1 <= K <= kmax:
-        raise ValueError(f"dladmm: layers must be in [1, {kmax}], got {K}")
+    if not 1 <= K <= _lib.MAX_LAYERS:
+        raise ValueError(f"dladmm: layers must be in [1, {_lib.MAX_LAYERS}], got {K}")
     Ws = [_f32_dev(w if w.dim() == 2 and w.stride(1) == 1 else w.contiguous(), f"W[{k}]")
           for k, w in enumerate(W)]
     ldw = Ws[0].stride(0)
@@ -304,19 +303,29 @@ def dladmm_backward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[
     return BackwardResult(gWo, g_scalar, g_row, g1, g2)
 
 
-_WS = {}
+_WS: "OrderedDict" = None
+_WS_PER_DEVICE = 4   # streams whose workspace stays cached per device (least recently used out)
 
 
 def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
     """Cached workspace per (device, stream), grown on demand (torch's allocator keeps it 256-B
     aligned).  Reuse is safe because it is stream-ordered: a buffer is only ever used by calls
     enqueued on the stream it was allocated on, so two streams of one device (say overlapping
-    eval and training) never share scratch memory, and a buffer dropped when it grows goes back
-    to the caching allocator under the one stream that used it."""
+    eval and training) never share scratch memory, and a buffer dropped when it grows -- or when
+    its stream falls out of the cache -- goes back to the caching allocator under the one stream
+    that used it.  At most _WS_PER_DEVICE streams per device keep a buffer (least recently used
+    evicted), so code that makes a new stream per pass does not grow memory without bound."""
+    global _WS
+    from collections import OrderedDict
+    if _WS is None:
+        _WS = OrderedDict()
     stream = torch.cuda.current_stream(dev)
     key = (dev.type, dev.index, stream.cuda_stream)
-    buf = _WS.get(key)
+    buf = _WS.pop(key, None)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(nbytes, 1), device=dev, dtype=torch.uint8)
-        _WS[key] = buf
+    _WS[key] = buf   # most recently used last
+    same = [k for k in _WS if k[:2] == key[:2]]
+    for k in same[:-_WS_PER_DEVICE]:
+        del _WS[k]
     return buf

@@ -30,8 +30,7 @@ extern "C" {
 #endif
 
 #define DLADMM_ABI_VERSION 5
-#define DLADMM_MAX_LAYERS 65536   /* K limit (V4-V6; e.g. the K=2000 KM ground-truth iteration) */
-#define DLADMM_MAX_LAYERS_V1 64   /* V1: per-layer per-sample beta pointer tables */
+#define DLADMM_MAX_LAYERS 65536   /* K limit, every variant (e.g. the K=2000 KM ground-truth run) */
 
 /* Reference variants (class DLADMMNet of the named reference script). */
 enum dladmm_variant {
@@ -219,7 +218,11 @@ typedef struct dladmm_bwd_desc {
   /* outputs (device) */
   float* gW; int64_t ld_gw;   /* [K][n][ld_gw], or [1][n][ld_gw] when gw_sum */
   double* g_scalar;           /* V4-V6: [K][DLADMM_NSCALAR] per-slot grads (slots the variant
-                                 does not use are 0; V1: unused) */
+                                 does not use are 0; V1: unused).  Slot DLADMM_P_S1 (the step
+                                 scaling W_k Var_k) is defined for the tied variant (V5) only:
+                                 for the others s1 is the constant 1 and the slot is unspecified
+                                 (0 on layers with theta_z >= 0, where q = W_k Var_k is not
+                                 formed) */
   double* g_row;              /* V2/V3: [K][DLADMM_NSCALAR][fwd.row_stride] per-row grads */
   float* const* g_beta1_elem; /* V1: host arrays of K device pointers, (m x fwd.ld_beta) each: */
   float* const* g_beta2_elem; /*     grads of the per-sample beta1[k] / beta2[k]              */

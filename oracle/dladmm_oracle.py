@@ -39,7 +39,7 @@ def self_active(x, theta):
     return np.maximum(x - theta, 0) - np.maximum(-1.0 * x - theta, 0)
 
 
-_GEMM = None  # None: fp32 BLAS as the reference; "bf16": see round_bf16 / forward(gemm=...)
+_GEMM = None  # None: fp32 BLAS as the reference; "bf16" / "bf16_acc32": see _mm
 
 
 def round_bf16(x):
@@ -51,16 +51,21 @@ def round_bf16(x):
 
 def _mm(a, b):
     """The GEMMs of the forward: fp32 (reference) or, for the bf16 operand mode of BASELINE
-    config 5, both operands rounded to bf16 and the product accumulated in fp64, stored fp32."""
+    config 5, both operands rounded to bf16 and the product accumulated in fp64, stored fp32
+    ("bf16"), or accumulated in fp32 ("bf16_acc32": a second valid implementation of the same
+    arithmetic, whose distance from "bf16" measures how far accumulation order alone moves the
+    result -- the bf16 parity bar's yardstick d_k, tests/test_gpu_bf16.py)."""
     if _GEMM == "bf16":
         return (round_bf16(a).astype(np.float64) @ round_bf16(b).astype(np.float64)).astype(
             np.float32)
+    if _GEMM == "bf16_acc32":
+        return round_bf16(a) @ round_bf16(b)
     return a @ b
 
 
 def _fc(W, Var):
     """nn.Linear(m, d, bias=False) applied as fc[k](Var.t()).t()  (main_lena.py:72)."""
-    if _GEMM == "bf16":
+    if _GEMM in ("bf16", "bf16_acc32"):
         return _mm(W, Var)
     return (Var.T @ W.T).T
 
@@ -100,7 +105,7 @@ def forward_news(variant, X, A, Z0, E0, L0, p, K, dtype):
 def forward(variant, X, A, Z0, E0, L0, state_dict, layers, dtype=np.float32, gemm=None):
     """Run the reference forward of `variant` ('v1'..'v7p'); returns dict(Z, E, L[, T]) of lists.
     gemm="bf16" restates the bf16-operand mode (BASELINE config 5) instead of the reference's
-    fp32 GEMMs."""
+    fp32 GEMMs ("bf16_acc32": the same with fp32 accumulation)."""
     global _GEMM
     prev, _GEMM = _GEMM, gemm
     try:

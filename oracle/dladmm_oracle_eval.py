@@ -4,10 +4,10 @@ ONLY.  Only tests/ may import it, as the checker.
 Each function restates, in numpy fp64, the per-batch accumulation of one objective of
 /root/reference/test_syn_l1l1_scalar.py:436-489 (and test_syn_lasso_scalar.py:477-503), literally
 with the product A @ Z_k, and returns the per-layer batch sums the reference adds into its
-accumulators.  Parity note: the reference runs these formulas as inline module-level code of its
-scripts (no function to call), so this restatement is checked against the formulas' text and
-against independent numpy evaluations in tests/test_gpu_eval.py -- "parity unpinned" in the
-sense of tests/golden: there is no reference-executed fixture for it.
+accumulators.  Pinned: tests/test_oracle_eval.py checks every function against fixtures that
+EXECUTED the reference scripts' own objective statements (tests/golden/make_golden_eval.py:
+test_syn_l1l1_scalar.py:450-604 and test_syn_lasso_scalar.py:446-568, ast-extracted and run on
+the scripts' own model class), tests/golden/eval_*.npz.
 """
 from __future__ import annotations
 

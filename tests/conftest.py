@@ -61,3 +61,15 @@ def load_golden(name):
     g = np.load(os.path.join(GOLDEN, name + ".npz"))
     meta = json.loads(str(g["meta"]))
     return g, meta
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """DLADMM_PARITY_JSON=<path>: write every error the parity tests checked (tests/parity.py)."""
+    path = os.environ.get("DLADMM_PARITY_JSON")
+    if not path:
+        return
+    import parity
+    if parity.LOG:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(parity.LOG, f)

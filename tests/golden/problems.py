@@ -282,3 +282,47 @@ LSKM_FIXTURES = {
                                mu_param=0.3),
     "lskm_sg_med": _lskm(_LM, 5, 5, True, True, delta=0.0, mu="EMA", mu_param=0.5),
 }
+
+
+# ---------------------------------------------------------------- evaluation objectives (row f3)
+# name -> test-script evaluation case (make_golden_eval.py executes the script's own objective
+# statements on the script's own model class): the script, the objectives it supports, the learned
+# parameter set (variant, perturbation, weight scale), the batch loop (batch_size x n_batches test
+# columns), alpha and the ground-truth KM depth (0: the script has no ground truth).
+EVAL_FIXTURES = {
+    "eval_l1l1": dict(script="test_syn_l1l1_scalar.py", variant="v4",
+                      objectives=["NMSE", "L1L1", "Normalized-L1L1", "GT", "Normalized-GT",
+                                  "S-L2"],
+                      m=64, n=128, batch_size=20, n_batches=3, layers=5, alpha=0.01, gt_K=2000,
+                      seed=1180, perturb=0.1, wscale=0.4),
+    "eval_lasso": dict(script="test_syn_lasso_scalar.py", variant="v6",
+                       objectives=["NMSE", "L1L1", "LASSO", "LASSO-ALL"],
+                       m=64, n=128, batch_size=20, n_batches=3, layers=6, alpha=0.05, gt_K=0,
+                       seed=1181, perturb=0.1, wscale=0.4),
+}
+
+
+def eval_problem(c: dict):
+    """Inputs (n_batches * batch_size test columns) and parameter set of an evaluation case; the
+    model's initial iterates are (., batch_size), as the test scripts build them
+    (test_syn_l1l1_scalar.py:422-424)."""
+    B = c["batch_size"] * c["n_batches"]
+    d = dict(variant=c["variant"], m=c["m"], n=c["n"], B=B, K=c["layers"], seed=c["seed"],
+             perturb=c["perturb"], wscale=c["wscale"])
+    inp, sd = build_problem(d)
+    bs = c["batch_size"]
+    for k in ("Z0", "E0", "L0"):
+        inp[k] = np.ascontiguousarray(inp[k][:, :bs])
+    return inp, sd
+
+
+# ---------------------------------------------------------------- bf16 operand mode (config 5)
+# name -> problem definition run through the reference classes with bf16-operand GEMMs
+# (make_golden_bf16.py); config-5 shape (m=1024, n=4096, K=15) at a few columns.
+BF16_FIXTURES = {
+    "bf16_v4": dict(variant="v4", m=96, n=200, B=24, K=6, seed=9310, perturb=0.1),
+    "bf16_v6": dict(variant="v6", m=96, n=200, B=24, K=6, seed=9311, perturb=0.1),
+    "bf16_v1": dict(variant="v1", m=96, n=200, B=24, K=6, seed=9312, perturb=0.1, wscale=0.4),
+    "bf16_v3": dict(variant="v3", m=96, n=200, B=24, K=6, seed=9313, perturb=0.1),
+    "bf16_cfg5": dict(variant="v4", m=1024, n=4096, B=3, K=15, seed=9314, perturb=0.1),
+}

@@ -128,3 +128,80 @@ def test_allreduce_grads_world2():
     for _, w, b in res:
         np.testing.assert_array_equal(w, np.full((3, 4), 3.0))
         np.testing.assert_array_equal(b, np.full((1, 1), 30.0))
+
+
+def _strong_worker(rank, world, port, q):
+    """bench.py's strong-scaling plumbing on one rank: its dist.shard_columns span of the global
+    batch (synth(..., cols=...)), the shard's objective sums (oracle), the ONE all-reduce
+    (global_objectives) and the max-over-ranks timing reduction (reduce_timing)."""
+    import importlib
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests", "golden"))
+    import bench
+    import problems
+    from oracle import dladmm_oracle as oracle
+    ddist = importlib.import_module("d-ladmm_amd.dist")
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m, n, Bg, K, alpha = 24, 48, 41, 3, 0.001
+    c0, c1 = ddist.shard_columns(Bg, rank, world)
+    A, X, Z0, E0, L0 = (t.numpy() for t in bench.synth(m, n, Bg, 0, "cpu", (c0, c1)))
+    sd = problems.make_state_dict("v4", m, n, 1, K, A, 5, perturb=0.1)
+    out = oracle.forward("v4", X, A, Z0, E0, L0, sd, K)
+    sums = torch.zeros(K, 2, dtype=torch.float64)
+    for k in range(K):
+        Zk = out["Z"][k].astype(np.float64)
+        sums[k, 0] = float(np.abs(Zk).sum())
+        sums[k, 1] = float(np.abs(X.astype(np.float64) - A.astype(np.float64) @ Zk).sum())
+    obj = ddist.global_objectives(sums, alpha, Bg)
+    el, kern, kerns = bench.reduce_timing(1.0 + rank, 0.5 * (rank + 1), world, "cpu")
+    q.put((rank, (c0, c1), obj.numpy(), (el, kern, kerns)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_strong_scaling_plumbing():
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests", "golden"))
+    import bench
+    import problems
+    from oracle import dladmm_oracle as oracle
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_strong_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    m, n, Bg, K, alpha = 24, 48, 41, 3, 0.001
+    A, X, Z0, E0, L0 = (t.numpy() for t in bench.synth(m, n, Bg, 0, "cpu"))
+    sd = problems.make_state_dict("v4", m, n, 1, K, A, 5, perturb=0.1)
+    full = oracle.forward("v4", X, A, Z0, E0, L0, sd, K)
+    ref = oracle.layer_objectives(full["Z"], X, A, alpha, "l1l1")
+    assert [r[1] for r in res] == [(0, 21), (21, 41)]   # the two spans tile the global batch
+    for _, _, obj, (el, kern, kerns) in res:
+        np.testing.assert_allclose(obj, ref, rtol=1e-6)  # every rank sees the global objective
+        assert (el, kern) == (2.0, 1.0) and kerns == [0.5, 1.0]   # max over ranks; rank order
+
+
+def test_bench_synth_shard_is_global_slice():
+    """Strong scaling generates the same global batch on every rank and keeps its columns: a
+    shard equals the columns of the whole batch."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    full = bench.synth(16, 32, 50, 0, "cpu")
+    part = bench.synth(16, 32, 50, 0, "cpu", (13, 29))
+    assert torch.equal(full[0], part[0])
+    for f, p in zip(full[1:], part[1:]):
+        assert torch.equal(f[:, 13:29], p)

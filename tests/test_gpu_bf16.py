@@ -9,6 +9,13 @@ bf16 restatement (it tracks the bf16 algorithm, not just "something near fp32") 
 1.25 s_k of the fp32 reference.  The slack covers the fp32 MFMA accumulation order and the
 state elements whose bf16 rounding falls on the other side of a rounding boundary when the
 fp32 state differs in its last bits.
+
+Where the iteration amplifies rounding (the config-5 shape m=1024, n=4096 at depth 15: s_k grows
+to 0.11), those boundary flips compound: two valid bf16 implementations that differ only in the
+accumulation order drift apart by d_k (~0.3 s_k by layer 15; measured on the reference itself,
+tests/golden/make_golden_bf16.py).  `bf16_bar` therefore allows max(0.25 s_k, 2 d_k) from the bf16
+reference and s_k + that from the fp32 reference (the triangle inequality); on the small shapes
+d_k ~ 0 and the bar is the 0.25 / 1.25 s_k one.
 """
 import numpy as np
 import pytest
@@ -25,6 +32,12 @@ def tile(request, monkeypatch):
     two workgroups per CU; DLADMM_BF16_TILE is read by the C ABI at every call)."""
     monkeypatch.setenv("DLADMM_BF16_TILE", request.param)
     return request.param
+
+
+def bf16_bar(s, d):
+    """(bound vs the bf16 reference, bound vs the fp32 reference) for yardsticks s_k, d_k."""
+    b = max(1e-5, 0.25 * s, 2.0 * d)
+    return b, 1e-5 + max(1.25 * s, s + b)
 
 
 def nrel(a, b):
@@ -162,3 +175,32 @@ def test_bf16_tile_widths_bit_identical(dl, monkeypatch):
         assert torch.equal(x, y)
     # the per-column partials are summed in a fixed order per slot; the slot layout is the same
     np.testing.assert_allclose(a.loss_sums.cpu().numpy(), b.loss_sums.cpu().numpy(), rtol=1e-6)
+
+
+@pytest.mark.parametrize("name", sorted(P.BF16_FIXTURES))
+def test_bf16_matches_reference_bf16_gemms(name, dl):
+    """Against the reference classes themselves run with bf16-operand GEMMs (exact accumulation,
+    fp32 state; tests/golden/make_golden_bf16.py) and unmodified in fp32, at bf16_bar with the
+    fixture's own yardsticks.  The config-5 fixture (m=1024, n=4096, K=15) runs its full depth."""
+    from conftest import load_golden
+    import parity
+    g, meta = load_golden(name)
+    d = meta["defn"]
+    inp, sd = P.build_problem(d)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+    net = dl.VARIANTS[d["variant"]](m=d["m"], n=0, d=d["n"], batch_size=d["B"], A=t(inp["A"]),
+                                    Z0=t(inp["Z0"]), E0=t(inp["E0"]), L0=t(inp["L0"]),
+                                    layers=d["K"])
+    net.load_state_dict({k: t(v) for k, v in sd.items()})
+    net.requires_grad_(False)
+    net.precision = "bf16"
+    with torch.no_grad():
+        out = net(t(inp["X"]).cuda())
+    for i, nm in enumerate("ZELT"[:len(out)]):
+        for k in range(g[nm].shape[0]):
+            got = out[i][k].cpu().numpy()
+            s, dk = float(g["s_" + nm][k]), float(g["d_" + nm][k])
+            b_bf, b_32 = bf16_bar(s, dk)
+            parity.check(name, "bf16", f"{nm}[{k}] vs ref-bf16", nrel(got, g[nm][k]), b_bf, s)
+            parity.check(name, "bf16", f"{nm}[{k}] vs ref-f32", nrel(got, g["f32_" + nm][k]),
+                         b_32, s)

@@ -1,0 +1,220 @@
+"""Every BASELINE.json config's workload, at its stated size, on the GPU.
+
+  cfg1  main_lena.py V1, m=64 n=256 K=5 B=20, default init   -> golden fixture v1_lena_cfg1
+  cfg2  V4 m=256 n=512 K=15 B=10,000 (ragged last tile)      -> column subset vs the oracle
+  cfg3  V4 m=256 n=512 K=15 B=262,144 batch-sharded          -> the whole batch on one GPU ==
+        the 8 (and 3, ragged) dist.shard_columns runs bit for bit; column subset vs the oracle
+  cfg4  V6 LASSO m=512 n=2048 K=40 B=65,536                   -> column subset vs the oracle
+  cfg5  bf16 operands m=1024 n=4096 K=15, B=16,384 per GPU   -> column subset vs the bf16
+        restatement (pinned by tests/golden/bf16_*.npz) and the fp32 oracle; shards bitwise
+
+Columns are independent samples, so the oracle run on a column subset must reproduce exactly
+those columns: that is how the full-size workloads are checked against the CPU restatement
+(tests/test_oracle.py pins it to the reference).  The bar is tests/parity.py's.
+"""
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+import parity
+import problems as P
+from test_gpu_parity import check_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def device_problem(m, n, B, seed):
+    """gen_syn_data.py:14-47 distribution generated on the device (seeded): A column-normalised
+    N(0,1), X = A Z* + E* with Bernoulli(0.1) * N(0,1) Z*, E*; Z0 = U(0,1)/n, E0 = L0 = 0."""
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    A = torch.randn(m, n, generator=g, device="cuda", dtype=torch.float64)
+    A = (A / A.pow(2).sum(0, keepdim=True).sqrt()).float()
+    zs = (torch.rand(n, B, generator=g, device="cuda") < 0.1) * \
+        torch.randn(n, B, generator=g, device="cuda")
+    es = (torch.rand(m, B, generator=g, device="cuda") < 0.1) * \
+        torch.randn(m, B, generator=g, device="cuda")
+    X = (A.double() @ zs.double() + es.double()).float()
+    del zs, es
+    Z0 = torch.rand(n, B, generator=g, device="cuda") / n
+    E0 = torch.zeros(m, B, device="cuda")
+    L0 = torch.zeros(m, B, device="cuda")
+    return dict(A=A, X=X, Z0=Z0, E0=E0, L0=L0)
+
+
+def build(dl, variant, d, K, seed):
+    m, n = d["A"].shape
+    B = d["X"].shape[1]
+    sd = P.make_state_dict(variant, m, n, 1, K, d["A"].cpu().numpy(), seed, perturb=0.1)
+    net = dl.VARIANTS[variant](m=m, n=0, d=n, batch_size=B, A=d["A"], Z0=d["Z0"], E0=d["E0"],
+                               L0=d["L0"], layers=K)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    net.requires_grad_(False)
+    return net, sd
+
+
+def pick_columns(B, count, seed):
+    """`count` random columns plus the first and the last 16 (the ragged last tile)."""
+    rng = np.random.default_rng(seed)
+    cols = set(rng.choice(B, size=count, replace=False).tolist()) | {0} | set(range(B - 16, B))
+    return np.array(sorted(cols))
+
+
+def subset_vs_oracle(oracle, variant, d, sd, K, r, cols, case, path):
+    """Z/E/L (and T) of the GPU run on `cols` against the oracle on those columns at the fp32 bar
+    (parity.check_f32); T against the scale of X."""
+    sub = {k: v[:, cols].cpu().numpy() for k, v in d.items() if k != "A"}
+    A = d["A"].cpu().numpy()
+    args = (variant, sub["X"], A, sub["Z0"], sub["E0"], sub["L0"], sd, K)
+    r32 = oracle.forward(*args)
+    r64 = oracle.forward(*args, dtype=np.float64)
+    cidx = torch.from_numpy(cols).cuda()
+    for nm in ("Z", "E", "L", "T"):
+        got_all = getattr(r, nm)
+        if got_all is None or nm not in r64:
+            continue
+        for k in range(got_all.shape[0]):
+            got = got_all[k].index_select(1, cidx).cpu().numpy().astype(np.float64)
+            if nm == "T":
+                sx = np.linalg.norm(sub["X"].astype(np.float64))
+                e32 = float(np.linalg.norm(got - r32[nm][k]) / sx)
+                e64 = float(np.linalg.norm(got - r64[nm][k]) / sx)
+                gap = float(np.linalg.norm(r32[nm][k] - r64[nm][k]) / sx)
+            else:
+                e32, e64 = parity.nrel(got, r32[nm][k]), parity.nrel(got, r64[nm][k])
+                gap = parity.nrel(r32[nm][k], r64[nm][k])
+            parity.check_f32(case, path, f"{nm}[{k}] columns vs oracle", e32, e64, gap)
+
+
+def objective_vs_reduction(d, r, alpha, kind, case, path):
+    """The fused per-layer objective sums == a separate fp64 reduction of the returned Z_k
+    (with the literal X - A Z_k), 1e-5 relative."""
+    A = d["A"].double()
+    X = d["X"].double()
+    for k in range(r.Z.shape[0]):
+        Zk = r.Z[k].double()
+        res = X - A @ Zk
+        fit = res.abs().sum() if kind == "l1l1" else 0.5 * (res * res).sum()
+        ref = float(alpha * Zk.abs().sum() + fit)
+        got = float(alpha * r.loss_sums[k, 0] + r.loss_sums[k, 1])
+        parity.check(case, path, f"objective {kind}[{k}] vs fp64 reduction",
+                     abs(got - ref) / abs(ref), parity.REL)
+
+
+def test_cfg1_lena_v1(dl):
+    """main_lena.py at BASELINE config 1's shape, V1 default init (ill-conditioned: the bar
+    follows the reference's own fp32-vs-fp64 gap)."""
+    g, meta = load_golden("v1_lena_cfg1")
+    d = meta["defn"]
+    assert (d["m"], d["n"], d["K"], d["B"]) == (64, 256, 5, 20)
+    inp, sd = P.build_problem(d)
+    t = torch.from_numpy
+    net = dl.DLADMMNet(m=64, n=0, d=256, batch_size=20, A=t(inp["A"]), Z0=t(inp["Z0"]),
+                       E0=t(inp["E0"]), L0=t(inp["L0"]), layers=5)
+    net.load_state_dict({k: t(v) for k, v in sd.items()}, strict=True)
+    net.requires_grad_(False)
+    X = t(inp["X"]).cuda()
+    with torch.no_grad():
+        out = net(X)
+    check_golden("cfg1 v1_lena", g, meta, net, X, out)
+
+
+@pytest.mark.parametrize("precision", ["f32", "f32_split"])
+def test_cfg2_v4_b10000(precision, dl, oracle):
+    m, n, K, B = 256, 512, 15, 10000
+    d = device_problem(m, n, B, 10201)
+    net, sd = build(dl, "v4", d, K, 10201)
+    net.precision = precision
+    with torch.no_grad():
+        r = net.run(d["X"], keep_all=True, loss_kind=dl._lib.LOSS_L1L1)
+    path = {"f32": "f32", "f32_split": "split"}[precision]
+    cols = pick_columns(B, 48, 10202)
+    subset_vs_oracle(oracle, "v4", d, sd, K, r, cols, "cfg2 v4 B=10000", path)
+    objective_vs_reduction(d, r, 1.0, "l1l1", "cfg2 v4 B=10000", path)
+
+
+def test_cfg3_v4_b262144_shards(dl, oracle):
+    """The global batch of config 3 on one GPU, and the same batch as dist.shard_columns shards
+    (8 ranks as in the config, 3 ranks for ragged shards): every shard's Z/E/L/T equals the
+    whole-batch run's columns bit for bit, and the shards' objective sums add up to the whole
+    batch's (what the RCCL all-reduce of bench.py / dist.global_objectives forms)."""
+    ddist = importlib.import_module("d-ladmm_amd.dist")
+    m, n, K, B = 256, 512, 15, 262144
+    d = device_problem(m, n, B, 10301)
+    net, sd = build(dl, "v4", d, K, 10301)
+    lk = dl._lib.LOSS_L1L1
+    with torch.no_grad():
+        full = net.run(d["X"], keep_all=True, loss_kind=lk)
+    torch.cuda.synchronize()
+    cols = pick_columns(B, 32, 10302)
+    subset_vs_oracle(oracle, "v4", d, sd, K, full, cols, "cfg3 v4 B=262144", "f32")
+    for world in (8, 3):
+        sums = torch.zeros_like(full.loss_sums)
+        for rank in range(world):
+            c0, c1 = ddist.shard_columns(B, rank, world)
+            with torch.no_grad():
+                sh = net._run_shard(d["X"][:, c0:c1], (c0, c1), want_T=True, loss_kind=lk)
+            for nm in "ZELT":
+                assert torch.equal(getattr(sh, nm), getattr(full, nm)[:, :, c0:c1]), \
+                    (world, rank, nm)
+            sums += sh.loss_sums
+            del sh
+        np.testing.assert_allclose(sums.cpu().numpy(), full.loss_sums.cpu().numpy(), rtol=1e-12)
+        glob = ddist.global_objectives(sums, 0.001, B)
+        ref = (0.001 * full.loss_sums[:, 0] + full.loss_sums[:, 1]) / B
+        np.testing.assert_allclose(glob.cpu().numpy(), ref.cpu().numpy(), rtol=1e-12)
+
+
+def test_cfg4_v6_lasso_512x2048_k40_b65536(dl, oracle):
+    """Config 4 at its full batch: the per-layer kernel pairs (beyond the fused kernel's register
+    budget), 2K+1 = 81 launches."""
+    m, n, K, B = 512, 2048, 40, 65536
+    d = device_problem(m, n, B, 10401)
+    net, sd = build(dl, "v6", d, K, 10401)
+    with torch.no_grad():
+        r = net.run(d["X"], keep_all=True, loss_kind=dl._lib.LOSS_LASSO)
+    cols = pick_columns(B, 24, 10402)
+    subset_vs_oracle(oracle, "v6", d, sd, K, r, cols, "cfg4 v6 B=65536", "layered")
+    objective_vs_reduction(d, r, 1.0, "lasso", "cfg4 v6 B=65536", "layered")
+
+
+def test_cfg5_bf16_1024x4096_k15_b16384(dl, oracle):
+    """Config 5's per-GPU shard (131,072 / 8) at full depth, bf16 operands / fp32 state: a column
+    subset against the bf16 restatement (the reference with bf16-operand GEMMs, pinned by
+    tests/golden/bf16_*.npz) and the fp32 oracle at test_gpu_bf16.bf16_bar, with s_k = the
+    distance between those two and d_k = the restatement's own accumulation-order spread (fp32
+    vs exact accumulation) on the same columns; two column shards equal the whole run bit for
+    bit."""
+    from test_gpu_bf16 import bf16_bar
+    m, n, K, B = 1024, 4096, 15, 16384
+    d = device_problem(m, n, B, 10501)
+    net, sd = build(dl, "v4", d, K, 10501)
+    net.precision = "bf16"
+    with torch.no_grad():
+        r = net.run(d["X"], keep_all=True)
+    cols = pick_columns(B, 16, 10502)
+    sub = {k: v[:, cols].cpu().numpy() for k, v in d.items() if k != "A"}
+    args = ("v4", sub["X"], d["A"].cpu().numpy(), sub["Z0"], sub["E0"], sub["L0"], sd, K)
+    rb = oracle.forward(*args, gemm="bf16")
+    ra = oracle.forward(*args, gemm="bf16_acc32")
+    r32 = oracle.forward(*args)
+    cidx = torch.from_numpy(cols).cuda()
+    for nm in "ZELT":
+        for k in range(len(rb[nm])):
+            got = getattr(r, nm)[k].index_select(1, cidx).cpu().numpy()
+            s = parity.nrel(rb[nm][k], r32[nm][k])
+            b_bf, b_32 = bf16_bar(s, parity.nrel(ra[nm][k], rb[nm][k]))
+            parity.check("cfg5 bf16 B=16384", "bf16", f"{nm}[{k}] columns vs bf16 restatement",
+                         parity.nrel(got, rb[nm][k]), b_bf, s)
+            parity.check("cfg5 bf16 B=16384", "bf16", f"{nm}[{k}] columns vs oracle32",
+                         parity.nrel(got, r32[nm][k]), b_32, s)
+    half = B // 2
+    for c0, c1 in ((0, half), (half, B)):
+        with torch.no_grad():
+            sh = net._run_shard(d["X"][:, c0:c1], (c0, c1), want_T=True, precision="bf16")
+        for nm in "ZELT":
+            assert torch.equal(getattr(sh, nm), getattr(r, nm)[:, :, c0:c1]), (c0, nm)
+        del sh

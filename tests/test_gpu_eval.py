@@ -111,3 +111,98 @@ def test_fused_per_column_objective(dl, case):
                     inp["A"].astype(np.float64) @ z).sum(0) for z in Zs])
     np.testing.assert_allclose(per, ref, rtol=2e-5)
     assert abs(per.sum() - oe.l1l1(Zs, inp["X"], inp["A"], 0.01).sum()) <= 1e-5 * per.sum()
+
+
+# ----------------------------------------------- pinned by the reference's own statements (f3)
+def _load_eval(name):
+    import json
+    import os
+    from conftest import GOLDEN
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    return g, json.loads(str(g["meta"]))
+
+
+def _eval_model(dl, c, inp, sd):
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+    kw = dict(m=c["m"], n=0, d=c["n"], batch_size=c["batch_size"], A=t(inp["A"]),
+              Z0=t(inp["Z0"]), E0=t(inp["E0"]), L0=t(inp["L0"]), layers=c["layers"])
+    net = (dl.DLADMMNetLSKM(**kw, alpha=c["alpha"]) if c["variant"] == "v4"
+           else dl.DLADMMNetLasso(**kw))
+    net.load_state_dict({k: t(v) for k, v in sd.items()}, strict=True)
+    net.requires_grad_(False)
+    return net
+
+
+def _run_evaluators(dl, c, inp, net, batches):
+    """Accumulate every objective of the case over `batches` = [(Z, E, L, T, gt)] of device
+    tensors exactly as the reference batch loop does; finalised per-layer values."""
+    bs, K = c["batch_size"], c["layers"]
+    res = {}
+    for ob in c["objectives"]:
+        e = ev(dl, ob, K=K, alpha=c["alpha"])
+        e.n_test = bs * c["n_batches"]
+        for j, (Z, E, L, T, gt) in enumerate(batches):
+            X = torch.from_numpy(np.ascontiguousarray(inp["X"][:, j * bs:(j + 1) * bs])).cuda()
+            lab = lambda a: torch.from_numpy(  # noqa: E731
+                np.ascontiguousarray(a[:, j * bs:(j + 1) * bs])).cuda()
+            e.add_batch(X, Z, E, L=L, T=T, Z_label=lab(inp["Zstar"]), E_label=lab(inp["Estar"]),
+                        gt=gt, model=net)
+        res[ob] = e.result(inp["Zstar"], inp["Estar"])
+    return res
+
+
+def _check(res, g, tol, tag):
+    for ob, got in res.items():
+        ref = g["obj_" + ob]
+        if ob == "NMSE":   # dB: compare the difference
+            np.testing.assert_allclose(got, ref, atol=10 * tol, err_msg=f"{tag} {ob}")
+        else:
+            np.testing.assert_allclose(got, ref, rtol=tol, err_msg=f"{tag} {ob}")
+
+
+@pytest.mark.parametrize("name", sorted(P.EVAL_FIXTURES))
+def test_objectives_on_reference_outputs_match_reference_statements(name, dl):
+    """Evaluator (dladmm_colobj_f32 / the S-L2 KM step + safeguard norm on the GPU) on the
+    reference forward's own outputs equals what test_syn_*_scalar.py's objective statements
+    computed from them (make_golden_eval.py): the objective computation alone."""
+    g, meta = _load_eval(name)
+    c = meta["case"]
+    inp, sd = P.eval_problem(c)
+    net = _eval_model(dl, c, inp, sd)
+    dev = lambda a: [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in a]  # noqa: E731
+    batches = []
+    for j in range(c["n_batches"]):
+        gt = None
+        if c["gt_K"]:
+            gt = tuple(torch.from_numpy(np.ascontiguousarray(g["gt_" + nm][j])).cuda()
+                       for nm in "ZET")
+        batches.append((dev(g["ref_Z"][j]), dev(g["ref_E"][j]), dev(g["ref_L"][j]),
+                        dev(g["ref_T"][j]), gt))
+    _check(_run_evaluators(dl, c, inp, net, batches), g, 1e-5, name)
+
+
+@pytest.mark.parametrize("name", sorted(P.EVAL_FIXTURES))
+def test_objectives_end_to_end_match_reference(name, dl):
+    """The whole evaluation on the GPU -- learned forward, K = 2000 KM ground truth, objectives --
+    against the reference script's values on the same test batches.  Tolerance 1e-4: the
+    forward outputs themselves carry the fp32 parity tolerance (1e-5 norm-relative) and the
+    Normalized-* objectives divide differences of them."""
+    g, meta = _load_eval(name)
+    c = meta["case"]
+    inp, sd = P.eval_problem(c)
+    net = _eval_model(dl, c, inp, sd)
+    bs = c["batch_size"]
+    batches = []
+    for j in range(c["n_batches"]):
+        X = torch.from_numpy(np.ascontiguousarray(inp["X"][:, j * bs:(j + 1) * bs])).cuda()
+        with torch.no_grad():
+            if c["variant"] == "v4":
+                Z, E, L, T = net(X, True, False, False)
+            else:
+                Z, E, L, T = net(X)
+            gt = None
+            if c["gt_K"]:
+                Zp, Ep, Lp, Tp = net(X, False, False, False, K=c["gt_K"])
+                gt = (Zp[-1], Ep[-1], Tp[-1])
+        batches.append((Z, E, L, T, gt))
+    _check(_run_evaluators(dl, c, inp, net, batches), g, 1e-4, name)

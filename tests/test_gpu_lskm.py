@@ -6,6 +6,7 @@ import pytest
 import torch
 
 from conftest import load_golden
+import parity
 import problems as P
 
 pytestmark = pytest.mark.gpu
@@ -43,8 +44,8 @@ def test_lskm_matches_reference(name, dl):
     for i, j in enumerate(g["layers_kept"]):
         for c, nm in enumerate("ZELT"):
             got = out[c][j + 1 if nm == "T" else j].cpu().numpy()
-            tol = max(1e-5, 3.0 * float(g["gap_" + nm][i]))
-            assert nrel(got, g[nm][i]) <= tol, (nm, int(j))
+            gap = float(g["gap_" + nm][i])
+            parity.check(name, "f32", f"{nm}[{int(j)}]", nrel(got, g[nm][i]), parity.tol(gap), gap)
     if "sg_count" in g.files:
         np.testing.assert_array_equal(out[4], g["sg_count"])
 

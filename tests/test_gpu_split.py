@@ -1,6 +1,7 @@
 """Parity of the split-f16 fused forward (precision "f32_split", DLADMM_PREC_F32_SPLIT,
 csrc/dladmm_fused_x3.hip) with the reference -- the SAME bars as the fp32 path
-(tests/test_gpu_parity.py): per layer, norm-relative <= max(1e-5, 3 x the reference's own
+(tests/test_gpu_parity.py, tests/parity.py): per layer, norm-relative <= max(1e-5, 2 x the
+reference's own
 fp32-vs-fp64 gap), against the reference's golden outputs and the oracle.
 
 The mode forms every fp32 GEMM as hi*hi + hi*lo + lo*hi of exactly split, power-of-two-scaled f16
@@ -15,7 +16,8 @@ import torch
 
 from conftest import load_golden
 import problems as P
-from test_gpu_parity import REL, _compare, _oracle_case, make_net, nrel
+import parity
+from test_gpu_parity import REL, _compare, _oracle_case, check_golden, make_net, nrel
 
 pytestmark = pytest.mark.gpu
 
@@ -62,17 +64,7 @@ def test_split_matches_reference_golden(name, dl):
         assert _path(dl, net, X) == 4
     with torch.no_grad():
         out = net(X)
-    names = ["Z", "E", "L", "T"][: len(out)]
-    for nm, seq in zip(names, out):
-        for k, t in enumerate(seq):
-            tol = max(REL, 3.0 * float(g["gap_" + nm][k]))
-            e = nrel(t.cpu().numpy(), g[nm][k])
-            assert e <= tol, f"{name} {nm}[{k}] nrel {e:.3e} > {tol:.3e}"
-    otol = max(2e-5, 3.0 * max(float(np.max(g["gap_" + nm])) for nm in names))
-    _, obj = net.layer_objectives(X, meta["alpha"], "l1l1")
-    np.testing.assert_allclose(obj.cpu().numpy(), g["loss_l1l1"], rtol=otol)
-    _, obj = net.layer_objectives(X, meta["alpha"], "lasso")
-    np.testing.assert_allclose(obj.cpu().numpy(), g["loss_lasso"], rtol=otol)
+    check_golden(name, g, meta, net, X, out, path="split")
 
 
 @pytest.mark.parametrize("variant", ["v4", "v5", "v6"])
@@ -83,7 +75,7 @@ def test_split_vs_oracle_baseline_shape(variant, B, dl, oracle):
     net = split_net(dl, variant, inp, sd, K)
     with torch.no_grad():
         out = net(torch.from_numpy(inp["X"]).cuda())
-    _compare(out, ref, tag=f"split {variant} B={B}")
+    _compare(out, ref, tag=f"split {variant} B={B}", path="split")
 
 
 @pytest.mark.parametrize("shape", [(16, 32), (30, 70), (64, 256), (250, 500), (200, 512)])
@@ -95,7 +87,7 @@ def test_split_padded_shapes(shape, dl, oracle):
         assert _path(dl, net, torch.from_numpy(inp["X"]).cuda()) == 4
         with torch.no_grad():
             out = net(torch.from_numpy(inp["X"]).cuda())
-        _compare(out, ref, tag=f"split {variant} {shape}")
+        _compare(out, ref, tag=f"split {variant} {shape}", path="split")
 
 
 def test_split_column_magnitudes(dl, oracle):
@@ -175,8 +167,10 @@ def test_split_baseline_size(dl, oracle):
     ref = oracle.forward("v4", X[:, cols], A, Z0[:, cols], E0[:, cols], L0[:, cols], sd, K)
     for nm, got, g32 in (("Z", r.Z, r32.Z), ("E", r.E, r32.E), ("L", r.L, r32.L)):
         for k in range(K):
-            assert nrel(got[k][:, cols].cpu().numpy(), ref[nm][k]) <= REL, (nm, k)
-            assert nrel(got[k].cpu().numpy(), g32[k].cpu().numpy()) <= REL, (nm, k)
+            parity.check("v4 B=65536 columns", "split", f"{nm}[{k}] vs oracle32",
+                         nrel(got[k][:, cols].cpu().numpy(), ref[nm][k]), REL)
+            parity.check("v4 B=65536", "split", f"{nm}[{k}] vs f32 path",
+                         nrel(got[k].cpu().numpy(), g32[k].cpu().numpy()), REL)
     Ad = torch.from_numpy(A).cuda().double()
     sep = []
     for k in range(K):

@@ -52,6 +52,9 @@ def test_reference_checkpoint_loads_unchanged(dl, tmp_path):
 def test_names_and_init(dl):
     assert _net(dl, "v1").name() == "DLADMMNet"
     assert _net(dl, "v4").name() == "DLADMMNet_scalar"
+    # main_syn_l1l1-sl2_scalar.py:113-114 / main_syn_l1l1_scalar_z0.py:113-114: same V4 body
+    assert _net(dl, "v4_sl2").name() == "DLADMMNet" and _net(dl, "v4_z0").name() == "DLADMMNet"
+    assert list(_net(dl, "v4_sl2").state_dict()) == list(_net(dl, "v4").state_dict())
     assert _net(dl, "v5").name() == "DLADMMNet_scalar_tied"
     assert _net(dl, "v7").name() == "DLADMMNet_scalar_newS_layerwise"
     assert _net(dl, "v7t").name() == "DLADMMNet_scalar_tied_newS_layerwise"

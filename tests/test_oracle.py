@@ -52,3 +52,27 @@ def test_literal_two_relu_shrink(oracle):
                                   np.array([-1.25, -0.25, 0.0, 0.25, 1.25], np.float32))
     np.testing.assert_array_equal(oracle.self_active(x, np.float32(0.25)),
                                   np.array([-0.75, 0.0, 0.0, 0.0, 0.75], np.float32))
+
+
+@pytest.mark.parametrize("name", sorted(P.BF16_FIXTURES))
+def test_bf16_restatement_matches_reference(name, oracle):
+    """oracle.forward(gemm="bf16") (BASELINE config 5 arithmetic: bf16 GEMM operands, exact
+    accumulation, fp32 state) equals the reference classes run with exactly that GEMM arithmetic
+    (tests/golden/make_golden_bf16.py) -- bit for bit in practice; the fp32 twins (the yardstick
+    s_k) equal the plain oracle within fp32 summation-order noise, which at the config-5 shape
+    grows to ~2e-5 by layer 15, three orders below s_k."""
+    g, meta = load_golden(name)
+    d = meta["defn"]
+    inp, sd = P.build_problem(d)
+    for k, v in inp.items():
+        assert P.sha256(v) == meta["sha256"][k], k
+    args = (d["variant"], inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd, d["K"])
+    rb = oracle.forward(*args, gemm="bf16")
+    r32 = oracle.forward(*args)
+    for nm in ("Z", "E", "L", "T"):
+        if nm not in g.files:
+            continue
+        for k in range(g[nm].shape[0]):
+            assert oracle.nrel(rb[nm][k], g[nm][k]) <= 1e-6, (nm, k)
+            assert oracle.nrel(r32[nm][k], g["f32_" + nm][k]) <= max(
+                1e-5, 1e-3 * float(g["s_" + nm][k])), (nm, k)
