@@ -53,12 +53,17 @@ __device__ __forceinline__ float col16_sum(float v) {
 
 // PH: 1 = BK1, 2 = BK2, 3 = BK3, 4 = BK1 on the forward's saved P_k = A Z_k (a.Pk; no GEMM:
 // an elementwise pass over the m x B adjoints), 5 = BK2 on the saved Z_k mask only (one GEMM,
-// 32-block slices; launched beside a PH 2 launch, each exits unless theta_z's sign is its case)
+// 32-block slices; launched beside a PH 2 launch, each exits unless theta_z's sign is its case),
+// 6 = BK3(k3) fused with BK1(k3 - 1) on the saved product (a.k = k3 - 1): BK3's epilogue has, per
+// element, the complete adjoint of L_{k3-1} and the adjoint of T_{k3} that BK1(k3 - 1) consumes,
+// so they never round-trip through HBM and BK1 needs no launch of its own
 template <int EMODE, int PKIND, int PH, int NW, int SB>
 __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs a) {
-  constexpr bool BK1 = PH == 1 || PH == 4;
+  constexpr bool FUS = PH == 6;
+  constexpr bool BK1 = PH == 1 || PH == 4 || FUS;
   constexpr bool BK2 = PH == 2 || PH == 5;
-  constexpr bool PSV = PH == 4;
+  constexpr bool PSV = PH == 4;            // no GEMM: one column per lane
+  constexpr bool SAVEDP = PH == 4 || FUS;  // P = A Z_k from the forward (a.Pk)
   if constexpr (BK2 && PKIND != PK_ROW) {
     // zk_mask 2: the PH 5 launch covers theta_z >= 0 and the PH 2 launch theta_z < 0
     if (a.zk_mask == 2) {
@@ -67,7 +72,7 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
     }
   }
   // BK1 keeps 4 workgroups per CU (its latency-bound epilogue needs them): a 2-deep B ring
-  constexpr int NSB = PH == 1 ? 2 : 3;
+  constexpr int NSB = (PH == 1 || FUS) ? 2 : 3;
   __shared__ f32x4 ring[PSV ? 1 : slice_lds_f4<NW, NSB>()];
 
   const int tid = threadIdx.x;
@@ -117,21 +122,33 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
     if constexpr (PKIND == PK_ROW) return rp[(int64_t)slot * a.rstride + rowc];
     else return spv[slot];
   };
+  // PH 6: beta1 of the BK3 layer k3 (its only parameter)
+  const int k3 = FUS ? a.k3 : k;
+  const float b1s3 = (FUS && PKIND != PK_ROW && PKIND != PK_ELEM)
+                         ? ((cfloat_p)a.scal)[k3 * DLADMM_NSCALAR + DLADMM_P_BETA1] : 0.0f;
+  const float* rp3 = (FUS && a.rowp) ? a.rowp + (int64_t)k3 * 8 * a.rstride : nullptr;
+  auto pm3_b1 = [&](int rowc) -> float {
+    if constexpr (PKIND == PK_ROW) return rp3[(int64_t)DLADMM_P_BETA1 * a.rstride + rowc];
+    else return b1s3;
+  };
   const int64_t ldw = a.ldw;  // row stride of the adjoint / operand workspaces
 
   // per-slot partial sums: scalar kind over the whole wave, row kind per row (col16_sum)
   float ps[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) ps[i] = 0.0f;
+  float ps3 = 0.0f;  // PH 6: the BK3 layer's beta1 partial
   const int cg = blockIdx.x * NW + w;  // column group (wave) index
-  auto row_flush = [&](int row, bool rok, const float (&v)[8], unsigned mask) {
+  auto row_flush = [&](int row, bool rok, const float (&v)[8], unsigned mask,
+                       float* part = nullptr) {
     if constexpr (PKIND == PK_ROW) {
+      float* dst = part ? part : a.part;
 #pragma unroll
       for (int sl = 0; sl < 8; ++sl) {
         if (!(mask & (1u << sl))) continue;
         const float s = PSV ? wave_sum(v[sl]) : col16_sum(v[sl]);
         if ((PSV ? lane == 0 : (lane & 15) == 0) && rok)
-          a.part[((int64_t)sl * a.rstride + row) * a.ncg + cg] = s;
+          dst[((int64_t)sl * a.rstride + row) * a.ncg + cg] = s;
       }
     }
   };
@@ -142,7 +159,10 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
   const BView vEp = make_view(a.Ep, m, a.ldep, g, col, cv);
   const BView vLp = make_view(a.Lp, m, a.ldlp, g, col, cv);
   const BView vTk = make_view(a.Tk, m, a.ldt, g, col, cv);
-  const BView vPk = make_view(PSV ? a.Pk : nullptr, m, a.ldt, g, col, cv);
+  const BView vPk = make_view(SAVEDP ? a.Pk : nullptr, m, a.ldt, g, col, cv);
+  const BView vTk3 = make_view(FUS ? a.Tk3 : nullptr, m, a.ldt, g, col, cv);  // T_{k3}
+  const BView vb13 = make_view(FUS && PKIND == PK_ELEM ? a.b1e3 : nullptr, m, a.ldb, g, col, cv);
+  const BView vgb13 = make_view(FUS && PKIND == PK_ELEM ? a.gb1e3 : nullptr, m, a.ldb, g, col, cv);
   const BView vZp = make_view(a.Zp, n, a.ldzp, g, col, cv);
   const BView vZk = make_view(BK2 && zmask ? a.Zk : nullptr, n, a.ldzk, g, col, cv);
   const BView vgZ = make_view(a.gZ, n, a.ldg, g, col, cv);
@@ -163,17 +183,23 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
   // The epilogue is software-pipelined over output blocks: pass 1 (bload) issues every load of
   // block i + 1 before pass 2 (bfinish) computes and stores block i -- the compiler cannot move a
   // load above a store it may alias, so element order would pay one memory round trip per block.
-  struct BIn { float x, ep, lp, tk, b1, b2, AL, gL, AT, gT, AE, gE, zp, AZ, gZ, gb1, P, zk; };
+  struct BIn { float x, ep, lp, tk, b1, b2, AL, gL, AT, gT, AE, gE, zp, AZ, gZ, gb1, P, zk,
+               tk3, b13, gb13; };
   auto bload_row = [&](int i, int r) {
     const uint32_t ru = (uint32_t)(16 * (ib0 + i) + r);  // uniform part of the row
     BIn v;
     if constexpr (BK1) {
       v.x = vX.ld(ru); v.ep = vEp.ld(ru); v.lp = vLp.ld(ru); v.tk = vTk.ld(ru);
-      if constexpr (PSV) v.P = vPk.ld(ru);
+      if constexpr (SAVEDP) v.P = vPk.ld(ru);
       if constexpr (PKIND == PK_ELEM) { v.b1 = vb1.ld(ru); v.b2 = vb2.ld(ru); }
       v.AL = vAL.ld(ru); v.gL = vgL.ld(ru);
-      v.AT = vAT.ld(ru); v.gT = vgT.ld(ru);
+      if constexpr (!FUS) v.AT = vAT.ld(ru);  // PH 6: formed by its BK3 part
+      v.gT = vgT.ld(ru);
       v.AE = vAE.ld(ru); v.gE = vgE.ld(ru);
+      if constexpr (FUS) {
+        v.tk3 = vTk3.ld(ru);
+        if constexpr (PKIND == PK_ELEM) { v.b13 = vb13.ld(ru); v.gb13 = vgb13.ld(ru); }
+      }
     } else if constexpr (BK2) {
       v.zp = vZp.ld(ru); v.AZ = vAZ.ld(ru); v.gZ = vgZ.ld(ru); v.zk = vZk.ld(ru);
     } else {
@@ -199,8 +225,28 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
         const bool ok = cv && rok;
         const int rowc = rok ? row : 0;
         float P;
-        if constexpr (PSV) P = v.P;
+        if constexpr (SAVEDP) P = v.P;
         else P = acc[i][r];
+        // PH 6: BK3 of layer k3 first -- gVar = M_k3^T gU; its outputs (the complete adjoint of
+        // L_{k3-1} and the adjoint of T_{k3}) are this BK1's incoming adjoints
+        float aLin = v.AL, aTin = v.AT;
+        if constexpr (FUS) {
+          const float gVar = acc[i][r];
+          const float b13 = (PKIND == PK_ELEM) ? v.b13 : pm3_b1(rowc);
+          float pb1 = gVar * v.tk3;
+          if constexpr (PKIND == PK_ELEM) vgb13.st(ru, v.gb13 + pb1);
+          aLin = v.AL + gVar;
+          aTin = b13 * gVar;   // adjoint of T_k3 (main_lena.py:85)
+          if (!ok) pb1 = 0.f;
+          if constexpr (PKIND == PK_ROW) {
+            float pv3[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            pv3[DLADMM_P_BETA1] = pb1;
+            row_flush(row, rok, pv3, 1u << DLADMM_P_BETA1, a.part3);
+          } else {
+            ps3 += pb1;
+            asm volatile("" : "+v"(ps3));
+          }
+        }
         const float x = v.x;
         const float ep = v.ep;
         const float lp = v.lp;
@@ -216,8 +262,8 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
           if constexpr (EMODE != EM_LASSO) b2 = pm(DLADMM_P_BETA2, rowc);
         }
         // incoming adjoints of L_k, T_{k+1}, E_k
-        const float aL = v.AL + v.gL;
-        const float aT = v.AT + v.gT;
+        const float aL = aLin + v.gL;
+        const float aT = aTin + v.gT;
         const float aE = v.AE + v.gE;
         // recompute the forward's E_k and T_{k+1} (same expressions as the forward kernels)
         float e, gP, gEp = 0.f, gLp;
@@ -394,6 +440,10 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
         if (PH == 5) a.part[(int64_t)sl * a.nslots + slot + gridDim.x * NW] = 0.0f;
       }
     };
+    if constexpr (FUS) {
+      const float s = wave_sum(ps3);
+      if (lane == 0) a.part3[(int64_t)DLADMM_P_BETA1 * a.nslots + slot] = s;
+    }
     if constexpr (BK1) {
       flush(DLADMM_P_BETA3);
       if constexpr (EMODE == EM_VVAR) { flush(DLADMM_P_BETA2); flush(DLADMM_P_SS2); flush(DLADMM_P_THETA_E); }
@@ -530,6 +580,7 @@ hipError_t launch_bwd(int phase, int variant, const BwdArgs& a, dim3 grid, int s
     case 5: return launch_bwd_ph<5>(variant, a, grid, sb, s);
     case 2: return launch_bwd_ph<2>(variant, a, grid, sb, s);
     case 3: return launch_bwd_ph<3>(variant, a, grid, sb, s);
+    case 6: return launch_bwd_ph<6>(variant, a, grid, sb, s);
   }
   return hipErrorInvalidValue;
 }

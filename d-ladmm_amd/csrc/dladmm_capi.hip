@@ -392,6 +392,13 @@ inline unsigned long long* dbg_ptr() {
   return p;
 }
 
+// DLADMM_BWD_UNFUSED=1: after a saved-product forward, BK1 still runs as its own launch
+// (phase 4) instead of inside BK3's (phase 6) -- A/B timing and the equivalence test
+inline bool fwd_unfused_bwd() {
+  const char* e = getenv("DLADMM_BWD_UNFUSED");
+  return e && e[0] == '1';
+}
+
 inline int run_fused(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStream_t s) {
   float* Ap = (float*)(ws + p.off_ap);
   float* Wp = (float*)(ws + p.off_wp);
@@ -627,7 +634,7 @@ struct BwdPlan {
   int wtiles, nchunks; int64_t chunk;
   bool saved_p;                   // BK1 reads the forward's A Z_k (fwd_desc.P)
   size_t off_a1, off_at, off_m, off_mt, off_az, off_ae, off_al, off_at_, off_gp, off_var,
-      off_part, off_wpart, total;
+      off_part, off_part2, off_wpart, total;
 };
 
 inline int validate_bwd(const dladmm_bwd_desc* d) {
@@ -706,6 +713,7 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   p->off_gp = o; o += align256(colb * m);
   p->off_var = o; o += align256(colb * p->Rm);
   p->off_part = o; o += align256(sizeof(float) * part_floats);
+  p->off_part2 = o; o += align256(sizeof(float) * part_floats);  // phase 6: layers of odd k
   p->off_wpart = o; o += align256(sizeof(float) * (size_t)p->nchunks * n * m);
   p->total = o;
   return 0;
@@ -729,7 +737,7 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
   float* AT = (float*)(ws + p.off_at_);
   float* GP = (float*)(ws + p.off_gp);
   float* VAR = (float*)(ws + p.off_var);
-  float* part = (float*)(ws + p.off_part);
+  float* const part = (float*)(ws + p.off_part);
   float* wpart = (float*)(ws + p.off_wpart);
   // adjoints start at zero; the padded rows / columns of gU and Var stay zero (wgrad reads them)
   if (hipError_t e = hipMemsetAsync(ws + p.off_az, 0, p.off_part - p.off_az, s)) return (int)e;
@@ -756,7 +764,42 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
   a.ldb = f.ld_beta;
   a.part = part;
   const dim3 gm(p.gx, p.slices_m), gn(p.gx, p.slices_n);
-  const size_t part_bytes = p.off_wpart - p.off_part;
+  const size_t part_bytes = p.off_part2 - p.off_part;
+  // with the forward's saved products (p.saved_p) BK1 of layer k-1 runs inside BK3(k)'s launch
+  // (phase 6); the parameter-slot partials of layer k then live in part buffer k & 1 (layer k's
+  // BK1 slots are written one iteration before its BK2 / BK3 ones)
+  const bool fuse = p.saved_p && !fwd_unfused_bwd();
+  float* part2 = (float*)(ws + p.off_part2);
+  auto partk = [&](int k) { return (fuse && (k & 1)) ? part2 : part; };
+  // phase 4: a wave covers 64 columns (one per lane), so its grid has a quarter of the tiles
+  const dim3 gm4(ceil_div((int)B, 64 * kBwdWaves), p.slices_m);
+  auto layer_args = [&](BwdArgs& x, int k) {
+    x.k = k;
+    x.Ep = k ? f.E + (k - 1) * ml : f.E0; x.ldep = k ? ldo : f.ld_e0;
+    x.Lp = k ? f.L + (k - 1) * ml : f.L0; x.ldlp = k ? ldo : f.ld_l0;
+    x.Zp = k ? f.Z + (k - 1) * zl : f.Z0; x.ldzp = k ? ldo : f.ld_z0;
+    x.Tk = f.T + k * ml; x.ldt = ldo;
+    x.gZ = d->gZ ? d->gZ[k] : nullptr;
+    x.gE = d->gE ? d->gE[k] : nullptr;
+    x.gL = d->gL ? d->gL[k] : nullptr;
+    x.gT = d->gT ? d->gT[k + 1] : nullptr;
+    if (v == DLADMM_V1_LENA) {
+      x.b1e = f.beta1_elem[k]; x.b2e = f.beta2_elem[k];
+      x.gb1e = d->g_beta1_elem[k]; x.gb2e = d->g_beta2_elem[k];
+    }
+    x.part = partk(k);
+  };
+  if (fuse) {
+    // scalar kinds: every slot of both buffers is rewritten per layer, zeroed once; per-row
+    // kinds re-zero a buffer before its layer's first write
+    if (hipError_t e = hipMemsetAsync(rowk ? partk(K - 1) : part, 0,
+                                      rowk ? part_bytes : 2 * part_bytes, s))
+      return (int)e;
+    BwdArgs b1 = a;
+    layer_args(b1, K - 1);
+    b1.Pk = f.P + (int64_t)(K - 1) * ml;
+    if (hipError_t e = launch_bwd(4, v, b1, gm4, p.SBm, s)) return (int)e;
+  }
   for (int k = K - 1; k >= 0; --k) {
     // W_k (q = W_k Var_k; both forward paths formed U = Z_{k-1} - s1 q bit for bit) and
     // (-s1 W_k)^T
@@ -767,31 +810,19 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
       return (int)e;
     // scalar kinds: every slot's entries are rewritten per layer (counts fixed), so the
     // partials are zeroed once; per-row kinds re-zero (rows past m/n are never written)
-    if (rowk || k == K - 1)
+    if (!fuse && (rowk || k == K - 1))
       if (hipError_t e = hipMemsetAsync(part, 0, part_bytes, s)) return (int)e;
-    a.k = k;
-    a.Ep = k ? f.E + (k - 1) * ml : f.E0; a.ldep = k ? ldo : f.ld_e0;
-    a.Lp = k ? f.L + (k - 1) * ml : f.L0; a.ldlp = k ? ldo : f.ld_l0;
-    a.Zp = k ? f.Z + (k - 1) * zl : f.Z0; a.ldzp = k ? ldo : f.ld_z0;
-    a.Tk = f.T + k * ml; a.ldt = ldo;
-    a.gZ = d->gZ ? d->gZ[k] : nullptr;
-    a.gE = d->gE ? d->gE[k] : nullptr;
-    a.gL = d->gL ? d->gL[k] : nullptr;
-    a.gT = d->gT ? d->gT[k + 1] : nullptr;
-    if (v == DLADMM_V1_LENA) {
-      a.b1e = f.beta1_elem[k]; a.b2e = f.beta2_elem[k];
-      a.gb1e = d->g_beta1_elem[k]; a.gb2e = d->g_beta2_elem[k];
+    layer_args(a, k);
+    if (!fuse) {
+      // BK1: P = A Z_k, recomputed -- or (phase 4) read from the forward's saved P_k, the same
+      // values bit for bit (the forward's own product), which leaves BK1 without a GEMM
+      BwdArgs b1 = a;
+      b1.KB = p.NB; b1.MBp = p.MBpm; b1.Krows = n; b1.Wp = A1;
+      b1.S = f.Z + k * zl; b1.ldS = ldo;
+      b1.Pk = p.saved_p ? f.P + k * ml : nullptr;
+      if (hipError_t e = launch_bwd(p.saved_p ? 4 : 1, v, b1, p.saved_p ? gm4 : gm, p.SBm, s))
+        return (int)e;
     }
-    // BK1: P = A Z_k, recomputed -- or (phase 4) read from the forward's saved P_k, the same
-    // values bit for bit (the forward's own product), which leaves BK1 without a GEMM
-    BwdArgs b1 = a;
-    b1.KB = p.NB; b1.MBp = p.MBpm; b1.Krows = n; b1.Wp = A1;
-    b1.S = f.Z + k * zl; b1.ldS = ldo;
-    b1.Pk = p.saved_p ? f.P + k * ml : nullptr;
-    // phase 4: a wave covers 64 columns (one per lane), so its grid has a quarter of the tiles
-    const dim3 gm4(ceil_div((int)B, 64 * kBwdWaves), p.slices_m);
-    if (hipError_t e = launch_bwd(p.saved_p ? 4 : 1, v, b1, p.saved_p ? gm4 : gm, p.SBm, s))
-      return (int)e;
     // BK2: R = A^T gP, q = M_k Var_k
     BwdArgs b2 = a;
     b2.KB = p.MB; b2.MBp = p.NBpn; b2.Krows = m;
@@ -808,12 +839,8 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
       if (hipError_t e = launch_bwd(5, v, b2, dim3(p.gx, p.slices_n / 2), 32, s)) return (int)e;
     }
     if (hipError_t e = launch_bwd(2, v, b2, gn, 16, s)) return (int)e;
-    // BK3: gVar = M_k^T gU
-    BwdArgs b3 = a;
-    b3.KB = p.NB; b3.MBp = p.MBpm; b3.Krows = n; b3.Wp = Mt;
-    b3.S = AZ; b3.ldS = ldw;
-    if (hipError_t e = launch_bwd(3, v, b3, gm, p.SBm, s)) return (int)e;
-    // weight gradient gW_k = -s1 * gU Var_k^T (split-K over the batch, fixed-order reduction)
+    // weight gradient gW_k = -s1 * gU Var_k^T (split-K over the batch, fixed-order reduction);
+    // before BK3: with phase 6 that launch overwrites Var with Var_{k-1}
     WgradArgs wa{};
     wa.G = AZ; wa.V = VAR; wa.ld = ldw; wa.n = n; wa.m = m;
     wa.NBp16 = (int)(p.Rn / 16); wa.MBp16 = (int)(p.Rm / 16);
@@ -824,16 +851,34 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
                                            has_s1 ? f.scalar_params : nullptr, k, tied ? 1 : 0,
                                            gWk, d->ld_gw, s))
       return (int)e;
+    // BK3: gVar = M_k^T gU -- with phase 6 fused with BK1 of layer k-1
+    BwdArgs b3 = a;
+    b3.KB = p.NB; b3.MBp = p.MBpm; b3.Krows = n; b3.Wp = Mt;
+    b3.S = AZ; b3.ldS = ldw;
+    if (fuse && k > 0) {
+      layer_args(b3, k - 1);           // the BK1 layer
+      b3.Pk = f.P + (int64_t)(k - 1) * ml;
+      b3.k3 = k;
+      b3.Tk3 = f.T + k * ml;
+      if (v == DLADMM_V1_LENA) { b3.b1e3 = f.beta1_elem[k]; b3.gb1e3 = d->g_beta1_elem[k]; }
+      b3.part3 = partk(k);
+      if (rowk)
+        if (hipError_t e = hipMemsetAsync(partk(k - 1), 0, part_bytes, s)) return (int)e;
+      if (hipError_t e = launch_bwd(6, v, b3, gm, p.SBm, s)) return (int)e;
+    } else {
+      if (hipError_t e = launch_bwd(3, v, b3, gm, p.SBm, s)) return (int)e;
+    }
+    float* const pk = partk(k);   // this layer's slots, for the reductions below
     // parameter slots: fixed-order fp64 sums of the per-wave partials
     if (v >= DLADMM_V4_SCALAR) {
       hipLaunchKernelGGL(param_reduce_kernel, dim3(DLADMM_NSCALAR), dim3(1024), 0, s,
-                         (const float*)part, p.nslots, p.gx * kBwdWaves * p.slices_m,
+                         (const float*)pk, p.nslots, p.gx * kBwdWaves * p.slices_m,
                          p.gx * kBwdWaves * p.slices_n,
                          d->g_scalar + (int64_t)k * DLADMM_NSCALAR);
       if (hipError_t e = hipGetLastError()) return (int)e;
     } else if (rowk) {
       hipLaunchKernelGGL(loss_reduce_kernel, dim3((unsigned)(DLADMM_NSCALAR * f.row_stride)),
-                         dim3(1024), 0, s, (const float*)part, p.ncg,
+                         dim3(1024), 0, s, (const float*)pk, p.ncg,
                          d->g_row + (int64_t)k * DLADMM_NSCALAR * f.row_stride);
       if (hipError_t e = hipGetLastError()) return (int)e;
     }

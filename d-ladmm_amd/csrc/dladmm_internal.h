@@ -145,6 +145,11 @@ struct BwdArgs {
   const float* b1e; const float* b2e; int64_t ldb;  // V1 betas of layer k
   float* gb1e; float* gb2e;                          // V1 beta grads of layer k
   float* part;
+  // PH 6 (BK3 of layer k3 fused with BK1 of layer k = k3 - 1): the BK3 layer's T_k3, V1 beta1 and
+  // its gradient, and the partial buffer of its parameter slot (beta1)
+  int k3;
+  const float* Tk3; const float* b1e3; float* gb1e3;
+  float* part3;
 };
 
 struct WgradArgs {

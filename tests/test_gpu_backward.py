@@ -243,12 +243,16 @@ def test_fused_training_loss(name, dl):
 
 @pytest.mark.parametrize("variant", ["v4", "v1", "v2", "v3", "v5", "v6"])
 @pytest.mark.parametrize("lossy", [False, True])
-def test_saved_product_backward_bit_identical(variant, lossy, dl):
+def test_saved_product_backward(variant, lossy, dl, monkeypatch):
     """A training forward on the fused kernel keeps P_k = A Z_k (fwd_desc.P) and BK1 reads it
-    instead of recomputing the product: the forward's own product, so every elementwise adjoint
-    and the weight and per-sample gradients equal the recomputing backward's bit for bit; the
-    parameter-slot sums agree to their fp32 partials' rounding; the saved P is A Z_k of the
-    returned Z_k."""
+    instead of recomputing the product, inside BK3's launch (phase 6).
+      (a) phase 6 == BK1 as its own launch (DLADMM_BWD_UNFUSED=1): every elementwise adjoint,
+          the weight and the per-sample gradients bit for bit, the parameter-slot sums to their
+          fp32 partials' rounding (the partials group the terms by wave differently);
+      (b) the saved P is A Z_k of the returned Z_k, and storing it changes no other output;
+      (c) a backward that recomputes P with the slice GEMM (a forward without P) agrees to fp32
+          rounding: the fused forward sums A Z_k in two accumulation chains, the slice GEMM in
+          one, so the recomputed P differs in the last bits."""
     from importlib import import_module
     ops = import_module("d-ladmm_amd.ops")
     m, n, B, K = 96, 200, 70, 4
@@ -281,17 +285,23 @@ def test_saved_product_backward_bit_identical(variant, lossy, dl):
     kw = dict(tied=net._shared_weight(), **tables)
     if lossy:
         kw.update(loss_kind=lk, loss_coef=torch.tensor([[1e-3, 1.0]] * K, device="cuda"))
-    res = [ops.dladmm_backward(*args, r, gz, ge, gl, gt, **kw) for r in (r1, r0)]
-    for f in ("gW", "g_scalar", "g_row"):
-        a, b = getattr(res[0], f), getattr(res[1], f)
-        assert (a is None) == (b is None)
-        if a is None:
-            continue
-        if f == "gW":
-            assert torch.equal(a, b), f
-        else:
-            # the GEMM-free BK1 maps a lane to one column (the recomputing one to the MFMA
-            # layout), so its per-wave partial sums group the same terms differently
-            assert nrel(a.cpu().numpy(), b.cpu().numpy()) <= 2e-6, f
-    for a, b in zip(res[0].g_beta1 + res[0].g_beta2, res[1].g_beta1 + res[1].g_beta2):
-        assert torch.equal(a, b)
+    fused = ops.dladmm_backward(*args, r1, gz, ge, gl, gt, **kw)
+    monkeypatch.setenv("DLADMM_BWD_UNFUSED", "1")
+    unfused = ops.dladmm_backward(*args, r1, gz, ge, gl, gt, **kw)
+    monkeypatch.delenv("DLADMM_BWD_UNFUSED")
+    recomp = ops.dladmm_backward(*args, r0, gz, ge, gl, gt, **kw)
+    for other, exact in ((unfused, True), (recomp, False)):
+        for f in ("gW", "g_scalar", "g_row"):
+            a, b = getattr(fused, f), getattr(other, f)
+            assert (a is None) == (b is None)
+            if a is None:
+                continue
+            if f == "gW" and exact:
+                assert torch.equal(a, b), f
+            else:
+                assert nrel(a.cpu().numpy(), b.cpu().numpy()) <= (2e-6 if exact else 1e-4), f
+        for a, b in zip(fused.g_beta1 + fused.g_beta2, other.g_beta1 + other.g_beta2):
+            if exact:
+                assert torch.equal(a, b)
+            else:
+                assert nrel(a.cpu().numpy(), b.cpu().numpy()) <= 1e-4
