@@ -26,7 +26,7 @@ P_BETA1, P_BETA2, P_BETA3, P_SS2, P_SS2B, P_THETA_E, P_THETA_Z, P_S1 = range(8)
 
 # every symbol include/dladmm.h declares (checked by tests/test_capi.py)
 EXPORTED = ("dladmm_abi_version", "dladmm_fwd_workspace_bytes", "dladmm_fwd_path",
-            "dladmm_fwd_f32", "dladmm_bwd_workspace_bytes", "dladmm_bwd_f32",
+            "dladmm_fwd_f32", "dladmm_bwd_workspace_bytes", "dladmm_bwd_path", "dladmm_bwd_f32",
             "dladmm_safeguard_f32", "dladmm_colobj_f32", "dladmm_error_string")
 # enum dladmm_mu_updater
 MU_NONE, MU_EMA, MU_GS, MU_RT = 0, 1, 2, 3
@@ -129,6 +129,8 @@ def lib():
     L.dladmm_fwd_f32.argtypes = [ctypes.POINTER(FwdDesc), ctypes.c_void_p]
     L.dladmm_bwd_workspace_bytes.restype = ctypes.c_size_t
     L.dladmm_bwd_workspace_bytes.argtypes = [ctypes.POINTER(BwdDesc)]
+    L.dladmm_bwd_path.restype = ctypes.c_int
+    L.dladmm_bwd_path.argtypes = [ctypes.POINTER(BwdDesc)]
     L.dladmm_bwd_f32.restype = ctypes.c_int
     L.dladmm_bwd_f32.argtypes = [ctypes.POINTER(BwdDesc), ctypes.c_void_p]
     L.dladmm_safeguard_f32.restype = ctypes.c_int

@@ -635,7 +635,20 @@ struct BwdPlan {
   bool saved_p;                   // BK1 reads the forward's A Z_k (fwd_desc.P)
   size_t off_a1, off_at, off_m, off_mt, off_az, off_ae, off_al, off_at_, off_gp, off_var,
       off_part, off_part2, off_wpart, total;
+  // reverse-sweep kernel (dladmm_reverse.hip): packed A^T and M_k^T, gU_k / Var_k of every
+  // layer (rows padded to Rn2 / Rm2 for the weight gradient), per-wave parameter partials
+  bool rev;
+  int rtiles, rncg;
+  int64_t Rn2, Rm2;
+  size_t off_ratp, off_rmtp, off_gu, off_rvar, off_rae, off_rpart;
 };
+
+// DLADMM_BWD_REV=0: the per-layer backward kernels even where the reverse-sweep kernel applies
+// (A/B timing and the equivalence tests)
+inline bool rev_enabled() {
+  const char* e = getenv("DLADMM_BWD_REV");
+  return !(e && e[0] == '0');
+}
 
 inline int validate_bwd(const dladmm_bwd_desc* d) {
   if (!d) return DLADMM_E_NULL;
@@ -692,6 +705,23 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   p->nslots = p->ncg * (p->slices_m > p->slices_n ? p->slices_m : p->slices_n);
   const int64_t rs = f.row_stride > 0 ? f.row_stride : 1;
   const int64_t part_floats = 8 * (p->nslots > rs * p->ncg ? (int64_t)p->nslots : rs * p->ncg);
+  // one reverse-sweep kernel: V4 / V6 after a saved-product fused forward, no upstream output
+  // cotangents (the fused objective is the training loss), 32-bit workspace offsets
+  p->rev = false;
+  if (p->saved_p && reverse_supports(f.variant) && !d->gZ && !d->gE && !d->gL && !d->gT &&
+      !d->gw_sum && rev_enabled()) {
+    const int MP = kShapeMP[p->fwd.shape], NP = kShapeNP[p->fwd.shape];
+    p->Rn2 = round_up(NP, 128);
+    p->Rm2 = round_up(MP, 128);
+    const int64_t lim = (int64_t)1 << 31;
+    if ((int64_t)NP * p->Bpad * 4 < lim && (int64_t)MP * p->Bpad * 4 < lim) {
+      p->rev = true;
+      p->Rn = p->Rn2;  // the weight gradient reads the reverse kernel's row padding
+      p->Rm = p->Rm2;
+      p->rtiles = ceil_div(f.batch, kTileCols);
+      p->rncg = p->rtiles * kWaves;
+    }
+  }
   p->wtiles = (int)((p->Rn / 128) * (p->Rm / 128));
   const int64_t steps = p->Bpad / 16;
   int64_t nch = (512 + p->wtiles - 1) / p->wtiles;
@@ -702,6 +732,19 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   const size_t fb = (size_t)kFrag * sizeof(float);
   const size_t colb = (size_t)p->Bpad * sizeof(float);
   size_t o = 0;
+  if (p->rev) {
+    const size_t wb = (size_t)kShapeMP[p->fwd.shape] * kShapeNP[p->fwd.shape] * sizeof(float);
+    const size_t K = (size_t)f.layers;
+    p->off_ratp = o; o += align256(wb);
+    p->off_rmtp = o; o += align256(wb * K);
+    p->off_gu = o; o += align256(colb * p->Rn2 * K);
+    p->off_rvar = o; o += align256(colb * p->Rm2 * K);
+    p->off_rae = o; o += align256(colb * kShapeMP[p->fwd.shape]);
+    p->off_rpart = o; o += align256(sizeof(float) * DLADMM_NSCALAR * K * p->rncg);
+    p->off_wpart = o; o += align256(sizeof(float) * (size_t)p->nchunks * n * m);
+    p->total = o;
+    return 0;
+  }
   p->off_a1 = o; o += align256(fb * p->NB * p->MBpm);     // A      [NB][MBpm]   (BK1)
   p->off_at = o; o += align256(fb * p->MB * p->NBpn);     // A^T    [MB][NBpn]   (BK2)
   p->off_m = o; o += align256(fb * p->MB * p->NBpn);      // M_k    [MB][NBpn]   (BK2)
@@ -719,7 +762,74 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   return 0;
 }
 
+// The reverse-sweep kernel: every layer's adjoints in one launch, then the weight gradients of
+// the K layers from the gU_k / Var_k it wrote, then the parameter slots.
+inline int run_reverse(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStream_t s) {
+  const dladmm_fwd_desc& f = d->fwd;
+  const int K = f.layers, m = f.m, n = f.n;
+  const int shape = p.fwd.shape, MP = kShapeMP[shape], NP = kShapeNP[shape];
+  const int MB = MP / 16, NB = NP / 16;
+  float* Atp = (float*)(ws + p.off_ratp);
+  float* Mtp = (float*)(ws + p.off_rmtp);
+  float* GU = (float*)(ws + p.off_gu);
+  float* VAR = (float*)(ws + p.off_rvar);
+  float* rpart = (float*)(ws + p.off_rpart);
+  float* wpart = (float*)(ws + p.off_wpart);
+  const int64_t ldw = p.Bpad, gus = p.Rn2 * ldw, vas = p.Rm2 * ldw;
+  // A^T (rows n, contraction m) and every M_k^T = (-s1 W_k)^T (rows m, contraction n), in the
+  // fused forward's paired fragment order
+  const float* asrc[1] = {f.A};
+  if (hipError_t e = pack(asrc, 1, n, m, f.ld_a, NB, MB, 2, Atp, s, 1.0f, nullptr, 1))
+    return (int)e;
+  if (hipError_t e = pack(f.W, K, m, n, f.ld_w, MB, NB, 2, Mtp, s, -1.0f, f.scalar_params, 1, 0))
+    return (int)e;
+  // slots a variant never writes stay 0; rows past NP / MP (to the weight gradient's 128-row
+  // tiles) are never written by the kernel
+  if (hipError_t e = hipMemsetAsync(rpart, 0, p.off_wpart - p.off_rpart, s)) return (int)e;
+  for (int k = 0; k < K && (p.Rn2 > NP || p.Rm2 > MP); ++k) {
+    if (p.Rn2 > NP)
+      if (hipError_t e = hipMemsetAsync(GU + k * gus + NP * ldw, 0,
+                                        (size_t)(p.Rn2 - NP) * ldw * sizeof(float), s))
+        return (int)e;
+    if (p.Rm2 > MP)
+      if (hipError_t e = hipMemsetAsync(VAR + k * vas + MP * ldw, 0,
+                                        (size_t)(p.Rm2 - MP) * ldw * sizeof(float), s))
+        return (int)e;
+  }
+  RevArgs r{};
+  r.m = m; r.n = n; r.B = (int)f.batch; r.K = K;
+  r.loss_kind = d->loss_kind; r.ncg = p.rncg;
+  r.Bw = p.Bpad;
+  r.X = f.X; r.ldx = f.ld_x;
+  r.E0 = f.E0; r.lde0 = f.ld_e0;
+  r.L0 = f.L0; r.ldl0 = f.ld_l0;
+  r.Z = f.Z; r.E = f.E; r.L = f.L; r.T = f.T; r.P = f.P; r.ldo = f.ld_out;
+  r.Atp = Atp; r.Mtp = Mtp;
+  r.scal = f.scalar_params;
+  r.lcoef = d->loss_kind ? d->loss_coef : nullptr;
+  r.GU = GU; r.VAR = VAR; r.ldw = ldw; r.gus = gus; r.vas = vas;
+  r.AEw = (float*)(ws + p.off_rae);
+  r.part = rpart;
+  if (hipError_t e = launch_reverse_shape(shape, f.variant, r, p.rtiles, s)) return (int)e;
+  // weight gradients gW_k = -s1 gU_k Var_k^T (split-K over the batch, fixed-order reduction)
+  for (int k = 0; k < K; ++k) {
+    WgradArgs wa{};
+    wa.G = GU + k * gus; wa.V = VAR + k * vas; wa.ld = ldw; wa.n = n; wa.m = m;
+    wa.NBp16 = (int)(p.Rn2 / 16); wa.MBp16 = (int)(p.Rm2 / 16);
+    wa.Bpad = p.Bpad; wa.chunk = p.chunk; wa.nchunks = p.nchunks; wa.part = wpart;
+    if (hipError_t e = launch_wgrad(wa, p.wtiles, s)) return (int)e;
+    if (hipError_t e = launch_wgrad_reduce(wpart, p.nchunks, n, m, f.scalar_params, k, 0,
+                                           d->gW + (int64_t)k * n * d->ld_gw, d->ld_gw, s))
+      return (int)e;
+  }
+  // parameter slots of every layer: fixed-order fp64 sums of the per-wave partials
+  hipLaunchKernelGGL(loss_reduce_kernel, dim3((unsigned)(DLADMM_NSCALAR * K)), dim3(1024), 0, s,
+                     (const float*)rpart, p.rncg, d->g_scalar);
+  return (int)hipGetLastError();
+}
+
 inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStream_t s) {
+  if (p.rev) return run_reverse(d, p, ws, s);
   const dladmm_fwd_desc& f = d->fwd;
   const int K = f.layers, m = f.m, n = f.n;
   const int64_t B = f.batch, ldo = f.ld_out, ldw = p.Bpad;
@@ -942,6 +1052,14 @@ size_t dladmm_bwd_workspace_bytes(const dladmm_bwd_desc* d) {
   BwdPlan p;
   if (make_bwd_plan(d, &p)) return 0;
   return p.total;
+}
+
+int dladmm_bwd_path(const dladmm_bwd_desc* d) {
+  using namespace dladmm;
+  if (int e = validate_bwd(d)) return e;
+  BwdPlan p;
+  if (int e = make_bwd_plan(d, &p)) return e;
+  return p.rev ? 1 : 0;
 }
 
 int dladmm_bwd_f32(const dladmm_bwd_desc* d, void* stream) {

@@ -170,6 +170,29 @@ static_assert(sizeof(LayerArgs) <= 2048, "kernel argument size");
 static_assert(sizeof(BwdArgs) <= 2048, "kernel argument size");
 static_assert(sizeof(WgradArgs) <= 2048, "kernel argument size");
 hipError_t launch_wgrad(const WgradArgs& a, int tiles, hipStream_t s);
+
+// ---- backward as one reverse sweep (dladmm_reverse.hip): V4 / V6 after a saved-product fused
+// forward, register-resident shapes (kShapeMP / kShapeNP), no upstream output cotangents
+struct RevArgs {
+  int m, n, B, K;
+  int loss_kind, ncg;              // ncg: waves (column groups) = partial entries per slot
+  int64_t Bw;                      // padded batch of the gU / Var workspaces (stored as zeros)
+  const float* X; int64_t ldx;
+  const float* E0; int64_t lde0;
+  const float* L0; int64_t ldl0;
+  const float* Z; const float* E; const float* L; const float* T; const float* P;
+  int64_t ldo;                     // the forward's outputs: Z, E, L, P [K][.][ldo], T [K+1]
+  const float* Atp;                // packed A^T            [NB/2][MB][2] fragments (pair order)
+  const float* Mtp;                // packed (-s1 W_k)^T [K][MB/2][NB][2]
+  const float* scal;               // [K][8]
+  const float* lcoef;              // fused objective [K][2] (cz_k, cf_k), or null
+  float* GU; float* VAR; int64_t ldw, gus, vas;   // gU_k [K][gus], Var_k [K][vas], row stride ldw
+  float* AEw;                      // V4: adjoint of E rows [MP][ldw] (carried between layers)
+  float* part;                     // parameter partials [K][8][ncg]
+};
+static_assert(sizeof(RevArgs) <= 2048, "kernel argument size");
+bool reverse_supports(int variant);
+hipError_t launch_reverse_shape(int shape, int variant, const RevArgs& a, int grid, hipStream_t s);
 hipError_t launch_wgrad_reduce(const float* part, int nchunks, int n, int m, const float* scal,
                                int k, int accumulate, float* gW, int64_t ldgw, hipStream_t s);
 

@@ -207,6 +207,7 @@ class BackwardResult:
     g_row: Optional[torch.Tensor]     # [K, 8, R] fp64 (V2, V3)
     g_beta1: List[torch.Tensor]       # V1: K tensors (m, B)
     g_beta2: List[torch.Tensor]
+    path: int = 0                     # dladmm_bwd_path: 1 = one reverse-sweep kernel, 0 = per layer
 
 
 def dladmm_backward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[torch.Tensor],
@@ -295,12 +296,13 @@ def dladmm_backward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[
     wsb = L.dladmm_bwd_workspace_bytes(ctypes.byref(d))
     if wsb == 0:
         raise ValueError("dladmm: invalid backward descriptor")
+    path = L.dladmm_bwd_path(ctypes.byref(d))
     ws = _workspace(dev, wsb)
     d.workspace, d.workspace_bytes = ws.data_ptr(), wsb
     stream = torch.cuda.current_stream(dev).cuda_stream
     _lib.check(L.dladmm_bwd_f32(ctypes.byref(d), ctypes.c_void_p(stream)))
     del keep
-    return BackwardResult(gWo, g_scalar, g_row, g1, g2)
+    return BackwardResult(gWo, g_scalar, g_row, g1, g2, path)
 
 
 _WS: "OrderedDict" = None

@@ -233,6 +233,11 @@ typedef struct dladmm_bwd_desc {
 /* Workspace the backward needs for this descriptor (0 on an invalid descriptor). */
 size_t dladmm_bwd_workspace_bytes(const dladmm_bwd_desc* d);
 
+/* Which kernels the backward runs: 1 = one reverse-sweep kernel for every layer's adjoints
+   (V4 / V6 after a fused-path forward that saved P, no upstream output cotangents: the fused
+   training objective), 0 = per-layer kernels, <0 = DLADMM_E_* error. */
+int dladmm_bwd_path(const dladmm_bwd_desc* d);
+
 /* Enqueue the whole reverse sweep on `stream` (hipStream_t).  Deterministic: every reduction
    (parameter slots, per-row params, weight gradients) is summed in a fixed order. */
 int dladmm_bwd_f32(const dladmm_bwd_desc* d, void* stream);

@@ -1,0 +1,110 @@
+"""The backward as one reverse-sweep kernel (csrc/dladmm_reverse.hip, dladmm_bwd_path() == 1)
+against the per-layer backward kernels (DLADMM_BWD_REV=0), on the same saved forward.
+
+The reverse kernel forms every product as the per-layer kernels do (one fma chain per output
+block, k in the same order) and every elementwise adjoint with the same expressions, so
+  * the weight gradients -- built from gU_k and Var_k -- are equal bit for bit;
+  * the parameter-slot gradients agree to the rounding of their fp32 per-wave partials (the
+    kernels group the terms by wave differently): 2e-6 norm-relative per layer.
+Covered: V4 (L1L1 and LASSO objective) and V6, the three register-resident shapes with ragged
+rows and columns, K = 1, theta < 0 layers (the shrink masks come from the saved Z_k), a batch
+that is not a multiple of 16 (zero padding of the gU / Var rows the weight gradient reads).
+Against the reference: tests/test_gpu_backward.py::test_fused_training_loss runs V4 / V6
+through this kernel (the fused objective), compared with the reference autograd and the oracle.
+"""
+from importlib import import_module
+
+import numpy as np
+import pytest
+import torch
+
+import problems as P
+from test_gpu_backward import make_train_net, nrel
+
+pytestmark = pytest.mark.gpu
+
+
+def saved_forward(dl, variant, m, n, B, K, seed, negtheta=False, lk=0):
+    ops = import_module("d-ladmm_amd.ops")
+    d = dict(variant=variant, m=m, n=n, B=B, K=K, seed=seed, perturb=0.1, negtheta=negtheta)
+    inp, sd = P.build_problem(d)
+    net = make_train_net(dl, variant, inp, sd, K).cuda()
+    X = torch.from_numpy(inp["X"]).cuda()
+    with torch.no_grad():
+        tables = net._tables(X.device)
+    W = [w.detach() for w in net._weights()]
+    args = (net.VARIANT, X, net.A, W, net.Z0, net.E0, net.L0)
+    with torch.no_grad():
+        r = ops.dladmm_forward(*args, keep_all=True, want_T=True, want_P=True, loss_kind=lk,
+                               **tables)
+    assert r.P is not None
+    return ops, args, r, tables
+
+
+def both(dl, variant, m, n, B, K, seed, kind, monkeypatch, negtheta=False):
+    lk = dl._lib.LOSS_LASSO if kind == "lasso" else dl._lib.LOSS_L1L1
+    ops, args, r, tables = saved_forward(dl, variant, m, n, B, K, seed, negtheta, lk)
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    coef = (torch.rand(K, 2, device="cuda", generator=g) * torch.tensor([1e-2, 1.0],
+                                                                           device="cuda")).contiguous()
+    kw = dict(loss_kind=lk, loss_coef=coef, **tables)
+    rev = ops.dladmm_backward(*args, r, **kw)
+    monkeypatch.setenv("DLADMM_BWD_REV", "0")
+    per = ops.dladmm_backward(*args, r, **kw)
+    monkeypatch.delenv("DLADMM_BWD_REV")
+    return rev, per
+
+
+def check_equal(rev, per, K):
+    assert rev.path == 1 and per.path == 0
+    assert torch.equal(rev.gW, per.gW)
+    gs_r = rev.g_scalar.cpu().numpy()
+    gs_p = per.g_scalar.cpu().numpy()
+    from importlib import import_module
+    lib = import_module("d-ladmm_amd._lib")
+    used = [s for s in range(lib.NSCALAR) if s != lib.P_S1]  # S1: defined for V5 only
+    for k in range(K):
+        e = nrel(gs_r[k, used], gs_p[k, used])
+        assert e <= 2e-6, (k, e, gs_r[k, used], gs_p[k, used])
+
+
+@pytest.mark.parametrize("variant,kind", [("v4", "l1l1"), ("v4", "lasso"), ("v6", "lasso")])
+@pytest.mark.parametrize("shape", [(20, 30, 70, 3), (64, 200, 333, 2), (250, 500, 200, 4),
+                                   (256, 512, 64, 1)])
+def test_reverse_matches_per_layer(variant, kind, shape, dl, monkeypatch):
+    m, n, B, K = shape
+    rev, per = both(dl, variant, m, n, B, K, 9700 + m, kind, monkeypatch)
+    check_equal(rev, per, K)
+
+
+@pytest.mark.parametrize("variant", ["v4", "v6"])
+def test_reverse_negative_thresholds(variant, dl, monkeypatch):
+    """theta_z, theta_e < 0 on every other layer: both relus open where |U| < |theta|; the
+    reverse kernel reads S'(U) off the saved Z_k (|Z| < 2|theta| there), the per-layer kernels
+    recompute U = Z_{k-1} - W_k Var_k (phase 2)."""
+    rev, per = both(dl, variant, 96, 200, 150, 4, 9800, "l1l1", monkeypatch, negtheta=True)
+    check_equal(rev, per, 4)
+
+
+def test_reverse_headline_shape_columns(dl, monkeypatch):
+    """The training bench's shape (V4, m=256, n=512, K=15) at 4,096 columns (64 workgroups)."""
+    rev, per = both(dl, "v4", 256, 512, 4096, 15, 9900, "l1l1", monkeypatch)
+    check_equal(rev, per, 15)
+
+
+def test_reverse_deterministic(dl):
+    ops, args, r, tables = saved_forward(dl, "v4", 64, 200, 333, 3, 9950, lk=dl._lib.LOSS_L1L1)
+    coef = torch.tensor([[1e-3, 1.0]] * 3, device="cuda")
+    kw = dict(loss_kind=dl._lib.LOSS_L1L1, loss_coef=coef, **tables)
+    a = ops.dladmm_backward(*args, r, **kw)
+    b = ops.dladmm_backward(*args, r, **kw)
+    assert a.path == 1
+    assert torch.equal(a.gW, b.gW) and torch.equal(a.g_scalar, b.g_scalar)
+
+
+def test_upstream_cotangents_use_per_layer_kernels(dl):
+    """Output cotangents (a torch loss on the outputs) keep the per-layer kernels."""
+    ops, args, r, tables = saved_forward(dl, "v4", 64, 200, 70, 2, 9960)
+    gz = [torch.ones(200, 70, device="cuda") for _ in range(2)]
+    res = ops.dladmm_backward(*args, r, gz, **tables)
+    assert res.path == 0
