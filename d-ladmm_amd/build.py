@@ -30,7 +30,8 @@ FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", f"--offload-arch={AR
          "-I", os.path.join(ROOT, "include")]
 # per-unit extras: the split-f16 kernel keeps scalar f32 VALU beside its MFMAs (packed v_pk_*
 # f32 ops issue slower there; MI355X_MICROARCH.md, price of one filler beside MFMAs)
-UNIT_FLAGS = {"dladmm_fused_x3.hip": ["-fno-slp-vectorize"]}
+UNIT_FLAGS = {"dladmm_fused_x3.hip": ["-fno-slp-vectorize"],
+              "dladmm_reverse.hip": ["-fno-slp-vectorize"]}
 
 
 def hipcc() -> str:

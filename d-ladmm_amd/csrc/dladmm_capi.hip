@@ -640,7 +640,7 @@ struct BwdPlan {
   bool rev;
   int rtiles, rncg;
   int64_t Rn2, Rm2;
-  size_t off_ratp, off_rmtp, off_gu, off_rvar, off_rae, off_rpart;
+  size_t off_ratp, off_rmtp, off_gu, off_rvar, off_rpart;
 };
 
 // DLADMM_BWD_REV=0: the per-layer backward kernels even where the reverse-sweep kernel applies
@@ -708,13 +708,14 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   // one reverse-sweep kernel: V4 / V6 after a saved-product fused forward, no upstream output
   // cotangents (the fused objective is the training loss), 32-bit workspace offsets
   p->rev = false;
+  // (E0 / L0 addressed with the outputs' row stride)
   if (p->saved_p && reverse_supports(f.variant) && !d->gZ && !d->gE && !d->gL && !d->gT &&
-      !d->gw_sum && rev_enabled()) {
+      !d->gw_sum && f.ld_e0 == f.ld_out && f.ld_l0 == f.ld_out && rev_enabled()) {
     const int MP = kShapeMP[p->fwd.shape], NP = kShapeNP[p->fwd.shape];
     p->Rn2 = round_up(NP, 128);
     p->Rm2 = round_up(MP, 128);
     const int64_t lim = (int64_t)1 << 31;
-    if ((int64_t)NP * p->Bpad * 4 < lim && (int64_t)MP * p->Bpad * 4 < lim) {
+    if ((int64_t)NP * p->Bpad * 4 < lim && 2 * (p->Rm2 + MP) * p->Bpad * 4 < lim) {
       p->rev = true;
       p->Rn = p->Rn2;  // the weight gradient reads the reverse kernel's row padding
       p->Rm = p->Rm2;
@@ -738,8 +739,9 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
     p->off_ratp = o; o += align256(wb);
     p->off_rmtp = o; o += align256(wb * K);
     p->off_gu = o; o += align256(colb * p->Rn2 * K);
-    p->off_rvar = o; o += align256(colb * p->Rm2 * K);
-    p->off_rae = o; o += align256(colb * kShapeMP[p->fwd.shape]);
+    // per layer: Var_k rows (Rm2, zero padded for the weight gradient), then MP rows of the
+    // adjoint of E_{k-1} (V4) that the next-lower layer's BK1 reads
+    p->off_rvar = o; o += align256(colb * (p->Rm2 + kShapeMP[p->fwd.shape]) * K);
     p->off_rpart = o; o += align256(sizeof(float) * DLADMM_NSCALAR * K * p->rncg);
     p->off_wpart = o; o += align256(sizeof(float) * (size_t)p->nchunks * n * m);
     p->total = o;
@@ -775,7 +777,7 @@ inline int run_reverse(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hip
   float* VAR = (float*)(ws + p.off_rvar);
   float* rpart = (float*)(ws + p.off_rpart);
   float* wpart = (float*)(ws + p.off_wpart);
-  const int64_t ldw = p.Bpad, gus = p.Rn2 * ldw, vas = p.Rm2 * ldw;
+  const int64_t ldw = p.Bpad, gus = p.Rn2 * ldw, vas = (p.Rm2 + MP) * ldw;
   // A^T (rows n, contraction m) and every M_k^T = (-s1 W_k)^T (rows m, contraction n), in the
   // fused forward's paired fragment order
   const float* asrc[1] = {f.A};
@@ -808,7 +810,7 @@ inline int run_reverse(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hip
   r.scal = f.scalar_params;
   r.lcoef = d->loss_kind ? d->loss_coef : nullptr;
   r.GU = GU; r.VAR = VAR; r.ldw = ldw; r.gus = gus; r.vas = vas;
-  r.AEw = (float*)(ws + p.off_rae);
+  r.aer = p.Rm2;
   r.part = rpart;
   if (hipError_t e = launch_reverse_shape(shape, f.variant, r, p.rtiles, s)) return (int)e;
   // weight gradients gW_k = -s1 gU_k Var_k^T (split-K over the batch, fixed-order reduction)

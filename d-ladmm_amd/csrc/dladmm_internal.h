@@ -187,7 +187,8 @@ struct RevArgs {
   const float* scal;               // [K][8]
   const float* lcoef;              // fused objective [K][2] (cz_k, cf_k), or null
   float* GU; float* VAR; int64_t ldw, gus, vas;   // gU_k [K][gus], Var_k [K][vas], row stride ldw
-  float* AEw;                      // V4: adjoint of E rows [MP][ldw] (carried between layers)
+  int64_t aer;                     // V4: rows aer.. of layer k's Var block hold the adjoint of
+                                   // E_{k-1} (carried from BK1(k) to BK1(k-1))
   float* part;                     // parameter partials [K][8][ncg]
 };
 static_assert(sizeof(RevArgs) <= 2048, "kernel argument size");

@@ -11,8 +11,8 @@
 //    (n rows) and the partial adjoint of L_{k-1} (m rows) -- and gP (m rows) stay in registers
 //    for all K layers, in the C/D layout of v_mfma_f32_16x16x4_f32 (lane l: column l & 15, rows
 //    16 b + 4 (l >> 4) + r); X sits in LDS.  The adjoint of E_{k-1} (V4 only; V6's E-step has
-//    no E term) round-trips through a workspace row buffer, read one block ahead with the saved
-//    state: in registers it would push the kernel past the 512-register budget (spills);
+//    no E term) round-trips through the workspace rows after Var_k's, read one block ahead with
+//    the saved state: in registers it would push the kernel past the 512-register budget;
 //  * per layer k = K-1 .. 0, two products shaped exactly like the forward's two:
 //      G1'(k)  R    = A^T gP_k     rows n, contraction m  (B operand gP_k, registers)
 //      G2'(k)  gVar = M_k^T gU_k   rows m, contraction n  (B operand gU_k, registers)
@@ -36,8 +36,9 @@
 #include "dladmm_internal.h"
 
 #ifndef REV_ABL
-#define REV_ABL 0  // register-pressure experiments only (WRONG results): 1 no prologue rows,
-                   // 2 no G2' rows, 4 no G1' rows
+#define REV_ABL 0  // timing / register-pressure experiments only (WRONG results): 1 no prologue
+                   // rows, 2 no G2' rows, 4 no G1' rows, 8 no Z_k loads, 16 no gU stores, 32 no
+                   // G2' operand loads, 64 no Var / adjoint-of-E stores
 #endif
 
 namespace dladmm {
@@ -147,15 +148,22 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   const bool cv = col < a.B;
   const int m = a.m, K = a.K;
   const int cg = blockIdx.x * kWaves + w;  // column group (wave) index of the partials
-  const bool lossq = __builtin_amdgcn_readfirstlane(a.loss_kind) == DLADMM_LOSS_LASSO;
+  const uint32_t lqm = __builtin_amdgcn_readfirstlane(a.loss_kind) == DLADMM_LOSS_LASSO ? ~0u : 0u;
   const int64_t ldo = a.ldo, ml = (int64_t)m * ldo, zl = (int64_t)a.n * ldo;
   auto lane_off = [&](int64_t ld, bool ok) -> uint32_t {
     return ok ? (uint32_t)((col + (int64_t)(4 * g) * ld) * 4) : kOOB;
   };
   const uint32_t vo = lane_off(ldo, cv);          // saved forward state
-  const uint32_t ve0 = lane_off(a.lde0, cv), vl0 = lane_off(a.ldl0, cv);
   const uint32_t vw = lane_off(a.ldw, col < a.Bw);  // gU / Var workspaces (padding: zeros)
   const rsrc_t none = mkrsrc(nullptr, 0u);
+  // buffer view of a wave-uniform (pointer, size) formed by runtime selects: readfirstlane keeps
+  // both in SGPRs (otherwise a select lands in VGPRs and every access becomes a waterfall loop)
+  auto urs = [](const float* p, uint32_t bytes) -> rsrc_t {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return mkrsrc((const float*)(((uint64_t)hi << 32) | lo), __builtin_amdgcn_readfirstlane(bytes));
+  };
 
   // adjoint state: of Z (AZ; gU once G1' formed it), of E_{k-1} (AE), partial adjoint of
   // L_{k-1} (AL), and gP (the G1' B operand).  AZ and GP are MFMA operands: AGPRs
@@ -252,36 +260,34 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   // ---------------------------------------------------------------- operand views
   // BK1 of layer j reads P_j, E_{j-1}, L_{j-1} (E0 / L0 for j = 0, their own strides), T_j;
   // the last G2' pass (BK3 of layer 0 alone) reads T_0 through the P slot
-  struct R2 { rsrc_t P, E, L, T; uint32_t voE, voL, ldE4, ldL4; };
+  struct R2 { rsrc_t P, E, L, T; };
   const uint32_t mbytes = (uint32_t)(ml * 4), ldo4 = (uint32_t)(ldo * 4);
   auto res2 = [&](int j) -> R2 {
     R2 o;
-    o.P = mkrsrc(a.P + j * ml, mbytes);
-    o.T = mkrsrc(a.T + j * ml, mbytes);
-    if (j >= 1) {
-      o.E = mkrsrc(a.E + (j - 1) * ml, mbytes);
-      o.L = mkrsrc(a.L + (j - 1) * ml, mbytes);
-      o.voE = vo; o.voL = vo; o.ldE4 = ldo4; o.ldL4 = ldo4;
-    } else {
-      o.E = mkrsrc(a.E0, (uint32_t)(m * a.lde0 * 4));
-      o.L = mkrsrc(a.L0, (uint32_t)(m * a.ldl0 * 4));
-      o.voE = ve0; o.voL = vl0;
-      o.ldE4 = (uint32_t)(a.lde0 * 4); o.ldL4 = (uint32_t)(a.ldl0 * 4);
-    }
+    o.P = urs(a.P + j * ml, mbytes);
+    o.T = urs(a.T + j * ml, mbytes);
+    // E0 / L0 share the outputs' row stride (host: dladmm_capi.hip make_bwd_plan)
+    o.E = urs(j >= 1 ? a.E + (j - 1) * ml : a.E0, mbytes);
+    o.L = urs(j >= 1 ? a.L + (j - 1) * ml : a.L0, mbytes);
     return o;
   };
   auto res2_last = [&]() -> R2 {
-    return R2{mkrsrc(a.T, mbytes), none, none, none, vo, vo, ldo4, ldo4};
+    return R2{mkrsrc(a.T, mbytes), none, none, none};
   };
-  auto rz = [&](int k) { return mkrsrc(a.Z + k * zl, (uint32_t)(zl * 4)); };
-  auto rgu = [&](int k) { return mkrsrc(a.GU + k * a.gus, (uint32_t)(NP * a.ldw * 4)); };
-  auto rvar = [&](int j) { return mkrsrc(a.VAR + j * a.vas, (uint32_t)(MP * a.ldw * 4)); };
+  auto rz = [&](int k) { return urs(a.Z + k * zl, (uint32_t)(zl * 4)); };
+  auto rgu = [&](int k) { return urs(a.GU + k * a.gus, (uint32_t)(NP * a.ldw * 4)); };
+  // Var_j (rows 0..) and the adjoint of E_{j-1} (rows aeo / 4 / ldw ..) of layer j, plus the
+  // next layer's block, which holds the adjoint of E_j that BK1(j) reads
+  auto rvar = [&](int j) {
+    return urs(a.VAR + j * a.vas, (uint32_t)((j + 1 < K ? 2 : 1) * a.vas * 4));
+  };
 
   // uniform row offsets: loads of the pair being fetched, stores of the rows being finished
-  SWalk wZ{0u, ldo4}, wPT{0u, ldo4}, wE{0u, ldo4}, wL{0u, ldo4};
+  SWalk wZ{0u, ldo4}, wPT{0u, ldo4};
   const uint32_t ldw4 = (uint32_t)(a.ldw * 4);
+  const uint32_t aeo = (uint32_t)(a.aer * a.ldw * 4);  // byte offset of the adjoint-of-E rows
+  const uint32_t vas4 = (uint32_t)(a.vas * 4);
   SWalk wG{0u, ldw4}, wV{0u, ldw4}, wA{0u, ldw4};
-  const rsrc_t rae = mkrsrc(kAE ? a.AEw : nullptr, kAE ? (uint32_t)(MP * a.ldw * 4) : 0u);
   auto ld = [](rsrc_t r, uint32_t voff, uint32_t soff) -> float {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
   };
@@ -290,19 +296,25 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
     pz[h][rr] = ld(r, vo, wZ.at(rr));
     if (rr == 3) wZ.next();
   };
-  // G2' operands, one block ahead: slot rr <- row rr of the next block
-  auto pre2 = [&](const R2& o, int rr) {
+  // G2' operands, one block ahead: slot rr <- row rr of the next block (rv: this pass's Var
+  // view, whose next-layer block holds the incoming adjoint of E)
+  auto pre2 = [&](const R2& o, rsrc_t rv, int rr) {
+    if constexpr (REV_ABL & 32) {
+      pv[rr][0] = 0.5f; pv[rr][1] = 0.25f; pv[rr][2] = 0.125f; pv[rr][3] = 1.f; pv[rr][4] = 0.f;
+      return;
+    }
     const uint32_t so = wPT.at(rr);
     pv[rr][0] = ld(o.P, vo, so);
-    pv[rr][1] = ld(o.E, o.voE, wE.at(rr));
-    pv[rr][2] = ld(o.L, o.voL, wL.at(rr));
+    pv[rr][1] = ld(o.E, vo, so);
+    pv[rr][2] = ld(o.L, vo, so);
     pv[rr][3] = ld(o.T, vo, so);
-    if constexpr (kAE) pv[rr][4] = ld(rae, vw, wA.at(rr));
-    if (rr == 3) { wPT.next(); wE.next(); wL.next(); wA.next(); }
+    if constexpr (kAE) pv[rr][4] = ld(rv, vw, wA.at(rr));
+    if (rr == 3) { wPT.next(); wA.next(); }
   };
-  auto reset2 = [&](const R2& o) {
-    wPT.reset(); wE.reset(); wL.reset(); wA.reset();
-    wE.ld4 = o.ldE4; wL.ld4 = o.ldL4;
+  auto reset2 = [&]() {
+    wPT.reset();
+    wA.cur = __builtin_amdgcn_readfirstlane(vas4 + aeo);
+    asm volatile("" : "+s"(wA.cur));
   };
 
   // partial of (layer, slot): one fixed-order sum per wave, written by lane 0
@@ -330,11 +342,14 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
     if constexpr (REV_ABL & 4) { AZ[b][r] = q[r]; pin_agpr(AZ[b][r]); return; }
     const float zk = pz[h][r];
     float gZt = AZ[b][r] + q[r];
-    gZt = gZt + P1.cz * (zk > 0.f ? 1.f : (zk < 0.f ? -1.f : 0.f));  // d/dZ_k of cz_k sum|Z_k|
-    // [U - th > 0], [-U - th > 0] from Z_k = S(U, th)
-    const float pp = zk > -P1.c ? 1.f : 0.f, qq = zk < P1.c ? 1.f : 0.f;
-    const float gU = gZt * (pp + qq);
-    psz += gZt * (qq - pp);
+    // + d/dZ_k of cz_k sum|Z_k|: cz_k sgn(Z_k) is exact, so the fma is phase 5's mul + add
+    const float sg = (zk > 0.f ? 1.f : 0.f) - (zk < 0.f ? 1.f : 0.f);
+    gZt = __builtin_fmaf(P1.cz, sg, gZt);
+    // S'(U) = [U - th > 0] + [-U - th > 0] in {0, 1, 2}, from Z_k = S(U, th); gZt * S' as a
+    // sum of selected gZt (exact), d/dth = [-U - th > 0] - [U - th > 0]
+    const float ga = zk > -P1.c ? gZt : 0.f, gb = zk < P1.c ? gZt : 0.f;
+    const float gU = ga + gb;
+    psz += gb - ga;
     asm volatile("" : "+v"(psz));
     AZ[b][r] = gU;  // adjoint of Z_{k-1}
     pin_agpr(AZ[b][r]);
@@ -353,7 +368,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
       psb1 += gVar * pv[r][0];
       asm volatile("" : "+v"(psb1));
       bstore_s(rv, vw, wV.at(r), 0.f);  // keeps the row's VM count (rv: no records)
-      if constexpr (kAE) bstore_s(rv, vw, wV.at(r), 0.f);
+      if constexpr (kAE) bstore_s(rv, vw, wV.at(r) + aeo, 0.f);
       if (r == 3) wV.next();
       return;
     } else {
@@ -375,10 +390,11 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
         const float gTn = aT + P.b3 * aL;
         p3 = aL * t;
         const float gEt = aE + gTn;
-        const float da = (eh - P.the) > 0.0f ? 1.0f : 0.0f;
-        const float db = (-eh - P.the) > 0.0f ? 1.0f : 0.0f;
-        const float gEh = gEt * (da + db);
-        pe = gEt * (db - da);
+        // shrink' = [eh - th > 0] + [-eh - th > 0]: gEt times it as a sum of selected gEt
+        const float ga = (eh - P.the) > 0.0f ? gEt : 0.f;
+        const float gb = (-eh - P.the) > 0.0f ? gEt : 0.f;
+        const float gEh = ga + gb;
+        pe = gb - ga;
         const float gVV = -P.ss2 * gEh;
         ps2 = -gEh * vv;
         gLp = aL + gVV;
@@ -398,7 +414,10 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
       }
       {  // d/dP of cf * fit (fit = sum|X - P|, torch sgn(0) = 0, or 0.5 sum (X - P)^2)
         const float res = x - Pv;
-        const float dfit = lossq ? res : (res > 0.f ? 1.f : (res < 0.f ? -1.f : 0.f));
+        const float sg = (res > 0.f ? 1.f : 0.f) - (res < 0.f ? 1.f : 0.f);
+        // uniform select by bit mask (a per-row branch here splits the unrolled body)
+        const float dfit = __builtin_bit_cast(
+            float, (lqm & __builtin_bit_cast(uint32_t, res)) | (~lqm & __builtin_bit_cast(uint32_t, sg)));
         gP = gP - P.cf * dfit;
       }
       if constexpr (MODE == 0) {
@@ -412,8 +431,12 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
       GP[b][r] = gP;
       pin_agpr(GP[b][r]);
       AL[b][r] = gLp;
-      bstore_s(rv, vw, wV.at(r), lp + P.b1 * tk);  // Var_{k-1} = L_{k-2} + b1 T_{k-1}
-      if constexpr (kAE) bstore_s(rae, vw, wV.at(r), gEp);  // adjoint of E_{k-2}
+      if constexpr (!(REV_ABL & 64)) {
+        bstore_s(rv, vw, wV.at(r), lp + P.b1 * tk);  // Var_{k-1} = L_{k-2} + b1 T_{k-1}
+        if constexpr (kAE) bstore_s(rv, vw, wV.at(r) + aeo, gEp);  // adjoint of E_{k-2}
+      } else {
+        asm volatile("" ::"v"(gEp), "v"(lp + P.b1 * tk));
+      }
       if (r == 3) wV.next();
     }
   };
@@ -458,9 +481,9 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
     const LP2 P = lp2(K, K - 1);
     const R2 o = res2(K - 1);
     const rsrc_t rv = rvar(K - 1);
-    reset2(o);
+    reset2();
     wV.reset();
-    static_for<4>([&](auto R_) { pre2(o, decltype(R_)::value); });
+    static_for<4>([&](auto R_) { pre2(o, rv, decltype(R_)::value); });
     static_for<MB / 2>([&](auto P_) {
       constexpr int p = decltype(P_)::value;
       load_x(p);
@@ -469,7 +492,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
         constexpr int h = i / 4, r = i % 4;
         if constexpr (!(REV_ABL & 1))
         epi2_row(std::integral_constant<int, 2>{}, P, rv, 2 * p + h, r, zero4, h ? xb : xa);
-        if constexpr (2 * p + h + 1 < MB) pre2(o, r);  // block 2p+h+1's row r
+        if constexpr (2 * p + h + 1 < MB) pre2(o, rv, r);  // block 2p+h+1's row r
       });
     });
     flush_bk1(K - 1);
@@ -505,7 +528,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
               if constexpr (!FIRST) {
                 epi2_row(std::integral_constant<int, 0>{}, Pp, rvp, MB - 2 + h, r,
                          h ? qb : qa, h ? xb : xa);
-                if constexpr (h == 0) pre2(op, r);  // the last block's row r
+                if constexpr (h == 0) pre2(op, rvp, r);  // the last block's row r
                 if constexpr (i == 7) {
                   flush(k + 1, DLADMM_P_BETA1, psb1);
                   psb1 = 0.f;
@@ -547,7 +570,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
     constexpr bool LAST = decltype(LAST_)::value;
     const int gi = 2 * (K - 1 - k) + 1;
     wV.reset();
-    reset2(o);
+    reset2();
     static_for<MB / 2>([&](auto P_) {
       constexpr int p = decltype(P_)::value;
       f32x4 ca = zero4, cb = zero4;
@@ -570,14 +593,14 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
             } else {
               epi2_row(std::integral_constant<int, LAST ? 1 : 0>{}, P, rv, 2 * p - 2 + h, r,
                        h ? qb : qa, h ? xb : xa);
-              pre2(o, r);  // row r of block 2p - 1 + h
+              pre2(o, rv, r);  // row r of block 2p - 1 + h
             }
           }
         });
         if constexpr (p == 0) {
           static_for<4>([&](auto PT_) {  // block 0's rows, one per part
             constexpr int part = decltype(PT_)::value;
-            if constexpr (rev_part_step(2 * part, NB) == kb) pre2(o, part);
+            if constexpr (rev_part_step(2 * part, NB) == kb) pre2(o, rv, part);
           });
         }
         const f32x4 wa = fr[(2 * s) % 4], wb = fr[(2 * s + 1) % 4];
@@ -617,7 +640,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
     constexpr int h = i / 4, r = i % 4;
     epi2_row(std::integral_constant<int, 1>{}, P0, none, MB - 2 + h, r, h ? qb : qa,
              h ? xb : xa);
-    if constexpr (h == 0) pre2(o0, r);
+    if constexpr (h == 0) pre2(o0, none, r);
   });
   flush(0, DLADMM_P_BETA1, psb1);
   // drain: the ring's last LDS-DMA must land before the workgroup's LDS is released
