@@ -460,26 +460,29 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
 
 // ------------------------------------------------------------------------ weight gradient
 // part[c][i][j] = sum_{b in chunk c} G[i][b] * V[j][b]   (G: n x ld, V: m x ld; both zero-padded
-// to whole 16-row blocks and whole 16-column steps, so no masks).  One workgroup = 4 waves in a
-// 2 x 2 grid over a 128 x 128 output tile; a wave keeps 4 x 4 16x16 accumulators.  Per 16-column
-// step a lane loads, for each of its 4 row blocks of G and of V, the float4 at
-// (row 16a + (l & 15), columns 16s + 4(l >> 4) .. +3) and issues, per block pair, 4 MFMAs whose
-// k-index is the batch column 16s + 4(l >> 4) + q -- the same permutation for both operands, so
-// the contraction is exact.  Operands are software-pipelined one step ahead.
-__global__ __launch_bounds__(256, 1) void wgrad_kernel(const WgradArgs a) {
+// to whole 128-row tiles and whole 16-column steps, so no masks).  One workgroup = 4 waves in a
+// 2 x 2 grid over a 128 x 128 output tile; a wave keeps 4 x 4 16x16 accumulators.
+// Operands stream by LDS-DMA through a 4-stage ring: a stage is one 16-column step of the tile,
+// 16 fragments of 1 KiB (G row blocks 0..7, V row blocks 0..7), each in the MFMA operand layout
+// (lane l: row 16 a + (l & 15), columns 16 s + 4 (l >> 4) .. +3), so every operand read is one
+// conflict-free ds_read_b128; wave w DMAs fragments 4w .. 4w+3, three steps ahead.  Per step and
+// block pair, 4 MFMAs whose k-index is the batch column 16 s + 4 (l >> 4) + q -- the same
+// permutation for both operands, so the contraction is exact.  ~110 registers: two workgroups
+// per CU.  (The previous form loaded the operands into registers one step ahead: 178 us per
+// layer at B = 65,536, latency-bound.)
+constexpr int kWgStages = 4;
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
+  __shared__ f32x4 ring[kWgStages * 16 * 64];
   const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tiles_m = a.MBp16 / 8;  // 128-column tiles (of V rows)
   const int tile = blockIdx.x;
   const int ti = tile / tiles_m, tj = tile % tiles_m;
-  const int i0 = ti * 128 + (w >> 1) * 64;  // G rows of this wave
-  const int j0 = tj * 128 + (w & 1) * 64;   // V rows of this wave
   const int64_t b0 = (int64_t)blockIdx.y * a.chunk;
   int64_t b1 = b0 + a.chunk;
   if (b1 > a.Bpad) b1 = a.Bpad;
   const int steps = b1 > b0 ? (int)((b1 - b0) / 16) : 0;
   const int r = lane & 15, g = lane >> 4;
-  const bool wok = i0 < a.NBp16 * 16 && j0 < a.MBp16 * 16;
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -487,22 +490,36 @@ __global__ __launch_bounds__(256, 1) void wgrad_kernel(const WgradArgs a) {
 #pragma unroll
     for (int y = 0; y < 4; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const float* Gp = a.G + (int64_t)(i0 + r) * a.ld + b0 + 4 * g;
-  const float* Vp = a.V + (int64_t)(j0 + r) * a.ld + b0 + 4 * g;
-  const int64_t rs16 = 16 * a.ld;
-  auto ld4 = [&](const float* p) -> f32x4 { return *reinterpret_cast<const f32x4*>(p); };
-  f32x4 ga[4], va[4], gn[4], vn[4];
-  if (wok && steps > 0) {
+  // this wave's DMA share: waves 0, 1 the G row blocks 4w .. 4w+3, waves 2, 3 the V row blocks
+  // 4(w-2) .. +3 of the tile; lane offset of row 16 f + r, column 4 g (bytes, < 2^31: host)
+  const float* src = w < 2 ? a.G + (int64_t)(ti * 128 + 64 * w) * a.ld
+                           : a.V + (int64_t)(tj * 128 + 64 * (w - 2)) * a.ld;
+  src += b0;
+  const uint32_t vl = (uint32_t)(((int64_t)r * a.ld + 4 * g) * 4);
+  const uint32_t rs16 = (uint32_t)(16 * a.ld * 4);
+  auto issue = [&](int s, int stage) {
+    uint64_t sb = (uint64_t)(src + 16 * (int64_t)s);
+    asm volatile("" : "+s"(sb));
 #pragma unroll
-    for (int x = 0; x < 4; ++x) { ga[x] = ld4(Gp + x * rs16); va[x] = ld4(Vp + x * rs16); }
-  }
-  for (int s = 0; wok && s < steps; ++s) {
-    if (s + 1 < steps) {
+    for (int f = 0; f < 4; ++f)
+      glds16((const float*)sb, vl + f * rs16, ring + (stage * 16 + 4 * w + f) * 64);
+  };
 #pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        gn[x] = ld4(Gp + x * rs16 + 16 * (s + 1));
-        vn[x] = ld4(Vp + x * rs16 + 16 * (s + 1));
-      }
+  for (int s = 0; s < kWgStages - 1; ++s)
+    if (s < steps) issue(s, s);
+  const int gf = 4 * (w >> 1), vf = 8 + 4 * (w & 1);  // this wave's operand fragments
+  for (int s = 0; s < steps; ++s) {
+    // stage s landed for every wave (the DMAs of the steps after it may stay in flight), and
+    // every wave is done reading stage s - 1, which the issue below overwrites
+    if (s + kWgStages - 2 < steps) ring_barrier_n<4 * (kWgStages - 2)>();
+    else ring_barrier_n<0>();
+    if (s + kWgStages - 1 < steps) issue(s + kWgStages - 1, (s + kWgStages - 1) % kWgStages);
+    const f32x4* st = ring + (s % kWgStages) * 16 * 64;
+    f32x4 ga[4], va[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      ga[x] = st[(gf + x) * 64 + lane];
+      va[x] = st[(vf + x) * 64 + lane];
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -510,11 +527,10 @@ __global__ __launch_bounds__(256, 1) void wgrad_kernel(const WgradArgs a) {
       for (int x = 0; x < 4; ++x)
 #pragma unroll
         for (int y = 0; y < 4; ++y) acc[x][y] = mfma4(ga[x][q], va[y][q], acc[x][y]);
-#pragma unroll
-    for (int x = 0; x < 4; ++x) { ga[x] = gn[x]; va[x] = vn[x]; }
   }
-  if (!wok) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA in flight when the LDS is released
   // C/D layout: lane holds column (l & 15) = V row j, rows 4g + r' = G rows
+  const int i0 = ti * 128 + (w >> 1) * 64, j0 = tj * 128 + (w & 1) * 64;
   float* out = a.part + (int64_t)blockIdx.y * a.n * a.m;
 #pragma unroll
   for (int x = 0; x < 4; ++x)
