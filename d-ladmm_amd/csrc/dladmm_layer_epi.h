@@ -15,10 +15,11 @@
 namespace dladmm {
 
 #ifndef DLADMM_EPI_NT
-#define DLADMM_EPI_NT 0  // experiment knob: 1 = non-temporal (nt) epilogue stores
+#define DLADMM_EPI_NT 0  // non-temporal (nt) epilogue stores, by output: 1 Z, 2 E and L, 4 T
 #endif
+template <int WHICH>
 __device__ __forceinline__ void epi_store(float* p, float v) {
-  if constexpr (DLADMM_EPI_NT) __builtin_nontemporal_store(v, p);
+  if constexpr ((DLADMM_EPI_NT & WHICH) != 0) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
 
@@ -88,7 +89,7 @@ struct LayerEpi {
       float u = accv;
       if constexpr (PKIND == PK_SCALAR) u = sp[DLADMM_P_S1] * u;
       const float z = shrink(v.zp - u, v.thz);                        // main_lena.py:79-80
-      if (ok) epi_store(a.Zo + (int64_t)row * a.ldo + col, z);
+      if (ok) epi_store<1>(a.Zo + (int64_t)row * a.ldo + col, z);
       lsum += ok ? fabsf(z) : 0.0f;
       return ok ? z : 0.0f;
     } else {
@@ -116,15 +117,15 @@ struct LayerEpi {
         t = (P + e) - x;                                                   // main_lena.py:88
         l = l0 + v.b3 * t;                                                 // main_lena.py:89
         if (ok) {
-          epi_store(a.Eo + (int64_t)row * a.ldo + col, e);
-          epi_store(a.Lo + (int64_t)row * a.ldo + col, l);
+          epi_store<2>(a.Eo + (int64_t)row * a.ldo + col, e);
+          epi_store<2>(a.Lo + (int64_t)row * a.ldo + col, l);
         }
         const float res = x - P;
         lsum += ok ? (lasso ? res * res : fabsf(res)) : 0.0f;
       }
-      if (ok && a.To) epi_store(a.To + (int64_t)row * a.ldo + col, t);
+      if (ok && a.To) epi_store<4>(a.To + (int64_t)row * a.ldo + col, t);
       const float var = l + v.b1n * t;                      // Var_{k+1} = L + b1 T  main_lena.py:85
-      if (ok && a.Vo) epi_store(a.Vo + (int64_t)row * a.ldv + col, var);
+      if (ok && a.Vo) epi_store<8>(a.Vo + (int64_t)row * a.ldv + col, var);
       return ok ? var : 0.0f;
     }
   }

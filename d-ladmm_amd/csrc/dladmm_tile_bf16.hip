@@ -29,7 +29,11 @@
 #include "dladmm_layer_epi.h"
 
 #ifndef DLADMM_TILE_EXP
-#define DLADMM_TILE_EXP 0  // experiment knob: 1 no in-loop DMA, 2 no MFMA, 3 no epilogue (WRONG)
+#define DLADMM_TILE_EXP 0  // experiment bits (WRONG results): 1 no in-loop DMA, 2 no MFMA,
+                           // 4 no epilogue
+#endif
+#ifndef DLADMM_TILE_LDSPAD
+#define DLADMM_TILE_LDSPAD 0  // experiment: extra dynamic LDS bytes per workgroup (occupancy)
 #endif
 
 namespace dladmm {
@@ -108,20 +112,20 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tile_bf16_kernel(const LayerA
     for (int j = 0; j < kWaveCB; ++j) bfr[j] = st[(kTileBlocks + kWaveCB * wc + j) * 64 + lane];
 #pragma unroll
     for (int i = 0; i < 4; ++i) a0[i] = st[(kWaveRB * wr + i) * 64 + lane];
-    if (DLADMM_TILE_EXP != 1) {
+    if (!(DLADMM_TILE_EXP & 1)) {
 #pragma unroll
       for (int q = 0; q < G::H1; ++q) issue(nkb, nslot, q);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) a1[i] = st[(kWaveRB * wr + 4 + i) * 64 + lane];
-    if (DLADMM_TILE_EXP == 2) continue;
+    if (DLADMM_TILE_EXP & 2) continue;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < kWaveCB; ++j) acc[i][j] = mfma_bf16(a0[i], bfr[j], acc[i][j]);
     __builtin_amdgcn_s_setprio(0);
-    if (DLADMM_TILE_EXP != 1) {
+    if (!(DLADMM_TILE_EXP & 1)) {
 #pragma unroll
       for (int q = G::H1; q < FPW; ++q) issue(nkb, nslot, q);
     }
@@ -136,7 +140,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tile_bf16_kernel(const LayerA
   }
   // drain the speculative stages before the workgroup's LDS can be handed to another
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  if (DLADMM_TILE_EXP == 3) {
+  if (DLADMM_TILE_EXP & 4) {
     float t = 0.f;  // keep every accumulator live
 #pragma unroll
     for (int i = 0; i < kWaveRB; ++i)
@@ -227,16 +231,16 @@ hipError_t launch_tile_ph(int variant, const LayerArgs& a, dim3 grid, hipStream_
   const dim3 blk(NW * 64);
   switch (variant) {
     case DLADMM_V1_LENA:
-      hipLaunchKernelGGL((tile_bf16_kernel<EM_V1, PK_ELEM, PH, NW>), grid, blk, 0, s, a); break;
+      hipLaunchKernelGGL((tile_bf16_kernel<EM_V1, PK_ELEM, PH, NW>), grid, blk, DLADMM_TILE_LDSPAD, s, a); break;
     case DLADMM_V2_LTHETA:
-      hipLaunchKernelGGL((tile_bf16_kernel<EM_V1, PK_ROW, PH, NW>), grid, blk, 0, s, a); break;
+      hipLaunchKernelGGL((tile_bf16_kernel<EM_V1, PK_ROW, PH, NW>), grid, blk, DLADMM_TILE_LDSPAD, s, a); break;
     case DLADMM_V3_FULL:
-      hipLaunchKernelGGL((tile_bf16_kernel<EM_VVAR, PK_ROW, PH, NW>), grid, blk, 0, s, a); break;
+      hipLaunchKernelGGL((tile_bf16_kernel<EM_VVAR, PK_ROW, PH, NW>), grid, blk, DLADMM_TILE_LDSPAD, s, a); break;
     case DLADMM_V4_SCALAR:
     case DLADMM_V5_TIED:
-      hipLaunchKernelGGL((tile_bf16_kernel<EM_VVAR, PK_SCALAR, PH, NW>), grid, blk, 0, s, a); break;
+      hipLaunchKernelGGL((tile_bf16_kernel<EM_VVAR, PK_SCALAR, PH, NW>), grid, blk, DLADMM_TILE_LDSPAD, s, a); break;
     case DLADMM_V6_LASSO:
-      hipLaunchKernelGGL((tile_bf16_kernel<EM_LASSO, PK_SCALAR, PH, NW>), grid, blk, 0, s, a); break;
+      hipLaunchKernelGGL((tile_bf16_kernel<EM_LASSO, PK_SCALAR, PH, NW>), grid, blk, DLADMM_TILE_LDSPAD, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
