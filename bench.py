@@ -155,10 +155,11 @@ def cpu_baseline(m, n, K, B, runs, variant="v4"):
             "host": h}
 
 
-def reduce_timing(elapsed, kern, world, dev):
+def reduce_timing(elapsed, kern, world, dev, use_dist=None):
     """Max over ranks of the wall seconds and of the mean kernel seconds, plus every rank's mean
-    kernel seconds in rank order (one MAX all-reduce + one all-gather; nothing at N = 1)."""
-    if world == 1:
+    kernel seconds in rank order (one MAX all-reduce + one all-gather; nothing at N = 1 unless the
+    process group is up anyway)."""
+    if not (world > 1 if use_dist is None else use_dist):
         return elapsed, kern, [kern]
     tt = torch.tensor([elapsed, kern], device=dev, dtype=torch.float64)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -200,7 +201,10 @@ def main():
     # control path with several ranks on fewer GPUs (rank r on GPU r % count); never for numbers
     backend = os.environ.get("DLADMM_BENCH_BACKEND", "nccl")
     gpu = local if backend == "nccl" else local % max(torch.cuda.device_count(), 1)
-    if world > 1:
+    # DLADMM_BENCH_DIST=1: the process group, barriers and timing collectives at N = 1 too
+    # (rehearses the RCCL control path on a one-GPU box)
+    use_dist = world > 1 or os.environ.get("DLADMM_BENCH_DIST", "") == "1"
+    if use_dist:
         torch.cuda.set_device(gpu)
         dist.init_process_group(backend)
     dev = torch.device("cuda", gpu if world > 1 else 0)
@@ -233,7 +237,7 @@ def main():
                 r, obj = w.step(keep_all)
                 del r
             torch.cuda.synchronize()
-            if world > 1:
+            if use_dist:
                 dist.barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -241,13 +245,13 @@ def main():
                 r, obj = w.step(keep_all, (ev[2 * i], ev[2 * i + 1]))
                 del r
             torch.cuda.synchronize()
-            if world > 1:
+            if use_dist:
                 dist.barrier()
             t1 = time.perf_counter()
         elapsed = t1 - t0
         kern = float(np.mean([ev[2 * i].elapsed_time(ev[2 * i + 1])
                               for i in range(a.steps)])) * 1e-3
-        elapsed, kern, kerns = reduce_timing(elapsed, kern, world, dev)
+        elapsed, kern, kerns = reduce_timing(elapsed, kern, world, dev, use_dist)
         return elapsed, kern, kerns, obj
 
     w = make(a.global_batch if strong else 0)
@@ -417,7 +421,7 @@ def main():
         if world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(m, n, K, a.cpu_batch, a.cpu_runs, a.variant)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 
