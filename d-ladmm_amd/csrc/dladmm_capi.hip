@@ -67,6 +67,37 @@ __global__ __launch_bounds__(256) void pack_frags_kernel(const PackArgs p) {
   reinterpret_cast<f32x4*>(p.dst)[((int64_t)t * p.RB * p.CB + fr) * 64 + lane] = v;
 }
 
+// ------------------------------------------------------------------------ zero fill
+// Stream-ordered zeroing of workspace regions as a kernel launch rather than hipMemsetAsync: a
+// forward captured into a HIP graph (torch.cuda.graph) and replayed measured stale partial sums
+// with hipMemsetAsync nodes (tests/test_gpu_graph.py); kernel nodes replay in stream order.
+__global__ __launch_bounds__(256) void zero_fill_kernel(uint32_t* p, int64_t words,
+                                                        uint8_t* tail, int ntail) {
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (int64_t i = i0; i < words; i += (int64_t)gridDim.x * 256) p[i] = 0u;
+  if (i0 < ntail) tail[i0] = 0;
+}
+inline hipError_t zero_async(void* p, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  const uintptr_t a = (uintptr_t)p;
+  const size_t head = (4 - (a & 3)) & 3;  // workspace regions are 256-B aligned: head = 0
+  if (head) {
+    hipLaunchKernelGGL(zero_fill_kernel, dim3(1), dim3(256), 0, s, (uint32_t*)nullptr,
+                       (int64_t)0, (uint8_t*)p, (int)(head < bytes ? head : bytes));
+    if (hipError_t e = hipGetLastError()) return e;
+    if (head >= bytes) return hipSuccess;
+    p = (uint8_t*)p + head;
+    bytes -= head;
+  }
+  const int64_t words = (int64_t)(bytes / 4);
+  const int ntail = (int)(bytes & 3);
+  int64_t blocks = (words + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks);
+  hipLaunchKernelGGL(zero_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (uint32_t*)p,
+                     words, (uint8_t*)p + 4 * words, ntail);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------ split-f16 packing
 // (DLADMM_PREC_F32_SPLIT, dladmm_fused_x3.hip).  Matrix M (R x C valid, zero padded to RB
 // blocks of 16 rows x KS steps of 32) -> per-tensor scale 2^sw (max|M| * 2^sw in [2^14, 2^15)),
@@ -485,7 +516,7 @@ inline int run_fused_x3(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipSt
   const int MB = p.MP / 16, NB = p.NP / 16, KS1 = p.MP / 32, KS2 = p.NP / 32;
   const bool shared = shared_weight(d);
   const int nw = shared ? 1 : d->layers;
-  if (hipError_t e = hipMemsetAsync(umax, 0, (size_t)(nw + 1) * sizeof(unsigned), s)) return (int)e;
+  if (hipError_t e = zero_async(umax, (size_t)(nw + 1) * sizeof(unsigned), s)) return (int)e;
   // A (rows m, contraction n) and every -W_k (rows n, contraction m)
   const float* asrc[1] = {d->A};
   if (hipError_t e = pack_x3(asrc, 1, d->m, d->n, d->ld_a, MB, KS2, 1.0f, Ap, umax, wexp, 0, s))
@@ -545,7 +576,7 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
                           nullptr, 0, 0, bf))
     return (int)e;
   if (d->loss_kind) {
-    if (hipError_t e = hipMemsetAsync(lossp, 0, (size_t)2 * K * p.nslots * sizeof(float), s))
+    if (hipError_t e = zero_async(lossp, (size_t)2 * K * p.nslots * sizeof(float), s))
       return (int)e;
   }
   const bool lean = !d->keep_all;
@@ -787,14 +818,14 @@ inline int run_reverse(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hip
     return (int)e;
   // slots a variant never writes stay 0; rows past NP / MP (to the weight gradient's 128-row
   // tiles) are never written by the kernel
-  if (hipError_t e = hipMemsetAsync(rpart, 0, p.off_wpart - p.off_rpart, s)) return (int)e;
+  if (hipError_t e = zero_async(rpart, p.off_wpart - p.off_rpart, s)) return (int)e;
   for (int k = 0; k < K && (p.Rn2 > NP || p.Rm2 > MP); ++k) {
     if (p.Rn2 > NP)
-      if (hipError_t e = hipMemsetAsync(GU + k * gus + NP * ldw, 0,
+      if (hipError_t e = zero_async(GU + k * gus + NP * ldw,
                                         (size_t)(p.Rn2 - NP) * ldw * sizeof(float), s))
         return (int)e;
     if (p.Rm2 > MP)
-      if (hipError_t e = hipMemsetAsync(VAR + k * vas + MP * ldw, 0,
+      if (hipError_t e = zero_async(VAR + k * vas + MP * ldw,
                                         (size_t)(p.Rm2 - MP) * ldw * sizeof(float), s))
         return (int)e;
   }
@@ -852,7 +883,7 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
   float* const part = (float*)(ws + p.off_part);
   float* wpart = (float*)(ws + p.off_wpart);
   // adjoints start at zero; the padded rows / columns of gU and Var stay zero (wgrad reads them)
-  if (hipError_t e = hipMemsetAsync(ws + p.off_az, 0, p.off_part - p.off_az, s)) return (int)e;
+  if (hipError_t e = zero_async(ws + p.off_az, p.off_part - p.off_az, s)) return (int)e;
   if (tied) {
     if (hipError_t e = hipMemset2DAsync(d->gW, d->ld_gw * sizeof(float), 0, m * sizeof(float), n, s))
       return (int)e;
@@ -904,7 +935,7 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
   if (fuse) {
     // scalar kinds: every slot of both buffers is rewritten per layer, zeroed once; per-row
     // kinds re-zero a buffer before its layer's first write
-    if (hipError_t e = hipMemsetAsync(rowk ? partk(K - 1) : part, 0,
+    if (hipError_t e = zero_async(rowk ? partk(K - 1) : part,
                                       rowk ? part_bytes : 2 * part_bytes, s))
       return (int)e;
     BwdArgs b1 = a;
@@ -923,7 +954,7 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
     // scalar kinds: every slot's entries are rewritten per layer (counts fixed), so the
     // partials are zeroed once; per-row kinds re-zero (rows past m/n are never written)
     if (!fuse && (rowk || k == K - 1))
-      if (hipError_t e = hipMemsetAsync(part, 0, part_bytes, s)) return (int)e;
+      if (hipError_t e = zero_async(part, part_bytes, s)) return (int)e;
     layer_args(a, k);
     if (!fuse) {
       // BK1: P = A Z_k, recomputed -- or (phase 4) read from the forward's saved P_k, the same
@@ -975,7 +1006,7 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
       if (v == DLADMM_V1_LENA) { b3.b1e3 = f.beta1_elem[k]; b3.gb1e3 = d->g_beta1_elem[k]; }
       b3.part3 = partk(k);
       if (rowk)
-        if (hipError_t e = hipMemsetAsync(partk(k - 1), 0, part_bytes, s)) return (int)e;
+        if (hipError_t e = zero_async(partk(k - 1), part_bytes, s)) return (int)e;
       if (hipError_t e = launch_bwd(6, v, b3, gm, p.SBm, s)) return (int)e;
     } else {
       if (hipError_t e = launch_bwd(3, v, b3, gm, p.SBm, s)) return (int)e;

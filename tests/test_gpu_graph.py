@@ -1,0 +1,92 @@
+"""The forward under HIP graph capture (torch.cuda.graph): a captured forward replayed on new
+input data equals the eager forward on that data bit for bit, on every kernel path -- the fused
+kernel, the per-layer kernel pairs (2K+1 launches: the launch-bound case a graph replays without
+host work), the split-f16 kernel and the bf16 tiles.  Capture needs the C ABI to enqueue only
+stream-ordered work on the caller's stream (no host synchronisation, no allocation of its own:
+outputs and workspace come from torch, which serves them from the graph's pool)."""
+import numpy as np
+import pytest
+import torch
+
+import problems as P
+from test_gpu_parity import make_net
+
+pytestmark = pytest.mark.gpu
+
+
+def capture(net, x_static, **run_kw):
+    """Warm up on a side stream (torch's capture recipe), then capture one forward."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s), torch.no_grad():
+        for _ in range(2):
+            net.run(x_static, **run_kw)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g), torch.no_grad():
+        out = net.run(x_static, **run_kw)
+    return g, out
+
+
+@pytest.mark.parametrize("path", ["fused", "layered", "f32_split", "bf16"])
+def test_graph_replay_equals_eager(path, dl, monkeypatch):
+    m, n, B, K = 256, 512, 640, 6
+    inp = P.make_inputs(m, n, B, 7101)
+    inp2 = P.make_inputs(m, n, B, 7102)
+    sd = P.make_state_dict("v4", m, n, B, K, inp["A"], 7101, perturb=0.1)
+    if path == "layered":
+        monkeypatch.setenv("DLADMM_PATH", "layered")
+    net = make_net(dl, "v4", inp, sd, K).cuda()
+    if path in ("f32_split", "bf16"):
+        net.precision = path
+    kw = dict(keep_all=True, loss_kind=dl._lib.LOSS_L1L1)
+    x = torch.from_numpy(inp["X"]).cuda()
+    g, out = capture(net, x, **kw)
+    for data in (inp2["X"], inp["X"]):
+        x.copy_(torch.from_numpy(data).cuda())
+        g.replay()
+        torch.cuda.synchronize()
+        with torch.no_grad():
+            ref = net.run(torch.from_numpy(data).cuda(), **kw)
+        for nm in ("Z", "E", "L", "T", "loss_sums"):
+            a, b = getattr(out, nm), getattr(ref, nm)
+            assert torch.equal(a, b), f"{path}: {nm} of the replayed graph differs from eager"
+    # the two inputs give different results (the replay did read the new data)
+    x.copy_(torch.from_numpy(inp2["X"]).cuda())
+    g.replay()
+    torch.cuda.synchronize()
+    z2 = out.Z.clone()
+    x.copy_(torch.from_numpy(inp["X"]).cuda())
+    g.replay()
+    torch.cuda.synchronize()
+    assert not torch.equal(z2, out.Z)
+
+
+def test_graph_replay_amortises_launches(dl, monkeypatch):
+    """The per-layer path replayed from a graph takes no longer than eagerly launched (it is the
+    same kernels; the graph only removes the host launch work).  A loose check (10 %): the point
+    is that replay works at a launch-heavy depth (K = 40: 81 launches)."""
+    monkeypatch.setenv("DLADMM_PATH", "layered")
+    m, n, B, K = 64, 256, 64, 40
+    inp = P.make_inputs(m, n, B, 7201)
+    sd = P.make_state_dict("v6", m, n, B, K, inp["A"], 7201, perturb=0.1)
+    net = make_net(dl, "v6", inp, sd, K).cuda()
+    kw = dict(keep_all=True, loss_kind=dl._lib.LOSS_LASSO)
+    x = torch.from_numpy(inp["X"]).cuda()
+    g, out = capture(net, x, **kw)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    torch.cuda.synchronize()
+    ev[0].record()
+    for _ in range(20):
+        g.replay()
+    ev[1].record()
+    with torch.no_grad():
+        for _ in range(20):
+            net.run(x, **kw)
+    ev[2].record()
+    torch.cuda.synchronize()
+    t_graph, t_eager = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
+    with torch.no_grad():
+        ref = net.run(x, **kw)
+    assert torch.equal(out.Z, ref.Z)
+    assert t_graph <= 1.1 * t_eager, (t_graph, t_eager)
