@@ -26,6 +26,7 @@ grad it runs the inference path (no T saved for V1-V3, nothing kept for backward
 """
 from __future__ import annotations
 
+from collections import OrderedDict
 from typing import List, Optional
 
 import numpy as np
@@ -220,7 +221,7 @@ class _DLADMMBase(nn.Module):
         with torch.no_grad():
             r = self._run_shard(x, cols, loss_kind=lk, want_T=self.RETURNS_T)
         per_layer = (alpha * r.loss_sums[:, 0] + r.loss_sums[:, 1]) / denom
-        c = torch.as_tensor(coeffs, dtype=torch.float64, device=per_layer.device)
+        c = _coef_tensor(coeffs, per_layer.device)
         return (c * per_layer).sum().to(torch.float32), per_layer.to(torch.float32)
 
     def _init_state(self, cols=None):
@@ -352,6 +353,23 @@ class _DLADMMFunction(torch.autograd.Function):
         return (None, None, None) + tuple(grads.get(n) for n in names)
 
 
+_COEF: "OrderedDict" = OrderedDict()
+
+
+def _coef_tensor(coeffs, dev) -> torch.Tensor:
+    """The layer coefficients as a device fp64 vector, cached per (device, values): a training
+    step then makes no host-to-device copy once warm, so it can be captured into a HIP graph
+    (tests/test_gpu_graph.py).  A handful of entries (the reference decays them per epoch)."""
+    key = (str(dev), tuple(coeffs))
+    c = _COEF.pop(key, None)
+    if c is None:
+        c = torch.as_tensor(list(coeffs), dtype=torch.float64, device=dev)
+    _COEF[key] = c
+    while len(_COEF) > 16:
+        _COEF.popitem(last=False)
+    return c
+
+
 class _DLADMMLossFunction(torch.autograd.Function):
     """The reference training objective fused into the op (SURVEY.md section 8 rows a11 + f1):
         total = sum_k coeffs[k] * (alpha * sum(|Z_k|, 0).mean() + sum(|X - A Z_k|, 0).mean())
@@ -371,7 +389,7 @@ class _DLADMMLossFunction(torch.autograd.Function):
         r = dladmm_forward(mod.VARIANT, x, mod.A, W, Z0, E0, L0, keep_all=True, want_T=True,
                            loss_kind=lk, want_P=True, **tables)
         per_layer = (alpha * r.loss_sums[:, 0] + r.loss_sums[:, 1]) / denom  # fp64 [K]
-        c = torch.as_tensor(coeffs, dtype=torch.float64, device=dev)
+        c = _coef_tensor(coeffs, dev)
         total = (c * per_layer).sum().to(torch.float32)
         ctx.mod, ctx.tables, ctx.W, ctx.lk, ctx.cols = mod, tables, W, lk, cols
         # (cz_k, cf_k) per unit upstream gradient

@@ -90,3 +90,57 @@ def test_graph_replay_amortises_launches(dl, monkeypatch):
         ref = net.run(x, **kw)
     assert torch.equal(out.Z, ref.Z)
     assert t_graph <= 1.1 * t_eager, (t_graph, t_eager)
+
+
+def test_graph_training_step(dl):
+    """forward + fused training objective + backward captured as one graph (torch's whole-network
+    recipe: warm up on a side stream, capture with static input and .grad buffers), replayed on
+    new data: the gradients and the objective equal an eager step's on the same parameters and
+    data bit for bit.  (The eager references run first: an eager step after capture would
+    rebind .grad and detach it from the buffers the graph writes.)"""
+    from test_gpu_backward import make_train_net
+    m, n, B, K = 256, 512, 640, 6
+    inp = P.make_inputs(m, n, B, 7401)
+    inp2 = P.make_inputs(m, n, B, 7402)
+    sd = P.make_state_dict("v4", m, n, B, K, inp["A"], 7401, perturb=0.1)
+    net = make_train_net(dl, "v4", inp, sd, K)
+    coeffs = [0.6] * (K - 1) + [1.0]
+
+    def step(xx):
+        total, _ = net.training_loss(xx, 1e-3, coeffs, "l1l1")
+        total.backward()
+        return total
+
+    def eager(data):
+        net.zero_grad(set_to_none=True)
+        tot = step(torch.from_numpy(data).cuda()).detach()
+        torch.cuda.synchronize()
+        return tot, {k: None if p.grad is None else p.grad.clone()
+                     for k, p in net.named_parameters()}
+
+    refs = [eager(inp2["X"]), eager(inp["X"])]
+    x = torch.from_numpy(inp["X"]).cuda()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            net.zero_grad(set_to_none=False)
+            step(x)
+    torch.cuda.current_stream().wait_stream(s)
+    net.zero_grad(set_to_none=False)   # the graph accumulates into these .grad buffers
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        static_total = step(x)
+    for data, (ref_total, ref) in zip((inp2["X"], inp["X"]), refs):
+        x.copy_(torch.from_numpy(data).cuda())
+        for p in net.parameters():
+            if p.grad is not None:
+                p.grad.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(static_total.detach(), ref_total)
+        for k, p in net.named_parameters():
+            if ref[k] is None:   # outside the objective's graph (the last layer's E/L step)
+                assert p.grad is None
+                continue
+            assert torch.equal(p.grad, ref[k]), f"grad {k} of the replayed step differs"
