@@ -189,6 +189,7 @@ class Workload:
         r = self.net.run(self.X, keep_all=keep_all, loss_kind=self.lk, kernel_events=evpair)
         # one RCCL all-reduce of the [K, 2] objective sums over xGMI (no-op at N = 1)
         obj = self.ddist.global_objectives(r.loss_sums, self.a.alpha, self.B_global)
+        self.path = r.path  # the kernel path the library chose (dladmm_fwd_path)
         return r, obj
 
 
@@ -257,12 +258,14 @@ def main():
     w = make(a.global_batch if strong else 0)
     B = w.B
     elapsed, kern_avg, kerns, obj = timed(w, a.precision)
+    head_path = w.path
     # the same workload with the fp32 GEMMs on the f16 matrix cores (split-f16, same fp32
     # tolerance tests; tests/test_gpu_split.py), timed the same way beside the headline
     split = None
     if a.precision == "f32" and m <= 256 and n <= 512 and B % 4 == 0 and \
             os.environ.get("DLADMM_PATH", "")[:1] != "l" and not a.no_split:
         s_el, s_kern, _, s_obj = timed(w, "f32_split")
+        assert w.path == 4, f"split leg ran on path {w.path}, not the split-f16 kernel"
         # untimed: per-layer norm-relative distance of the split path's Z/E/L/T from the fp32
         # path's on this whole batch (max over layers and outputs)
         with torch.no_grad():
@@ -298,10 +301,8 @@ def main():
     torch.cuda.synchronize()
 
     if rank == 0:
-        fused = (m <= 256 and n <= 512 and os.environ.get("DLADMM_PATH", "")[:1] != "l"
-                 and a.precision in ("f32", "f32_split"))
-        path = ("fused-split-f16" if a.precision == "f32_split" else "fused") if fused \
-            else "per-layer"
+        path = {1: "fused", 2: "per-layer", 3: "bf16-tiles", 4: "fused-split-f16"}.get(
+            head_path, f"path {head_path}")
         # split-f16: 3 f16 MFMA products per fp32 product -> the fp32-GEMM ceiling of the
         # scheme is the dense f16 MFMA peak / 3
         peak = {"bf16": PEAK_BF16_MFMA, "f32": PEAK_F32_MFMA,

@@ -17,9 +17,14 @@ namespace dladmm {
 #ifndef DLADMM_EPI_NT
 #define DLADMM_EPI_NT 0  // non-temporal (nt) epilogue stores, by output: 1 Z, 2 E and L, 4 T
 #endif
+#ifndef DLADMM_EPI_ABL
+#define DLADMM_EPI_ABL 0  // timing experiments only (WRONG results): 1 no fp32 output stores,
+                          // 2 no operand loads (constants instead)
+#endif
 template <int WHICH>
 __device__ __forceinline__ void epi_store(float* p, float v) {
-  if constexpr ((DLADMM_EPI_NT & WHICH) != 0) __builtin_nontemporal_store(v, p);
+  if constexpr (DLADMM_EPI_ABL & 1) asm volatile("" ::"v"(v));
+  else if constexpr ((DLADMM_EPI_NT & WHICH) != 0) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
 
@@ -53,6 +58,12 @@ struct LayerEpi {
   };
   __device__ __forceinline__ In load(int row, bool cv, int64_t colc) const {
     In v{};
+    if constexpr (DLADMM_EPI_ABL & 2) {
+      v.zp = 0.25f; v.thz = 0.1f; v.x = 0.5f; v.e0 = 0.125f; v.l0 = 0.0625f;
+      v.b2 = 1.f; v.b3 = 1.f; v.b1n = 1.f;
+      asm volatile("" : "+v"(v.zp), "+v"(v.x), "+v"(v.e0), "+v"(v.l0));
+      return v;
+    }
     const int k = a.k;
     if constexpr (PH == 0) {
       const bool ok = cv && row < a.n;

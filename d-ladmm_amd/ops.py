@@ -25,6 +25,8 @@ class ForwardResult:
     loss_sums: Optional[torch.Tensor]  # [K, 2] fp64: (sum|Z_k|, fit_k)
     col_loss: Optional[torch.Tensor] = None  # [K, 2, B] fp32 per-column terms (want_col_loss)
     P: Optional[torch.Tensor] = None  # [K, m, B] A Z_k per layer (want_P: training forwards)
+    path: int = 0  # dladmm_fwd_path: the kernel path that ran (1 fused, 2 per-layer, 3 bf16
+                   # tiles, 4 fused split-f16; 0 = nothing launched)
 
 
 def _f32_dev(t: torch.Tensor, name: str) -> torch.Tensor:
@@ -192,6 +194,7 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
     if wsb == 0:
         path = L.dladmm_fwd_path(ctypes.byref(d))
         _lib.check(path if path < 0 else -7)
+    out.path = L.dladmm_fwd_path(ctypes.byref(d))
     ws = _workspace(dev, wsb)
     d.workspace, d.workspace_bytes = ws.data_ptr(), wsb
     stream = torch.cuda.current_stream(dev).cuda_stream

@@ -170,8 +170,9 @@ int dladmm_abi_version(void);
 size_t dladmm_fwd_workspace_bytes(const dladmm_fwd_desc* d);
 
 /* Which kernel path this descriptor takes: 1 = fused persistent K-layer kernel,
-   2 = per-layer kernel pair (large shapes), 3 = per-layer kernels on bf16 operands,
-   <0 = DLADMM_E_* error. */
+   2 = per-layer kernel pair (large shapes, or one layer's matrix >= 2^31 bytes), 3 = per-layer
+   tile kernels on bf16 operands, 4 = fused kernel on split-f16 operands (DLADMM_PREC_F32_SPLIT),
+   <0 = DLADMM_E_* error.  Host-only: no device work. */
 int dladmm_fwd_path(const dladmm_fwd_desc* d);
 
 /* Enqueue the whole K-layer forward on `stream` (hipStream_t). */

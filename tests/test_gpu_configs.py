@@ -218,3 +218,18 @@ def test_cfg5_bf16_1024x4096_k15_b16384(dl, oracle):
         for nm in "ZELT":
             assert torch.equal(getattr(sh, nm), getattr(r, nm)[:, :, c0:c1]), (c0, nm)
         del sh
+
+
+def test_batch_beyond_32bit_row_offsets(dl, oracle):
+    """A batch so wide that one layer's [n][B] matrix passes 2^31 bytes (B > 2^20 at n = 512):
+    the fused kernels address rows with 32-bit buffer offsets, so this runs on the per-layer
+    kernels, whose addresses are 64-bit -- the path for per-GPU batches of 1-3.5 M columns that
+    288 GB of HBM allows.  Column subset (incl. the last columns) vs the oracle."""
+    m, n, K, B = 256, 512, 2, (1 << 20) + 64
+    d = device_problem(m, n, B, 10801)
+    net, sd = build(dl, "v4", d, K, 10801)
+    with torch.no_grad():
+        r = net.run(d["X"], keep_all=True, loss_kind=dl._lib.LOSS_L1L1)
+    cols = pick_columns(B, 32, 10802)
+    subset_vs_oracle(oracle, "v4", d, sd, K, r, cols, "v4 B=2^20+64", "layered")
+    objective_vs_reduction(d, r, 1.0, "l1l1", "v4 B=2^20+64", "layered")
