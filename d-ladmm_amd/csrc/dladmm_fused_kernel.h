@@ -453,6 +453,23 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
   // Part `part` (0..7: block half h = part / 4, row r = part % 4) of the beta prefetch for the
   // pair being computed: right after the pending pair's row `part` consumed its slot (G2 pairs
   // p > 0), or spread over the first half of pair 0's steps (step (part * NB) / 16).
+  // V1: the layer's beta pointers (b1 of layer k and k + 1, b2 of k), read from the device tables
+  // once per G2 pass by SCALAR loads: a generic-pointer table read compiles to vector loads whose
+  // waits drain every VM operation in flight (the weight DMA and the counted stores) -- 1.5 ms
+  // per forward at the headline shape.
+  const float* bp1 = nullptr;
+  const float* bp2 = nullptr;
+  const float* bpn = nullptr;
+  auto beta_ptrs = [&](int k) {
+    if constexpr (PKIND == PK_ELEM) {
+      typedef const float* const __attribute__((address_space(4)))* ctab_p;
+      const ctab_p t1 = (ctab_p)a.b1t, t2 = (ctab_p)a.b2t;
+      const int kk = k < 0 ? 0 : k, kn = k + 1 < K ? k + 1 : kk;
+      bp1 = t1[kk];
+      bp2 = t2[kk];
+      bpn = t1[kn];
+    }
+  };
   auto prefetch_part = [&](int k, bool pro, auto PART_) {
     constexpr int part = decltype(PART_)::value, h = part / 4, r = part % 4;
 #if DLADMM_ABLATE & 8  // timing experiment: no per-element beta loads (WRONG results)
@@ -463,9 +480,9 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
 #endif
     if constexpr (PKIND == PK_ELEM) {
       const uint32_t eb = (uint32_t)(m * a.ldb * 4);
-      const rsrc_t r1 = mkrsrc(pro ? nullptr : a.b1t[k], pro ? 0u : eb);
-      const rsrc_t r2 = pro ? mkrsrc(a.E0, (uint32_t)(m * a.lde0 * 4)) : mkrsrc(a.b2t[k], eb);
-      const rsrc_t rn = mkrsrc(k + 1 < K ? a.b1t[k + 1] : nullptr, k + 1 < K ? eb : 0u);
+      const rsrc_t r1 = mkrsrc(pro ? nullptr : bp1, pro ? 0u : eb);
+      const rsrc_t r2 = pro ? mkrsrc(a.E0, (uint32_t)(m * a.lde0 * 4)) : mkrsrc(bp2, eb);
+      const rsrc_t rn = mkrsrc(k + 1 < K ? bpn : nullptr, k + 1 < K ? eb : 0u);
       const uint32_t so = bw.at(r);
       pb[h][0][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r1, (int)vb, (int)so, 0));
       pb[h][1][r] = pro ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r2, (int)ve, (int)ew.at(r), 0))
@@ -601,6 +618,7 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     mw.reset();
     bw.reset();
     if constexpr (PRO) ew.reset();
+    beta_ptrs(k);
     static_for<MB / 2>([&](auto P_) {
       constexpr int p = decltype(P_)::value;
       f32x4 ca = zero4, cb = zero4;
