@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--layers", type=int, default=15)
     ap.add_argument("--alpha", type=float, default=0.001)
+    ap.add_argument("--variant", default="v4", choices=["v1", "v2", "v3", "v4", "v5", "v6"],
+                    help="model variant (v6: LASSO objective); the torch-op loss is V4's L1L1")
     ap.add_argument("--fused-loss", action="store_true",
                     help="net.training_loss (objective fused into the kernels) instead of the "
                          "reference's torch-op loss over the returned Z_k")
@@ -48,7 +50,11 @@ def main():
     dev = torch.device("cuda", 0)
     m, n, K, B = a.m, a.n, a.layers, a.batch
     A, X, Z0, E0, L0 = bench.synth(m, n, B, 0, dev)
-    net = dl.DLADMMNetScalar(m=m, n=0, d=n, batch_size=B, A=A, Z0=Z0, E0=E0, L0=L0, layers=K)
+    net = dl.VARIANTS[a.variant](m=m, n=0, d=n, batch_size=B, A=A, Z0=Z0, E0=E0, L0=L0,
+                                 layers=K)
+    kind = "lasso" if a.variant == "v6" else "l1l1"
+    if not a.fused_loss and a.variant != "v4":
+        raise SystemExit("the torch-op loss leg is V4's (main_syn_l1l1_scalar.py)")
     opt = torch.optim.Adam(net.parameters(), lr=0.005)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
 
@@ -58,7 +64,7 @@ def main():
             ev[0].record()
         coeffs = [0.6 if k < K - 1 else 1.0 for k in range(K)]
         if a.fused_loss:
-            tot, _ = net.training_loss(X, a.alpha, coeffs, "l1l1")
+            tot, _ = net.training_loss(X, a.alpha, coeffs, kind)
             if timed:
                 ev[1].record()
                 ev[2].record()
@@ -96,7 +102,8 @@ def main():
     flop_b = 6 * K * m * n * B       # performed
     flop_r = 10 * K * m * n * B      # reference-equivalent (recomputing backward)
     res = {
-        "metric": "training steps/s (V4 forward + L1L1 loss + backward + Adam)",
+        "metric": f"training steps/s ({a.variant.upper()} forward + {kind} loss + backward + Adam)",
+        "variant": a.variant,
         "loss_path": "fused (net.training_loss)" if a.fused_loss else "torch ops on Z_k",
         "batch": B, "m": m, "n": n, "layers": K,
         "step_ms": med(tot_t) * 1e3,
