@@ -94,11 +94,11 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
     slice_gemm<NW, SB, NSB>(ring, a.Wp, a.MBp, ib0, a.KB, a.S, a.ldS, a.Krows, a.B, acc);
   else
     (void)ring;
-  // BK2: with a uniform theta_z >= 0 the shrink S(U, theta_z) is nonzero exactly where
-  // |U| > theta_z, so the forward's own Z_k gives S'(U) (and the objective's sign(Z_k)); then
-  // q = W_k Var_k is needed only for a trainable step s1 (V5) -- host: zk_mask -- and for
-  // theta_z < 0 (both relus open), where the second GEMM still runs
-  // (the PH 2 launch of a zk_mask layer reaches here only with theta_z < 0: it forms q)
+  // BK2: the shrink is monotone, so the forward's own Z_k gives S'(U) and dS/dtheta_z (and the
+  // objective's sign(Z_k)) for either sign of theta_z; then q = W_k Var_k is needed only for a
+  // trainable step s1 (V5).  PH 5 (one GEMM) runs the per-row kinds (V2, V3) and, with a uniform
+  // theta_z >= 0, the scalar ones; a scalar layer with theta_z < 0 still goes through PH 2 (the
+  // PH 2 launch of a zk_mask layer reaches here only then: it forms q)
   constexpr bool zmask = PH == 5;
   f32x4 acc2[PH == 2 ? SB : 1];
   if constexpr (PH == 5) {
@@ -357,8 +357,13 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
         // d/dZ_k of cz_k * sum|Z_k|
         gZt = gZt + czk * (z > 0.f ? 1.f : (z < 0.f ? -1.f : 0.f));
         SD d = shrink_d(U, thz);
-        if (zmask) {  // theta_z >= 0: [U - th > 0] = [Z_k > 0], [-U - th > 0] = [Z_k < 0]
-          const float zp1 = z > 0.f ? 1.f : 0.f, zn1 = z < 0.f ? 1.f : 0.f;
+        if (zmask) {
+          // S is monotone: [U - th > 0] = [Z_k > -c], [-U - th > 0] = [Z_k < c] with c = 0 for
+          // th >= 0 and c = 2|th| for th < 0 (both relus open, Z = 2U, where |Z_k| < 2|th|).
+          // The scalar kinds reach PH 5 only with th >= 0 (c = 0); the per-row kinds take
+          // every row's own sign here.
+          const float c = thz >= 0.f ? 0.f : -2.0f * thz;
+          const float zp1 = z > -c ? 1.f : 0.f, zn1 = z < c ? 1.f : 0.f;
           d = SD{zp1 + zn1, zn1 - zp1};
         }
         const float gU = gZt * d.dx;
@@ -567,12 +572,8 @@ hipError_t launch_bwd_v(const BwdArgs& a, dim3 grid, int sb, hipStream_t s) {
   // PH 5 (one GEMM, light epilogue) runs 32
   constexpr int SB = PH == 5 ? 32 : 16;
   if (sb != SB) return hipErrorInvalidValue;
-  if constexpr (PH == 5 && PK == PK_ROW) {
-    return hipErrorInvalidValue;
-  } else {
-    hipLaunchKernelGGL((bwd_kernel<EM, PK, PH, NW, SB>), grid, dim3(NW * 64), 0, s, a);
-    return hipGetLastError();
-  }
+  hipLaunchKernelGGL((bwd_kernel<EM, PK, PH, NW, SB>), grid, dim3(NW * 64), 0, s, a);
+  return hipGetLastError();
 }
 
 template <int PH>

@@ -674,6 +674,13 @@ struct BwdPlan {
   size_t off_ratp, off_rmtp, off_gu, off_rvar, off_rpart;
 };
 
+// DLADMM_BWD_ZMASK=0: V2 / V3 form q = W_k Var_k in BK2 (PH 2) instead of reading the shrink
+// masks off the saved Z_k (PH 5)
+inline bool zmask_rows_enabled() {
+  const char* e = getenv("DLADMM_BWD_ZMASK");
+  return !(e && e[0] == '0');
+}
+
 // DLADMM_BWD_REV=0: the per-layer backward kernels even where the reverse-sweep kernel applies
 // (A/B timing and the equivalence tests)
 inline bool rev_enabled() {
@@ -975,13 +982,18 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
     // per row (V2, V3); the kernel also checks theta_z >= 0
     b2.Zk = f.Z + k * zl; b2.ldzk = ldo;
     const bool zm = v == DLADMM_V1_LENA || v == DLADMM_V4_SCALAR || v == DLADMM_V6_LASSO;
+    // per-row theta_z (V2, V3): PH 5 takes each row's sign from the table, no PH 2 launch
+    // (DLADMM_BWD_ZMASK=0: the recomputing PH 2 for these too -- A/B and equivalence tests)
+    const bool zrow = (v == DLADMM_V2_LTHETA || v == DLADMM_V3_FULL) && zmask_rows_enabled();
     // mask variants: a PH 5 launch (32-block slices, one GEMM) does the layer when theta_z >= 0,
     // the PH 2 launch when theta_z < 0; the other exits at once (the sign is read on the device)
     b2.zk_mask = zm ? 2 : 0;
-    if (zm) {
+    if (zm || zrow) {
       if (hipError_t e = launch_bwd(5, v, b2, dim3(p.gx, p.slices_n / 2), 32, s)) return (int)e;
     }
-    if (hipError_t e = launch_bwd(2, v, b2, gn, 16, s)) return (int)e;
+    if (!zrow) {
+      if (hipError_t e = launch_bwd(2, v, b2, gn, 16, s)) return (int)e;
+    }
     // weight gradient gW_k = -s1 * gU Var_k^T (split-K over the batch, fixed-order reduction);
     // before BK3: with phase 6 that launch overwrites Var with Var_{k-1}
     WgradArgs wa{};

@@ -108,3 +108,45 @@ def test_upstream_cotangents_use_per_layer_kernels(dl):
     gz = [torch.ones(200, 70, device="cuda") for _ in range(2)]
     res = ops.dladmm_backward(*args, r, gz, **tables)
     assert res.path == 0
+
+
+def _zmask_ab(dl, variant, m, n, B, K, seed, monkeypatch, mixed=False):
+    """The per-row-theta variants' BK2 with masks read off the saved Z_k (PH 5) against the
+    recomputing BK2 (PH 2, DLADMM_BWD_ZMASK=0).  mixed: theta_z of every other ROW negative in
+    every layer (each row takes its own branch of the mask)."""
+    ops = import_module("d-ladmm_amd.ops")
+    d = dict(variant=variant, m=m, n=n, B=B, K=K, seed=seed, perturb=0.1, negtheta=not mixed)
+    inp, sd = P.build_problem(d)
+    if mixed:
+        for k in range(K):
+            key = f"active_para.{k}"
+            v = sd[key].copy()
+            v[1::2] = -0.3 * np.abs(v[1::2])
+            sd[key] = v
+    net = make_train_net(dl, variant, inp, sd, K).cuda()
+    X = torch.from_numpy(inp["X"]).cuda()
+    with torch.no_grad():
+        tables = net._tables(X.device)
+    W = [w.detach() for w in net._weights()]
+    args = (net.VARIANT, X, net.A, W, net.Z0, net.E0, net.L0)
+    lk = dl._lib.LOSS_L1L1
+    with torch.no_grad():
+        r = ops.dladmm_forward(*args, keep_all=True, want_T=True, want_P=True, loss_kind=lk,
+                               **tables)
+    coef = torch.tensor([[1e-2, 1.0]] * K, device="cuda")
+    kw = dict(loss_kind=lk, loss_coef=coef, **tables)
+    a = ops.dladmm_backward(*args, r, **kw)
+    monkeypatch.setenv("DLADMM_BWD_ZMASK", "0")
+    b = ops.dladmm_backward(*args, r, **kw)
+    monkeypatch.delenv("DLADMM_BWD_ZMASK")
+    assert nrel(a.gW.cpu().numpy(), b.gW.cpu().numpy()) <= 1e-6
+    ga, gb = a.g_row.cpu().numpy(), b.g_row.cpu().numpy()
+    for k in range(K):
+        assert nrel(ga[k], gb[k]) <= 1e-6, k
+
+
+@pytest.mark.parametrize("variant", ["v2", "v3"])
+@pytest.mark.parametrize("mixed", [False, True])
+def test_per_row_theta_zmask_matches_recomputing(variant, mixed, dl, monkeypatch):
+    """negtheta (mixed=False): theta < 0 on every other layer; mixed: on every other row."""
+    _zmask_ab(dl, variant, 96, 200, 150, 4, 9870, monkeypatch, mixed)
