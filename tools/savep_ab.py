@@ -12,6 +12,8 @@ net.requires_grad_(False)
 tables = net._tables(dev); W = [w.detach() for w in net._weights()]
 args = (net.VARIANT, X, net.A, W, net.Z0, net.E0, net.L0)
 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+for e in ev:
+    e.record()  # torch creates the hipEvent lazily: make the handles exist
 res = {True: [], False: []}
 for rep in range(12):
     for wp in (False, True):
