@@ -550,18 +550,51 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
 }
 
 // gW[i][j] (+)= scale * sum_c part[c][i][j], c in fixed order; scale = -s1_k (or -1)
+// gW = -s1_k * sum of the chunk partials G = gU_k Var_k^T (accumulate: tied V5 sums layers).
+// Wd (V5): also the block's share of <W, G> in fp64 -> dotp[block]: ss1_k's gradient is
+// sum_b sum_i gU_ib * dU_ib/dss1 = -sum_ij W_ij G_ij, the inner product of the tied weight with
+// the same sums the weight gradient forms (no q = W Var_k product needed)
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* part, int nchunks,
                                                            int64_t nm, const float* scal, int k,
                                                            int accumulate, float* gW,
-                                                           int64_t ldgw, int m) {
+                                                           int64_t ldgw, int m, const float* Wd,
+                                                           int64_t ldwd, double* dotp) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= nm) return;
-  float s = 0.0f;
-  for (int c = 0; c < nchunks; ++c) s += part[(int64_t)c * nm + e];
-  const float scale = -(scal ? scal[k * DLADMM_NSCALAR + DLADMM_P_S1] : 1.0f);
-  const int64_t i = e / m, j = e % m;
-  float* dst = gW + i * ldgw + j;
-  *dst = accumulate ? *dst + scale * s : scale * s;
+  double dv = 0.0;
+  if (e < nm) {
+    float s = 0.0f;
+    for (int c = 0; c < nchunks; ++c) s += part[(int64_t)c * nm + e];
+    const float scale = -(scal ? scal[k * DLADMM_NSCALAR + DLADMM_P_S1] : 1.0f);
+    const int64_t i = e / m, j = e % m;
+    float* dst = gW + i * ldgw + j;
+    *dst = accumulate ? *dst + scale * s : scale * s;
+    if (Wd) dv = (double)Wd[i * ldwd + j] * (double)s;
+  }
+  if (Wd) {  // uniform: fixed-order block sum
+    __shared__ double red[256];
+    red[threadIdx.x] = dv;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) dotp[blockIdx.x] = red[0];
+  }
+}
+
+// g_s1 = -sum_b dotp[b] (fixed order) -> the layer's ss1 slot of the scalar gradients
+__global__ __launch_bounds__(256) void s1_dot_finish_kernel(const double* dotp, int nb,
+                                                            double* out) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int b = threadIdx.x; b < nb; b += 256) s += dotp[b];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = -red[0];
 }
 
 // ------------------------------------------------------------------------ dispatch
@@ -608,10 +641,19 @@ hipError_t launch_wgrad(const WgradArgs& a, int tiles, hipStream_t s) {
 }
 
 hipError_t launch_wgrad_reduce(const float* part, int nchunks, int n, int m, const float* scal,
-                               int k, int accumulate, float* gW, int64_t ldgw, hipStream_t s) {
+                               int k, int accumulate, float* gW, int64_t ldgw, hipStream_t s,
+                               const float* Wd, int64_t ldwd, double* dotp) {
   const int64_t nm = (int64_t)n * m;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((nm + 255) / 256)), dim3(256), 0, s,
-                     part, nchunks, nm, scal, k, accumulate, gW, ldgw, m);
+                     part, nchunks, nm, scal, k, accumulate, gW, ldgw, m, Wd, ldwd, dotp);
+  return hipGetLastError();
+}
+
+int s1_dot_blocks(int n, int m) { return (int)(((int64_t)n * m + 255) / 256); }
+
+hipError_t launch_s1_dot_finish(const double* dotp, int n, int m, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(s1_dot_finish_kernel, dim3(1), dim3(256), 0, s, dotp, s1_dot_blocks(n, m),
+                     out);
   return hipGetLastError();
 }
 

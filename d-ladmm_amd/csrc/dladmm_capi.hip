@@ -98,6 +98,20 @@ inline hipError_t zero_async(void* p, size_t bytes, hipStream_t s) {
   return hipGetLastError();
 }
 
+// rows x cols fp32 at leading dimension ld (the tied weight gradient; no hipMemset2DAsync, for
+// the same capture reason as zero_async)
+__global__ __launch_bounds__(256) void zero_2d_kernel(float* p, int64_t ld, int cols, int rows) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t < (int64_t)rows * cols) p[(t / cols) * ld + t % cols] = 0.0f;
+}
+inline hipError_t zero_2d_async(float* p, int64_t ld, int cols, int rows, hipStream_t s) {
+  const int64_t total = (int64_t)rows * cols;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(zero_2d_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p, ld,
+                     cols, rows);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------ split-f16 packing
 // (DLADMM_PREC_F32_SPLIT, dladmm_fused_x3.hip).  Matrix M (R x C valid, zero padded to RB
 // blocks of 16 rows x KS steps of 32) -> per-tensor scale 2^sw (max|M| * 2^sw in [2^14, 2^15)),
@@ -665,7 +679,7 @@ struct BwdPlan {
   int wtiles, nchunks; int64_t chunk;
   bool saved_p;                   // BK1 reads the forward's A Z_k (fwd_desc.P)
   size_t off_a1, off_at, off_m, off_mt, off_az, off_ae, off_al, off_at_, off_gp, off_var,
-      off_part, off_part2, off_wpart, total;
+      off_part, off_part2, off_wpart, off_s1dot, total;
   // reverse-sweep kernel (dladmm_reverse.hip): packed A^T and M_k^T, gU_k / Var_k of every
   // layer (rows padded to Rn2 / Rm2 for the weight gradient), per-wave parameter partials
   bool rev;
@@ -748,7 +762,7 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   p->rev = false;
   // (E0 / L0 addressed with the outputs' row stride)
   if (p->saved_p && reverse_supports(f.variant) && !d->gZ && !d->gE && !d->gL && !d->gT &&
-      !d->gw_sum && f.ld_e0 == f.ld_out && f.ld_l0 == f.ld_out && rev_enabled()) {
+      f.ld_e0 == f.ld_out && f.ld_l0 == f.ld_out && rev_enabled()) {
     const int MP = kShapeMP[p->fwd.shape], NP = kShapeNP[p->fwd.shape];
     p->Rn2 = round_up(NP, 128);
     p->Rm2 = round_up(MP, 128);
@@ -782,6 +796,7 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
     p->off_rvar = o; o += align256(colb * (p->Rm2 + kShapeMP[p->fwd.shape]) * K);
     p->off_rpart = o; o += align256(sizeof(float) * DLADMM_NSCALAR * K * p->rncg);
     p->off_wpart = o; o += align256(sizeof(float) * (size_t)p->nchunks * n * m);
+    p->off_s1dot = o; o += align256(sizeof(double) * (size_t)s1_dot_blocks(n, m) * K);
     p->total = o;
     return 0;
   }
@@ -798,6 +813,7 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   p->off_part = o; o += align256(sizeof(float) * part_floats);
   p->off_part2 = o; o += align256(sizeof(float) * part_floats);  // phase 6: layers of odd k
   p->off_wpart = o; o += align256(sizeof(float) * (size_t)p->nchunks * n * m);
+  p->off_s1dot = o; o += align256(sizeof(double) * (size_t)s1_dot_blocks(n, m));
   p->total = o;
   return 0;
 }
@@ -851,21 +867,37 @@ inline int run_reverse(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hip
   r.aer = p.Rm2;
   r.part = rpart;
   if (hipError_t e = launch_reverse_shape(shape, f.variant, r, p.rtiles, s)) return (int)e;
-  // weight gradients gW_k = -s1 gU_k Var_k^T (split-K over the batch, fixed-order reduction)
-  for (int k = 0; k < K; ++k) {
+  // weight gradients gW_k = -s1 gU_k Var_k^T (split-K over the batch, fixed-order reduction),
+  // layers K-1 .. 0 as the per-layer sweep visits them (a tied weight sums them in that order);
+  // V5: each layer's <W, gU_k Var_k^T> for ss1_k's gradient
+  const bool tied = d->gw_sum != 0, v5 = f.variant == DLADMM_V5_TIED;
+  double* s1dot = (double*)(ws + p.off_s1dot);
+  const int nbd = s1_dot_blocks(n, m);
+  if (tied)
+    if (hipError_t e = zero_2d_async(d->gW, d->ld_gw, m, n, s)) return (int)e;
+  for (int k = K - 1; k >= 0; --k) {
     WgradArgs wa{};
     wa.G = GU + k * gus; wa.V = VAR + k * vas; wa.ld = ldw; wa.n = n; wa.m = m;
     wa.NBp16 = (int)(p.Rn2 / 16); wa.MBp16 = (int)(p.Rm2 / 16);
     wa.Bpad = p.Bpad; wa.chunk = p.chunk; wa.nchunks = p.nchunks; wa.part = wpart;
     if (hipError_t e = launch_wgrad(wa, p.wtiles, s)) return (int)e;
-    if (hipError_t e = launch_wgrad_reduce(wpart, p.nchunks, n, m, f.scalar_params, k, 0,
-                                           d->gW + (int64_t)k * n * d->ld_gw, d->ld_gw, s))
+    if (hipError_t e = launch_wgrad_reduce(wpart, p.nchunks, n, m, f.scalar_params, k,
+                                           tied ? 1 : 0,
+                                           tied ? d->gW : d->gW + (int64_t)k * n * d->ld_gw,
+                                           d->ld_gw, s, v5 ? f.W[k] : nullptr, f.ld_w,
+                                           v5 ? s1dot + (int64_t)k * nbd : nullptr))
       return (int)e;
   }
   // parameter slots of every layer: fixed-order fp64 sums of the per-wave partials
   hipLaunchKernelGGL(loss_reduce_kernel, dim3((unsigned)(DLADMM_NSCALAR * K)), dim3(1024), 0, s,
                      (const float*)rpart, p.rncg, d->g_scalar);
-  return (int)hipGetLastError();
+  if (hipError_t e = hipGetLastError()) return (int)e;
+  for (int k = 0; k < K && v5; ++k)
+    if (hipError_t e = launch_s1_dot_finish(s1dot + (int64_t)k * nbd, n, m,
+                                            d->g_scalar + (int64_t)k * DLADMM_NSCALAR +
+                                                DLADMM_P_S1, s))
+      return (int)e;
+  return 0;
 }
 
 inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStream_t s) {
@@ -892,9 +924,10 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
   // adjoints start at zero; the padded rows / columns of gU and Var stay zero (wgrad reads them)
   if (hipError_t e = zero_async(ws + p.off_az, p.off_part - p.off_az, s)) return (int)e;
   if (tied) {
-    if (hipError_t e = hipMemset2DAsync(d->gW, d->ld_gw * sizeof(float), 0, m * sizeof(float), n, s))
-      return (int)e;
+    if (hipError_t e = zero_2d_async(d->gW, d->ld_gw, m, n, s)) return (int)e;
   }
+  const bool v5 = v == DLADMM_V5_TIED;
+  double* s1dot = (double*)(ws + p.off_s1dot);
   const float* asrc[1] = {f.A};
   // BK1 operand: A (rows m, contraction n); BK2 operand: A^T (rows n, contraction m)
   if (hipError_t e = pack(asrc, 1, m, n, f.ld_a, p.MBpm, p.NB, 1, A1, s)) return (int)e;
@@ -981,7 +1014,9 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
     // S'(U_k) from the saved Z_k unless a parameter scales W_k Var_k (V5's ss1) or theta_z is
     // per row (V2, V3); the kernel also checks theta_z >= 0
     b2.Zk = f.Z + k * zl; b2.ldzk = ldo;
-    const bool zm = v == DLADMM_V1_LENA || v == DLADMM_V4_SCALAR || v == DLADMM_V6_LASSO;
+    // (V5: ss1's gradient comes from the weight gradient's sums, so q is not needed either)
+    const bool zm = v == DLADMM_V1_LENA || v == DLADMM_V4_SCALAR || v == DLADMM_V5_TIED ||
+                    v == DLADMM_V6_LASSO;
     // per-row theta_z (V2, V3): PH 5 takes each row's sign from the table, no PH 2 launch
     // (DLADMM_BWD_ZMASK=0: the recomputing PH 2 for these too -- A/B and equivalence tests)
     const bool zrow = (v == DLADMM_V2_LTHETA || v == DLADMM_V3_FULL) && zmask_rows_enabled();
@@ -1004,7 +1039,8 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
     float* gWk = tied ? d->gW : d->gW + (int64_t)k * n * d->ld_gw;
     if (hipError_t e = launch_wgrad_reduce(wpart, p.nchunks, n, m,
                                            has_s1 ? f.scalar_params : nullptr, k, tied ? 1 : 0,
-                                           gWk, d->ld_gw, s))
+                                           gWk, d->ld_gw, s, v5 ? f.W[k] : nullptr, f.ld_w,
+                                           v5 ? s1dot : nullptr))
       return (int)e;
     // BK3: gVar = M_k^T gU -- with phase 6 fused with BK1 of layer k-1
     BwdArgs b3 = a;
@@ -1031,6 +1067,10 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
                          p.gx * kBwdWaves * p.slices_n,
                          d->g_scalar + (int64_t)k * DLADMM_NSCALAR);
       if (hipError_t e = hipGetLastError()) return (int)e;
+      if (v5)  // ss1_k: the weight gradient's <W, gU_k Var_k^T> replaces BK2's partials
+        if (hipError_t e = launch_s1_dot_finish(s1dot, n, m, d->g_scalar +
+                                                (int64_t)k * DLADMM_NSCALAR + DLADMM_P_S1, s))
+          return (int)e;
     } else if (rowk) {
       hipLaunchKernelGGL(loss_reduce_kernel, dim3((unsigned)(DLADMM_NSCALAR * f.row_stride)),
                          dim3(1024), 0, s, (const float*)pk, p.ncg,

@@ -195,6 +195,12 @@ static_assert(sizeof(RevArgs) <= 2048, "kernel argument size");
 bool reverse_supports(int variant);
 hipError_t launch_reverse_shape(int shape, int variant, const RevArgs& a, int grid, hipStream_t s);
 hipError_t launch_wgrad_reduce(const float* part, int nchunks, int n, int m, const float* scal,
-                               int k, int accumulate, float* gW, int64_t ldgw, hipStream_t s);
+                               int k, int accumulate, float* gW, int64_t ldgw, hipStream_t s,
+                               const float* Wd = nullptr, int64_t ldwd = 0,
+                               double* dotp = nullptr);
+// V5: ss1_k's gradient from the weight gradient's sums (-<W, gU_k Var_k^T>): dotp holds
+// s1_dot_blocks(n, m) fp64 block partials of one layer
+int s1_dot_blocks(int n, int m);
+hipError_t launch_s1_dot_finish(const double* dotp, int n, int m, double* out, hipStream_t s);
 
 }  // namespace dladmm

@@ -656,14 +656,19 @@ hipError_t launch_rev(const RevArgs& a, int grid, hipStream_t s) {
 template <int MP, int NP>
 hipError_t launch_rev_v(int variant, const RevArgs& a, int grid, hipStream_t s) {
   switch (variant) {
-    case DLADMM_V4_SCALAR: return launch_rev<MP, NP, EM_VVAR>(a, grid, s);
+    case DLADMM_V4_SCALAR:
+    case DLADMM_V5_TIED: return launch_rev<MP, NP, EM_VVAR>(a, grid, s);
     case DLADMM_V6_LASSO: return launch_rev<MP, NP, EM_LASSO>(a, grid, s);
   }
   return hipErrorInvalidValue;
 }
 
+// V5 (tied, a trainable step ss1_k on W Var): M_k^T packs -ss1_k W^T, the masks come from Z_k as
+// for V4, and ss1_k's gradient -<W, gU_k Var_k^T> is taken from the weight gradient's sums
+// (wgrad_reduce_kernel), so the sweep needs no q = W Var_k
 bool reverse_supports(int variant) {
-  return variant == DLADMM_V4_SCALAR || variant == DLADMM_V6_LASSO;
+  return variant == DLADMM_V4_SCALAR || variant == DLADMM_V5_TIED ||
+         variant == DLADMM_V6_LASSO;
 }
 
 hipError_t launch_reverse_shape(int shape, int variant, const RevArgs& a, int grid,

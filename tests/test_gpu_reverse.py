@@ -150,3 +150,23 @@ def _zmask_ab(dl, variant, m, n, B, K, seed, monkeypatch, mixed=False):
 def test_per_row_theta_zmask_matches_recomputing(variant, mixed, dl, monkeypatch):
     """negtheta (mixed=False): theta < 0 on every other layer; mixed: on every other row."""
     _zmask_ab(dl, variant, 96, 200, 150, 4, 9870, monkeypatch, mixed)
+
+
+@pytest.mark.parametrize("tied", [False, True])
+def test_reverse_v5_tied_step(tied, dl, monkeypatch):
+    """V5 (one shared weight, a trainable step ss1_k on W Var_k) on the reverse sweep: ss1_k's
+    gradient -<W, gU_k Var_k^T> from the weight gradient's sums in both paths; the per-layer
+    path's BK2 reads the masks off Z_k too.  gW summed over the layers (tied) or per layer."""
+    ops, args, r, tables = saved_forward(dl, "v5", 64, 200, 333, 4, 9990, lk=dl._lib.LOSS_L1L1)
+    coef = torch.tensor([[1e-2, 1.0]] * 4, device="cuda")
+    kw = dict(loss_kind=dl._lib.LOSS_L1L1, loss_coef=coef, tied=tied, **tables)
+    rev = ops.dladmm_backward(*args, r, **kw)
+    monkeypatch.setenv("DLADMM_BWD_REV", "0")
+    per = ops.dladmm_backward(*args, r, **kw)
+    monkeypatch.delenv("DLADMM_BWD_REV")
+    assert rev.path == 1 and per.path == 0
+    assert torch.equal(rev.gW, per.gW)
+    gs_r, gs_p = rev.g_scalar.cpu().numpy(), per.g_scalar.cpu().numpy()
+    for k in range(4):
+        assert nrel(gs_r[k], gs_p[k]) <= 2e-6, (k, gs_r[k], gs_p[k])
+    assert np.all(gs_r[:, 7] != 0.0)  # the ss1 slot (P_S1) is filled
