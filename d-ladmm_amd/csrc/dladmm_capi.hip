@@ -194,6 +194,10 @@ __global__ __launch_bounds__(1024) void param_reduce_kernel(const float* part, i
                                                             int cnt_m, int cnt_n, double* sums) {
   __shared__ double red[1024];
   const int sl = blockIdx.x;
+  if (sl == DLADMM_P_S1) {  // V5 writes ss1's gradient afterwards; for the others s1 is 1: 0
+    if (threadIdx.x == 0) sums[sl] = 0.0;
+    return;
+  }
   const int cnt = (sl == DLADMM_P_THETA_Z || sl == DLADMM_P_S1) ? cnt_n : cnt_m;
   double s = 0.0;
   for (int w = threadIdx.x; w < cnt; w += 1024) s += (double)part[(int64_t)sl * stride + w];

@@ -220,10 +220,8 @@ typedef struct dladmm_bwd_desc {
   float* gW; int64_t ld_gw;   /* [K][n][ld_gw], or [1][n][ld_gw] when gw_sum */
   double* g_scalar;           /* V4-V6: [K][DLADMM_NSCALAR] per-slot grads (slots the variant
                                  does not use are 0; V1: unused).  Slot DLADMM_P_S1 (the step
-                                 scaling W_k Var_k) is defined for the tied variant (V5) only:
-                                 for the others s1 is the constant 1 and the slot is unspecified
-                                 (0 on layers with theta_z >= 0, where q = W_k Var_k is not
-                                 formed) */
+                                 scaling W_k Var_k) holds ss1_k's gradient for the tied variant
+                                 (V5); for the others s1 is the constant 1 and the slot is 0 */
   double* g_row;              /* V2/V3: [K][DLADMM_NSCALAR][fwd.row_stride] per-row grads */
   float* const* g_beta1_elem; /* V1: host arrays of K device pointers, (m x fwd.ld_beta) each: */
   float* const* g_beta2_elem; /*     grads of the per-sample beta1[k] / beta2[k]              */

@@ -62,10 +62,12 @@ def check_equal(rev, per, K):
     gs_p = per.g_scalar.cpu().numpy()
     from importlib import import_module
     lib = import_module("d-ladmm_amd._lib")
-    used = [s for s in range(lib.NSCALAR) if s != lib.P_S1]  # S1: defined for V5 only
     for k in range(K):
-        e = nrel(gs_r[k, used], gs_p[k, used])
-        assert e <= 2e-6, (k, e, gs_r[k, used], gs_p[k, used])
+        e = nrel(gs_r[k], gs_p[k])
+        assert e <= 2e-6, (k, e, gs_r[k], gs_p[k])
+        # the ss1 slot is V5's; s1 is the constant 1 elsewhere and its slot 0 on both paths
+        # (also on theta_z < 0 layers, where the per-layer BK2 forms q)
+        assert gs_r[k, lib.P_S1] == 0.0 and gs_p[k, lib.P_S1] == 0.0
 
 
 @pytest.mark.parametrize("variant,kind", [("v4", "l1l1"), ("v4", "lasso"), ("v6", "lasso")])
