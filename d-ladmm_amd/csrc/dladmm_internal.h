@@ -132,11 +132,12 @@ struct BwdArgs {
   const float* Tk; int64_t ldt;    // T_k
   const float* Pk;                 // BK1 with the forward's saved A Z_k (row stride ldt)
   const float* Zk; int64_t ldzk;   // BK2: the forward's Z_k (its shrink mask, zk_mask)
-  int zk_mask;                     // BK2: 2 = no parameter scales W_k Var_k (s1): the layer
-                                   // runs a PH 5 launch (theta_z >= 0: the mask comes from Z_k,
-                                   // q = W_k Var_k is not formed) beside a PH 2 launch (theta_z
-                                   // < 0), each exiting unless theta_z's sign is its case; 0 =
-                                   // PH 2 only
+  int zk_mask;                     // BK2, scalar kinds: 2 = the layer runs a PH 5 launch
+                                   // (theta_z >= 0: the mask comes from Z_k, q = W_k Var_k is
+                                   // not formed; V5's ss1 gradient comes from the weight
+                                   // gradient) beside a PH 2 launch (theta_z < 0), each exiting
+                                   // unless theta_z's sign is its case; 0 = PH 2 only.  Per-row
+                                   // kinds run PH 5 alone (each row's sign in the epilogue)
   const float* gZ; const float* gE; const float* gL; const float* gT; int64_t ldg;  // upstream
   int loss_kind; const float* lcoef;  // fused training objective: device [K][2] (cz_k, cf_k)
   float* AZ; float* AE; float* AL; float* AT; float* GP; float* VAR; int64_t ldw;   // workspace
