@@ -9,7 +9,7 @@ the [K, 2] objective sums.  Batch is sharded across ranks: the headline is weak 
 fixed); `--global-batch G` makes it strong scaling instead (BASELINE config 3: G = 262,144 columns
 split by dist.shard_columns over the ranks).  The default run also times config 3's strong-scaling
 workload beside the headline (`cfg3_strong`), so every driver run at N = 1/2/4/8 records both
-curves.  The model is built after torch.manual_seed(1126), so the objective is
+curves, and at N = 1 config 2 (B = 10,000, `cfg2`).  The model is built after torch.manual_seed(1126), so the objective is
 reproducible.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B | --global-batch G]
@@ -51,8 +51,8 @@ def parse():
                     help="strong scaling: this many columns in total, split over the ranks by "
                          "dist.shard_columns (BASELINE config 3: 262144)")
     ap.add_argument("--no-cfg3", action="store_true",
-                    help="skip the secondary config-3 strong-scaling measurement (262,144 "
-                         "global columns)")
+                    help="skip the secondary measurements of config 3 (strong scaling, 262,144 "
+                         "global columns) and config 2 (B = 10,000, N = 1)")
     ap.add_argument("--m", type=int, default=256)
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--layers", type=int, default=15)
@@ -298,6 +298,16 @@ def main():
         cfg3 = dict(value=262144 * a.steps / c_el, ms_per_step=c_el / a.steps * 1e3,
                     kern=c_kern, kerns=c_kerns, B=w3.B, obj=float(c_obj.cpu().numpy()[-1]))
         del w3
+    # BASELINE config 2 (V4, B = 10,000 on one GPU) beside the headline at N = 1: 625 sixteen-
+    # column units on 1,024 SIMDs
+    cfg2 = None
+    if world == 1 and not strong and not a.no_cfg3 and a.variant == "v4" and \
+            a.precision == "f32" and (m, n, K) == (256, 512, 15) and B != 10000:
+        w2 = Workload(dl, a, m, n, K, 10000, 10000, None, rank, dev, rank)
+        c_el, c_kern, _, c_obj = timed(w2, "f32")
+        cfg2 = dict(value=10000 * a.steps / c_el, ms_per_step=c_el / a.steps * 1e3, kern=c_kern,
+                    obj=float(c_obj.cpu().numpy()[-1]))
+        del w2
     torch.cuda.synchronize()
 
     if rank == 0:
@@ -398,6 +408,18 @@ def main():
                 "max_rel_dev_vs_f32": s_dev,
                 "max_rel_dev_note": "max over layers of ||X_split - X_f32|| / ||X_f32|| for X in "
                                     "Z, E, L, T on this batch (parity tolerance: 1e-5)",
+            }
+        if cfg2 is not None:
+            f2 = (4 * K + 2) * m * n * 10000
+            res["cfg2"] = {
+                "workload": "BASELINE config 2: V4 forward m=256 n=512 K=15, B=10000 on one GPU, "
+                            "all layers written + fused L1L1 objective",
+                "value": cfg2["value"], "unit": "samples/s", "ms_per_step": cfg2["ms_per_step"],
+                "kernel_ms": cfg2["kern"] * 1e3,
+                "roofline_frac": f2 / cfg2["kern"] / PEAK_F32_MFMA,
+                "note": "625 sixteen-column units on 1,024 SIMDs: at most 61 % of the chip busy "
+                        "(DESIGN.md section 12)",
+                "objective_last_layer": cfg2["obj"],
             }
         if cfg3 is not None:
             f3 = (4 * K + 2) * m * n * cfg3["B"]
