@@ -9,7 +9,8 @@ the [K, 2] objective sums.  Batch is sharded across ranks: the headline is weak 
 fixed); `--global-batch G` makes it strong scaling instead (BASELINE config 3: G = 262,144 columns
 split by dist.shard_columns over the ranks).  The default run also times config 3's strong-scaling
 workload beside the headline (`cfg3_strong`), so every driver run at N = 1/2/4/8 records both
-curves, and at N = 1 config 2 (B = 10,000, `cfg2`).  The model is built after torch.manual_seed(1126), so the objective is
+curves, and at N = 1 configs 2 (B = 10,000), 4 (V6 LASSO 512 x 2048, K = 40) and 5 (bf16,
+1024 x 4096): `cfg2`, `cfg4`, `cfg5`.  The model is built after torch.manual_seed(1126), so the objective is
 reproducible.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B | --global-batch G]
@@ -308,6 +309,23 @@ def main():
         cfg2 = dict(value=10000 * a.steps / c_el, ms_per_step=c_el / a.steps * 1e3, kern=c_kern,
                     obj=float(c_obj.cpu().numpy()[-1]))
         del w2
+    # BASELINE configs 4 (V6 LASSO m=512 n=2048 K=40, per-layer kernels) and 5 (bf16 operands,
+    # m=1024 n=4096 K=15, 16,384 columns = its 131,072 over 8 GPUs) at N = 1
+    cfg45 = {}
+    if world == 1 and not strong and not a.no_cfg3 and a.variant == "v4" and \
+            a.precision == "f32" and (m, n, K) == (256, 512, 15):
+        import copy
+        for name, var, prec, (m_, n_, K_, B_) in (("cfg4", "v6", "f32", (512, 2048, 40, 65536)),
+                                                  ("cfg5", "v4", "bf16", (1024, 4096, 15, 16384))):
+            a_ = copy.copy(a)
+            a_.variant = var
+            w_ = Workload(dl, a_, m_, n_, K_, B_, B_, None, rank, dev, rank)
+            c_el, c_kern, _, c_obj = timed(w_, prec)
+            cfg45[name] = dict(value=B_ * a.steps / c_el, ms_per_step=c_el / a.steps * 1e3,
+                               kern=c_kern, obj=float(c_obj.cpu().numpy()[-1]), path=w_.path,
+                               shape=(m_, n_, K_, B_), var=var, prec=prec)
+            del w_
+            torch.cuda.empty_cache()
     torch.cuda.synchronize()
 
     if rank == 0:
@@ -420,6 +438,23 @@ def main():
                 "note": "625 sixteen-column units on 1,024 SIMDs: at most 61 % of the chip busy "
                         "(DESIGN.md section 12)",
                 "objective_last_layer": cfg2["obj"],
+            }
+        for name, c in cfg45.items():
+            m_, n_, K_, B_ = c["shape"]
+            fl = (4 * K_ + 2) * m_ * n_ * B_
+            pk = PEAK_BF16_MFMA if c["prec"] == "bf16" else PEAK_F32_MFMA
+            res[name] = {
+                "workload": (f"BASELINE config {name[-1]}: {c['var'].upper()} forward m={m_} "
+                             f"n={n_} K={K_}, B={B_} on one GPU, "
+                             f"{'bf16 MFMA operands / fp32 state' if c['prec'] == 'bf16' else 'fp32'}"
+                             ", all layers written + fused objective"),
+                "value": c["value"], "unit": "samples/s", "ms_per_step": c["ms_per_step"],
+                "path": {1: "fused", 2: "per-layer", 3: "bf16-tiles", 4: "fused-split-f16"}.get(
+                    c["path"], c["path"]),
+                "kernels_ms": c["kern"] * 1e3,
+                "roofline_frac": fl / c["kern"] / pk,
+                "roofline_peak": "bf16 dense MFMA" if c["prec"] == "bf16" else "fp32 MFMA",
+                "objective_last_layer": c["obj"],
             }
         if cfg3 is not None:
             f3 = (4 * K + 2) * m * n * cfg3["B"]
