@@ -765,7 +765,10 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   // cotangents (the fused objective is the training loss), 32-bit workspace offsets
   p->rev = false;
   // (E0 / L0 addressed with the outputs' row stride)
-  if (p->saved_p && reverse_supports(f.variant) && !d->gZ && !d->gE && !d->gL && !d->gT &&
+  // Z cotangents (a torch-op loss over the returned Z_k) ride along when they share the
+  // outputs' row stride and their pointer table fits the kernel arguments
+  const bool gz_ok = !d->gZ || (d->ld_g == f.ld_out && f.layers <= kRevMaxGZ);
+  if (p->saved_p && reverse_supports(f.variant) && gz_ok && !d->gE && !d->gL && !d->gT &&
       f.ld_e0 == f.ld_out && f.ld_l0 == f.ld_out && rev_enabled()) {
     const int MP = kShapeMP[p->fwd.shape], NP = kShapeNP[p->fwd.shape];
     p->Rn2 = round_up(NP, 128);
@@ -870,6 +873,8 @@ inline int run_reverse(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hip
   r.GU = GU; r.VAR = VAR; r.ldw = ldw; r.gus = gus; r.vas = vas;
   r.aer = p.Rm2;
   r.part = rpart;
+  r.has_gz = d->gZ ? 1 : 0;
+  for (int k = 0; k < K && d->gZ; ++k) r.gz[k] = d->gZ[k];
   if (hipError_t e = launch_reverse_shape(shape, f.variant, r, p.rtiles, s)) return (int)e;
   // weight gradients gW_k = -s1 gU_k Var_k^T (split-K over the batch, fixed-order reduction),
   // layers K-1 .. 0 as the per-layer sweep visits them (a tied weight sums them in that order);

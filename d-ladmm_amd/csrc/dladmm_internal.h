@@ -174,6 +174,7 @@ hipError_t launch_wgrad(const WgradArgs& a, int tiles, hipStream_t s);
 
 // ---- backward as one reverse sweep (dladmm_reverse.hip): V4 / V6 after a saved-product fused
 // forward, register-resident shapes (kShapeMP / kShapeNP), no upstream output cotangents
+constexpr int kRevMaxGZ = 128;  // layers whose Z cotangents fit the kernel-argument table
 struct RevArgs {
   int m, n, B, K;
   int loss_kind, ncg;              // ncg: waves (column groups) = partial entries per slot
@@ -191,6 +192,8 @@ struct RevArgs {
   int64_t aer;                     // V4: rows aer.. of layer k's Var block hold the adjoint of
                                    // E_{k-1} (carried from BK1(k) to BK1(k-1))
   float* part;                     // parameter partials [K][8][ncg]
+  int has_gz;                      // per-layer cotangents of Z (row stride ldo), NULL = 0
+  const float* gz[kRevMaxGZ];
 };
 static_assert(sizeof(RevArgs) <= 2048, "kernel argument size");
 bool reverse_supports(int variant);

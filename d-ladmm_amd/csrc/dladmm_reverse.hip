@@ -130,7 +130,10 @@ struct RevWin {
   }
 };
 
-template <int MP, int NP, int EMODE>
+// GZ: per-layer output cotangents of Z (a loss built from the returned Z_k with torch ops, as
+// the reference's training loops do): one more load per G1' element, added where the per-layer
+// BK2 adds it ((adjoint + gZ_k) + A^T gP)
+template <int MP, int NP, int EMODE, bool GZ>
 __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   using F = Rev<MP, NP>;
   constexpr int MB = F::MB, NB = F::NB, CF = F::CF, NCH = F::NCH;
@@ -169,6 +172,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   // L_{k-1} (AL), and gP (the G1' B operand).  AZ and GP are MFMA operands: AGPRs
   float AZ[NB][4], GP[MB][4], AL[MB][4];
   float pz[2][4];      // Z_k rows of the G1' pair being computed
+  float pg[2][4];      // GZ: the cotangent of Z_k at those rows
   float pv[4][5];      // P_{k-1}, E_{k-2}, L_{k-2}, T_{k-1}, AE: row r of the next G2' block
   float psz = 0.f, psb1 = 0.f, ps[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // parameter partials
 
@@ -274,7 +278,18 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   auto res2_last = [&]() -> R2 {
     return R2{mkrsrc(a.T, mbytes), none, none, none};
   };
-  auto rz = [&](int k) { return urs(a.Z + k * zl, (uint32_t)(zl * 4)); };
+  struct R1 { rsrc_t z, gz; };  // Z_k and (GZ) its cotangent, same row stride (host: ld_g = ldo)
+  auto rz = [&](int k) -> R1 {
+    R1 o;
+    o.z = urs(a.Z + k * zl, (uint32_t)(zl * 4));
+    if constexpr (GZ) {
+      const float* gp = a.gz[k];  // kernel-argument table: scalar load
+      o.gz = urs(gp, gp ? (uint32_t)(zl * 4) : 0u);
+    } else {
+      o.gz = o.z;
+    }
+    return o;
+  };
   auto rgu = [&](int k) { return urs(a.GU + k * a.gus, (uint32_t)(NP * a.ldw * 4)); };
   // Var_j (rows 0..) and the adjoint of E_{j-1} (rows aeo / 4 / ldw ..) of layer j, plus the
   // next layer's block, which holds the adjoint of E_j that BK1(j) reads
@@ -291,9 +306,10 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   auto ld = [](rsrc_t r, uint32_t voff, uint32_t soff) -> float {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
   };
-  auto pre1 = [&](rsrc_t r, int h, int rr) {
+  auto pre1 = [&](const R1& r, int h, int rr) {
     if constexpr (REV_ABL & 8) { pz[h][rr] = 0.5f; return; }
-    pz[h][rr] = ld(r, vo, wZ.at(rr));
+    pz[h][rr] = ld(r.z, vo, wZ.at(rr));
+    if constexpr (GZ) pg[h][rr] = ld(r.gz, vo, wZ.at(rr));
     if (rr == 3) wZ.next();
   };
   // G2' operands, one block ahead: slot rr <- row rr of the next block (rv: this pass's Var
@@ -341,7 +357,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   auto epi1_row = [&](const LP1& P1, rsrc_t rg, int b, int h, int r, const f32x4& q) {
     if constexpr (REV_ABL & 4) { AZ[b][r] = q[r]; pin_agpr(AZ[b][r]); return; }
     const float zk = pz[h][r];
-    float gZt = AZ[b][r] + q[r];
+    float gZt = (GZ ? AZ[b][r] + pg[h][r] : AZ[b][r]) + q[r];
     // + d/dZ_k of cz_k sum|Z_k|: cz_k sgn(Z_k) is exact, so the fma is phase 5's mul + add
     const float sg = (zk > 0.f ? 1.f : 0.f) - (zk < 0.f ? 1.f : 0.f);
     gZt = __builtin_fmaf(P1.cz, sg, gZt);
@@ -505,7 +521,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   // G1'(k): A^T gP_k over blocks (2p, 2p+1), contraction jb = 0..MB-1.  Pair 0 runs the rows of
   // G2'(k+1)'s last pair (Pp, rvp; none in the first pass), then flushes layer k+1's beta1 and
   // layer k's BK1 partials.
-  auto g1_pass = [&](auto FIRST_, int k, const LP1& P1, rsrc_t rzk, rsrc_t rg, const LP2& Pp,
+  auto g1_pass = [&](auto FIRST_, int k, const LP1& P1, const R1& rzk, rsrc_t rg, const LP2& Pp,
                      const R2& op, rsrc_t rvp) {
     constexpr bool FIRST = decltype(FIRST_)::value;
     const int gi = 2 * (K - 1 - k);
@@ -649,7 +665,10 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
 
 template <int MP, int NP, int EM>
 hipError_t launch_rev(const RevArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((reverse_kernel<MP, NP, EM>), dim3(grid), dim3(256), 0, s, a);
+  if (a.has_gz)
+    hipLaunchKernelGGL((reverse_kernel<MP, NP, EM, true>), dim3(grid), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((reverse_kernel<MP, NP, EM, false>), dim3(grid), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -104,11 +104,24 @@ def test_reverse_deterministic(dl):
     assert torch.equal(a.gW, b.gW) and torch.equal(a.g_scalar, b.g_scalar)
 
 
-def test_upstream_cotangents_use_per_layer_kernels(dl):
-    """Output cotangents (a torch loss on the outputs) keep the per-layer kernels."""
-    ops, args, r, tables = saved_forward(dl, "v4", 64, 200, 70, 2, 9960)
-    gz = [torch.ones(200, 70, device="cuda") for _ in range(2)]
-    res = ops.dladmm_backward(*args, r, gz, **tables)
+def test_z_cotangents_on_the_reverse_sweep(dl, monkeypatch):
+    """A torch-op loss over the returned Z_k (the reference's own training loop) hands the
+    backward per-layer Z cotangents only: the reverse sweep adds them where the per-layer BK2
+    does ((adjoint + gZ_k) + A^T gP), so both paths agree bit for bit on the weight gradients;
+    an unread layer's cotangent may be None.  E / L / T cotangents keep the per-layer kernels."""
+    ops, args, r, tables = saved_forward(dl, "v4", 64, 200, 333, 3, 9960, lk=dl._lib.LOSS_L1L1)
+    g = torch.Generator(device="cuda").manual_seed(9961)
+    gz = [torch.randn(200, 333, device="cuda", generator=g), None,
+          torch.randn(200, 333, device="cuda", generator=g)]
+    coef = torch.tensor([[1e-3, 1.0]] * 3, device="cuda")
+    kw = dict(loss_kind=dl._lib.LOSS_L1L1, loss_coef=coef, **tables)
+    rev = ops.dladmm_backward(*args, r, gz, **kw)
+    monkeypatch.setenv("DLADMM_BWD_REV", "0")
+    per = ops.dladmm_backward(*args, r, gz, **kw)
+    monkeypatch.delenv("DLADMM_BWD_REV")
+    check_equal(rev, per, 3)
+    ge = [torch.ones(64, 333, device="cuda") for _ in range(3)]
+    res = ops.dladmm_backward(*args, r, gz, ge, **tables)
     assert res.path == 0
 
 
