@@ -71,6 +71,19 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
       if (pos != (PH == 5)) return;  // uniform: the whole grid exits
     }
   }
+  if constexpr (BK2 && PKIND == PK_ROW) {
+    // per-row theta_z (V2, V3): the PH 5 launch covers layers whose every row has theta_z >= 0,
+    // the PH 2 launch the others.  With theta < 0 both relus are open on |U| < |theta| and the
+    // forward's literal shrink rounds U within an ulp of -|theta| to Z = -2|theta|, the value
+    // U = -|theta| gives too: the saved Z_k cannot tell the two masks apart, U can
+    if (a.zk_mask == 2) {
+      const float* th = a.rowp + ((int64_t)a.k * 8 + DLADMM_P_THETA_Z) * a.rstride;
+      int neg = 0;
+      for (int r = threadIdx.x; r < a.n; r += NW * 64) neg |= th[r] < 0.0f ? 1 : 0;
+      neg = __syncthreads_or(neg);
+      if ((neg == 0) != (PH == 5)) return;  // uniform over the workgroup (and the grid)
+    }
+  }
   // BK1 keeps 4 workgroups per CU (its latency-bound epilogue needs them): a 2-deep B ring
   constexpr int NSB = (PH == 1 || FUS) ? 2 : 3;
   __shared__ f32x4 ring[PSV ? 1 : slice_lds_f4<NW, NSB>()];
@@ -360,8 +373,8 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
         if (zmask) {
           // S is monotone: [U - th > 0] = [Z_k > -c], [-U - th > 0] = [Z_k < c] with c = 0 for
           // th >= 0 and c = 2|th| for th < 0 (both relus open, Z = 2U, where |Z_k| < 2|th|).
-          // The scalar kinds reach PH 5 only with th >= 0 (c = 0); the per-row kinds take
-          // every row's own sign here.
+          // Both kinds reach PH 5 only with th >= 0 on every row (c = 0: exact); the c > 0
+          // branch serves the DLADMM_BWD_ZMASK experiments.
           const float c = thz >= 0.f ? 0.f : -2.0f * thz;
           const float zp1 = z > -c ? 1.f : 0.f, zn1 = z < c ? 1.f : 0.f;
           d = SD{zp1 + zn1, zn1 - zp1};

@@ -112,6 +112,30 @@ inline hipError_t zero_2d_async(float* p, int64_t ld, int cols, int rows, hipStr
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------ device pointer tables
+// dst[0 .. n) = src[0 .. n) for host arrays of device pointers, kPtrChunk entries per launch,
+// the values travelling as kernel arguments (graph-capturable; no host buffer outlives the call)
+constexpr int kPtrChunk = 64;
+struct PtrChunk {
+  const void* p[kPtrChunk];
+  const void** dst;
+  int n;
+};
+__global__ __launch_bounds__(64) void ptr_table_kernel(const PtrChunk c) {
+  if ((int)threadIdx.x < c.n) c.dst[threadIdx.x] = c.p[threadIdx.x];
+}
+inline hipError_t write_ptr_table(const void* const* src, int n, const void** dst, hipStream_t s) {
+  for (int b = 0; b < n; b += kPtrChunk) {
+    PtrChunk c{};
+    c.n = n - b < kPtrChunk ? n - b : kPtrChunk;
+    for (int i = 0; i < c.n; ++i) c.p[i] = src[b + i];
+    c.dst = dst + b;
+    hipLaunchKernelGGL(ptr_table_kernel, dim3(1), dim3(64), 0, s, c);
+    if (hipError_t e = hipGetLastError()) return e;
+  }
+  return hipSuccess;
+}
+
 // ------------------------------------------------------------------------ split-f16 packing
 // (DLADMM_PREC_F32_SPLIT, dladmm_fused_x3.hip).  Matrix M (R x C valid, zero padded to RB
 // blocks of 16 rows x KS steps of 32) -> per-tensor scale 2^sw (max|M| * 2^sw in [2^14, 2^15)),
@@ -475,18 +499,18 @@ inline int run_fused(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStrea
   a.rowp = d->row_params; a.rstride = d->row_stride;
   a.ldb = d->ld_beta;
   if (d->variant == DLADMM_V1_LENA) {
-    // the K per-layer beta pointers of each table go to the workspace (no depth limit); the
-    // host array is staged by the runtime before hipMemcpyAsync returns
-    const float** tab = (const float**)(ws + p.off_btab);
-    const size_t K = (size_t)d->layers;
-    if (hipError_t e = hipMemcpyAsync(tab, d->beta1_elem, K * sizeof(void*),
-                                      hipMemcpyHostToDevice, s))
+    // the K per-layer beta pointers of each table go to the workspace (no depth limit), written
+    // by a kernel whose arguments carry them: a graph capture records the pointer values with
+    // the launch, where a memcpy from the caller's (short-lived) host array would replay from
+    // freed memory
+    const void** tab = (const void**)(ws + p.off_btab);
+    if (hipError_t e = write_ptr_table((const void* const*)d->beta1_elem, d->layers, tab, s))
       return (int)e;
-    if (hipError_t e = hipMemcpyAsync(tab + K, d->beta2_elem, K * sizeof(void*),
-                                      hipMemcpyHostToDevice, s))
+    if (hipError_t e = write_ptr_table((const void* const*)d->beta2_elem, d->layers,
+                                       tab + d->layers, s))
       return (int)e;
-    a.b1t = tab;
-    a.b2t = tab + K;
+    a.b1t = (const float* const*)tab;
+    a.b2t = (const float* const*)(tab + d->layers);
   }
   a.Zo = d->Z; a.Eo = d->E; a.Lo = d->L; a.To = d->T; a.ldo = d->ld_out;
   a.lossp = lossp;
@@ -736,6 +760,23 @@ inline int validate_bwd(const dladmm_bwd_desc* d) {
 }
 
 inline int64_t round_up(int64_t x, int64_t q) { return (x + q - 1) / q * q; }
+inline int64_t K_of(const dladmm_fwd_desc& f) { return f.layers; }
+
+// Largest workspace the reverse sweep may ask for: DLADMM_REV_WS_MAX_MB, else a quarter of the
+// device's memory (72 GB on an MI355X)
+inline size_t rev_ws_cap() {
+  static const size_t cap = [] {
+    const char* e = getenv("DLADMM_REV_WS_MAX_MB");
+    if (e && *e) return (size_t)strtoull(e, nullptr, 10) << 20;
+    int dev = 0;
+    size_t total = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceTotalMem(&total, dev) == hipSuccess &&
+        total)
+      return total / 4;
+    return (size_t)64 << 30;
+  }();
+  return cap;
+}
 
 inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   *p = BwdPlan{};
@@ -761,8 +802,9 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   p->nslots = p->ncg * (p->slices_m > p->slices_n ? p->slices_m : p->slices_n);
   const int64_t rs = f.row_stride > 0 ? f.row_stride : 1;
   const int64_t part_floats = 8 * (p->nslots > rs * p->ncg ? (int64_t)p->nslots : rs * p->ncg);
-  // one reverse-sweep kernel: V4 / V6 after a saved-product fused forward, no upstream output
-  // cotangents (the fused objective is the training loss), 32-bit workspace offsets
+  // one reverse-sweep kernel: V4 / V5 / V6 after a saved-product fused forward, no gE / gL / gT
+  // cotangents (gZ allowed, below), 32-bit workspace offsets, workspace under rev_ws_cap()
+  // (the conditions include/dladmm.h documents at dladmm_bwd_path)
   p->rev = false;
   // (E0 / L0 addressed with the outputs' row stride)
   // Z cotangents (a torch-op loss over the returned Z_k) ride along when they share the
@@ -774,7 +816,13 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
     p->Rn2 = round_up(NP, 128);
     p->Rm2 = round_up(MP, 128);
     const int64_t lim = (int64_t)1 << 31;
-    if ((int64_t)NP * p->Bpad * 4 < lim && 2 * (p->Rm2 + MP) * p->Bpad * 4 < lim) {
+    // the sweep keeps gU_k and Var_k of every layer: (Rn2 + Rm2 + MP) x Bpad floats per layer
+    // (≈256 MiB per layer at 256 x 512, B = 65,536) where the per-layer phases need O(1) in K;
+    // above rev_ws_cap() the per-layer phases run instead of a workspace that may not fit
+    const size_t rev_bytes = (size_t)(K_of(f) + 1) * MP * NP * 4 +
+                             (size_t)K_of(f) * (p->Rn2 + p->Rm2 + MP) * p->Bpad * 4;
+    if ((int64_t)NP * p->Bpad * 4 < lim && 2 * (p->Rm2 + MP) * p->Bpad * 4 < lim &&
+        rev_bytes <= rev_ws_cap()) {
       p->rev = true;
       p->Rn = p->Rn2;  // the weight gradient reads the reverse kernel's row padding
       p->Rm = p->Rm2;
@@ -1026,18 +1074,18 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
     // (V5: ss1's gradient comes from the weight gradient's sums, so q is not needed either)
     const bool zm = v == DLADMM_V1_LENA || v == DLADMM_V4_SCALAR || v == DLADMM_V5_TIED ||
                     v == DLADMM_V6_LASSO;
-    // per-row theta_z (V2, V3): PH 5 takes each row's sign from the table, no PH 2 launch
-    // (DLADMM_BWD_ZMASK=0: the recomputing PH 2 for these too -- A/B and equivalence tests)
+    // per-row theta_z (V2, V3): PH 5 when no row of the layer has theta_z < 0 (checked on the
+    // device), PH 2 otherwise (DLADMM_BWD_ZMASK=0: the recomputing PH 2 for these too -- A/B
+    // and equivalence tests)
     const bool zrow = (v == DLADMM_V2_LTHETA || v == DLADMM_V3_FULL) && zmask_rows_enabled();
     // mask variants: a PH 5 launch (32-block slices, one GEMM) does the layer when theta_z >= 0,
     // the PH 2 launch when theta_z < 0; the other exits at once (the sign is read on the device)
-    b2.zk_mask = zm ? 2 : 0;
+    // (per-row kinds: the PH 5 launch when every row's theta_z >= 0, else the PH 2 launch)
+    b2.zk_mask = (zm || zrow) ? 2 : 0;
     if (zm || zrow) {
       if (hipError_t e = launch_bwd(5, v, b2, dim3(p.gx, p.slices_n / 2), 32, s)) return (int)e;
     }
-    if (!zrow) {
-      if (hipError_t e = launch_bwd(2, v, b2, gn, 16, s)) return (int)e;
-    }
+    if (hipError_t e = launch_bwd(2, v, b2, gn, 16, s)) return (int)e;
     // weight gradient gW_k = -s1 * gU Var_k^T (split-K over the batch, fixed-order reduction);
     // before BK3: with phase 6 that launch overwrites Var with Var_{k-1}
     WgradArgs wa{};

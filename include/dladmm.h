@@ -232,9 +232,18 @@ typedef struct dladmm_bwd_desc {
 /* Workspace the backward needs for this descriptor (0 on an invalid descriptor). */
 size_t dladmm_bwd_workspace_bytes(const dladmm_bwd_desc* d);
 
-/* Which kernels the backward runs: 1 = one reverse-sweep kernel for every layer's adjoints
-   (V4 / V6 after a fused-path forward that saved P, no upstream output cotangents: the fused
-   training objective), 0 = per-layer kernels, <0 = DLADMM_E_* error. */
+/* Which kernels the backward runs: 1 = one reverse-sweep kernel for every layer's adjoints,
+   0 = per-layer kernels, <0 = DLADMM_E_* error.  The reverse sweep runs when ALL of these hold:
+     - variant V4, V5 or V6 (and the newS models built on them);
+     - the forward ran on the fused fp32 path and saved P (fwd.P != NULL, keep_all);
+     - no gE / gL / gT cotangents; gZ is allowed when ld_g == fwd.ld_out and layers <= 128;
+     - fwd.ld_e0 == fwd.ld_l0 == fwd.ld_out;
+     - its 32-bit workspace offsets hold and its workspace, about
+       (layers + 1) * MP * NP * 4 + layers * (Rn + 2 * MP) * Bpad * 4 bytes (MP, NP: the
+       instantiation's padded m, n; Rn = NP rounded up to 128; Bpad = batch rounded up to 16),
+       stays under a quarter of the device memory (DLADMM_REV_WS_MAX_MB overrides);
+     - DLADMM_BWD_REV is not "0".
+   dladmm_bwd_workspace_bytes() reports the size of whichever path this returns. */
 int dladmm_bwd_path(const dladmm_bwd_desc* d);
 
 /* Enqueue the whole reverse sweep on `stream` (hipStream_t).  Deterministic: every reduction

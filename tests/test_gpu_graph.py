@@ -62,6 +62,40 @@ def test_graph_replay_equals_eager(path, dl, monkeypatch):
     assert not torch.equal(z2, out.Z)
 
 
+@pytest.mark.parametrize("K", [5, 70])
+def test_graph_replay_v1_beta_tables(K, dl):
+    """V1 (main_lena.py:57-98): the fused kernel reads its per-layer per-sample beta pointers from
+    a device table the library writes per call.  The table is written by a kernel
+    whose arguments carry the pointers, so a captured forward replays with them after the host
+    arrays of the call are gone; K = 70 writes it in two chunks.  The replays equal eager
+    forwards bit for bit, including after the parameters are updated in place."""
+    m, n, B = 64, 256, 192
+    inp = P.make_inputs(m, n, B, 7301)
+    inp2 = P.make_inputs(m, n, B, 7302)
+    sd = P.make_state_dict("v1", m, n, B, K, inp["A"], 7301, perturb=0.1, wscale=0.4)
+    net = make_net(dl, "v1", inp, sd, K).cuda()
+    kw = dict(keep_all=True, loss_kind=dl._lib.LOSS_L1L1)
+    x = torch.from_numpy(inp["X"]).cuda()
+    g, out = capture(net, x, **kw)
+    import gc
+    gc.collect()
+    for step, data in enumerate((inp2["X"], inp["X"])):
+        if step == 1:
+            with torch.no_grad():   # in place: the graph reads the same parameter storage
+                for p in net.beta1:
+                    p.mul_(0.9)
+        x.copy_(torch.from_numpy(data).cuda())
+        g.replay()
+        torch.cuda.synchronize()
+        with torch.no_grad():
+            ref = net.run(torch.from_numpy(data).cuda(), **kw)
+        for nm in ("Z", "E", "L", "T", "loss_sums"):
+            a, b = getattr(out, nm), getattr(ref, nm)
+            if b is None:
+                continue
+            assert torch.equal(a, b), f"V1 K={K}: {nm} of the replayed graph differs from eager"
+
+
 def test_graph_replay_launch_heavy_path(dl, monkeypatch):
     """The per-layer path at a launch-heavy depth (V6, K = 40: 81 launches) replays from a graph
     with the eager results (timing is not asserted: on a shared box it is noise-bound)."""

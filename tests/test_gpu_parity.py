@@ -130,21 +130,16 @@ def _oracle_case(oracle, variant, m, n, B, K, seed, perturb=0.1, wscale=None, sd
 def _compare(out, ref, tag="", path="f32"):
     """Per layer, against the fp64 oracle: nrel(gpu, oracle64) <= max(1e-5, 2 x nrel(oracle32,
     oracle64)) -- the GPU's fp32 result may be as far from the exact one as the reference's own
-    fp32 evaluation is (it sums its GEMMs in another order).  T (= A Z + E - X, a small residual)
-    is measured against the scale of X."""
+    fp32 evaluation is (it sums its GEMMs in another order).  Every output is measured by its own
+    norm, T (= A Z + E - X, a small residual) included: where that residual's rounding puts 1e-5
+    out of reach, the gap clause applies."""
     names = ["Z", "E", "L", "T"][: len(out)]
     for nm, seq in zip(names, out):
         for k, t in enumerate(seq):
             r = np.asarray(ref["r64"][nm][k], np.float64)
             r32 = np.asarray(ref[nm][k], np.float64)
             got = t.cpu().numpy().astype(np.float64)
-            if nm == "T":
-                sx = max(np.linalg.norm(ref["Xs"]), 1e-30)
-                e32 = float(np.linalg.norm(got - r32) / sx)
-                e64 = float(np.linalg.norm(got - r) / sx)
-                gap = float(np.linalg.norm(r32 - r) / sx)
-            else:
-                e32, e64, gap = nrel(got, r32), nrel(got, r), ref["gap"][nm][k]
+            e32, e64, gap = nrel(got, r32), nrel(got, r), ref["gap"][nm][k]
             parity.check_f32(tag, path, f"{nm}[{k}] vs oracle", e32, e64, gap)
 
 
