@@ -17,6 +17,12 @@ restatement, which sums its GEMMs in another order) it is the larger of the two:
 conditioned layers a single fp32 run's distance from fp64 is a noisy sample (v1_lena_cfg1 L[3]:
 torch 8.0e-6, numpy 2.0e-5).  `check_f32` states the bar once so every test applies it.
 
+`fp32_refs` forms ref32 and the gap for the oracle cases: ref32 = the torch-op restatement
+(oracle/dladmm_torch_cpu.py, the reference's ATen ops, bit-equal to the reference classes on the
+fixtures), the gap = the larger of its and the numpy restatement's distance from fp64 (round 4:
+a single-column T, a residual, has one fp32 rounding sample per layer; v5 B=1 T[9]: numpy
+2.2e-5, the GPU 4.5e-5).
+
 `record` logs every checked error; with DLADMM_PARITY_JSON=<path> set, conftest.py writes the log
 at the end of the session (tools/parity_report.py summarises it per case and path into
 profiles/r03_parity.json).
@@ -40,6 +46,31 @@ def nrel(a, b) -> float:
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def fp32_refs(oracle, variant, X, A, Z0, E0, L0, sd, K):
+    """(ref32, ref64, gap, o32): ref32 the reference's own fp32 op sequence on the CPU (torch
+    restatement; the numpy restatement for the variants it does not cover), ref64 the fp64
+    oracle, gap[name][k] = max over the CPU fp32 evaluations of their distance from ref64, o32
+    the numpy restatement's fp32 output."""
+    args = (variant, X, A, Z0, E0, L0, sd, K)
+    o32 = oracle.forward(*args)
+    r64 = oracle.forward(*args, dtype=np.float64)
+    names = [nm for nm in ("Z", "E", "L", "T") if nm in o32]
+    ref32 = {nm: list(o32[nm]) for nm in names}
+    runs = [ref32]
+    if variant in ("v1", "v2", "v3", "v4", "v5", "v6"):
+        import torch
+        from oracle import dladmm_torch_cpu as tcpu
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32))  # noqa: E731
+        out = tcpu.forward(variant, t(X), t(A), t(Z0), t(E0), t(L0),
+                           {k: t(v) for k, v in sd.items()}, K)
+        tr = {nm: [x.numpy() for x in seq] for nm, seq in zip("ZELT", out)}
+        ref32 = {nm: tr[nm] for nm in names}
+        runs.append(ref32)
+    gap = {nm: [max(nrel(r[nm][k], r64[nm][k]) for r in runs) for k in range(len(r64[nm]))]
+           for nm in names}
+    return ref32, r64, gap, o32
 
 
 def record(case: str, path: str, what: str, err: float, bound: float, gap: float = 0.0,

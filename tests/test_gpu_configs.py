@@ -68,9 +68,8 @@ def subset_vs_oracle(oracle, variant, d, sd, K, r, cols, case, path):
     (parity.check_f32), each output -- T too -- by its own norm."""
     sub = {k: v[:, cols].cpu().numpy() for k, v in d.items() if k != "A"}
     A = d["A"].cpu().numpy()
-    args = (variant, sub["X"], A, sub["Z0"], sub["E0"], sub["L0"], sd, K)
-    r32 = oracle.forward(*args)
-    r64 = oracle.forward(*args, dtype=np.float64)
+    r32, r64, gaps, _ = parity.fp32_refs(oracle, variant, sub["X"], A, sub["Z0"], sub["E0"],
+                                         sub["L0"], sd, K)
     cidx = torch.from_numpy(cols).cuda()
     for nm in ("Z", "E", "L", "T"):
         got_all = getattr(r, nm)
@@ -81,7 +80,7 @@ def subset_vs_oracle(oracle, variant, d, sd, K, r, cols, case, path):
             # every output by its own norm, T (a small residual) included: where its own
             # rounding puts 1e-5 out of reach, the gap clause of check_f32 applies
             e32, e64 = parity.nrel(got, r32[nm][k]), parity.nrel(got, r64[nm][k])
-            gap = parity.nrel(r32[nm][k], r64[nm][k])
+            gap = gaps[nm][k]
             parity.check_f32(case, path, f"{nm}[{k}] columns vs oracle", e32, e64, gap)
 
 

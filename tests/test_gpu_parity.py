@@ -117,12 +117,11 @@ def _oracle_case(oracle, variant, m, n, B, K, seed, perturb=0.1, wscale=None, sd
     if sd is None:
         sd = P.make_state_dict(variant, m, n, B, K, inp["A"], seed, perturb=perturb,
                                wscale=wscale)
-    args = (variant, inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd, K)
-    ref = oracle.forward(*args)
-    ref64 = oracle.forward(*args, dtype=np.float64)
+    r32, ref64, gap, ref = parity.fp32_refs(oracle, variant, inp["X"], inp["A"], inp["Z0"],
+                                            inp["E0"], inp["L0"], sd, K)
+    ref.update(r32)   # ref32 = the reference's own op sequence (torch restatement)
     ref["Xs"] = inp["X"]
-    ref["gap"] = {nm: [nrel(a, b) for a, b in zip(ref[nm], ref64[nm])]
-                  for nm in ("Z", "E", "L", "T") if nm in ref}
+    ref["gap"] = gap
     ref["r64"] = ref64
     return inp, sd, ref
 
