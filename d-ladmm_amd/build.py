@@ -16,22 +16,43 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-UNITS = ("dladmm_capi.hip", "dladmm_fused.hip", "dladmm_fused_savep.hip", "dladmm_fused_x3.hip", "dladmm_layered.hip",
-         "dladmm_backward.hip", "dladmm_lskm.hip", "dladmm_eval.hip", "dladmm_tile_bf16.hip",
-         "dladmm_reverse.hip")
-HEADERS = (os.path.join(ROOT, "include", "dladmm.h"), os.path.join(CSRC, "dladmm_common.h"),
-           os.path.join(CSRC, "dladmm_fused_kernel.h"),
-           os.path.join(CSRC, "dladmm_internal.h"), os.path.join(CSRC, "dladmm_slice.h"),
-           os.path.join(CSRC, "dladmm_layer_epi.h"))
+UNITS = ("dladmm_capi.hip", "dladmm_fused.hip", "dladmm_fused_savep.hip", "dladmm_fused_x3.hip",
+         "dladmm_layered.hip", "dladmm_backward.hip", "dladmm_lskm.hip", "dladmm_eval.hip",
+         "dladmm_tile_bf16.hip", "dladmm_reverse.hip",
+         # reverse-sweep instantiations: one unit per E-step form and shape group (minutes each)
+         "dladmm_reverse_vvar.hip", "dladmm_reverse_v1.hip", "dladmm_reverse_lasso.hip",
+         "dladmm_reverse_vvar_small.hip", "dladmm_reverse_v1_small.hip",
+         "dladmm_reverse_lasso_small.hip")
+INCLUDE = os.path.join(ROOT, "include")
 OUT = os.path.join(HERE, "lib", "libdladmm_hip.so")
 OBJ = os.path.join(HERE, "lib", "obj")
 ARCH = os.environ.get("DLADMM_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", f"--offload-arch={ARCH}",
          "-I", os.path.join(ROOT, "include")]
-# per-unit extras: the split-f16 kernel keeps scalar f32 VALU beside its MFMAs (packed v_pk_*
-# f32 ops issue slower there; MI355X_MICROARCH.md, price of one filler beside MFMAs)
-UNIT_FLAGS = {"dladmm_fused_x3.hip": ["-fno-slp-vectorize"],
-              "dladmm_reverse.hip": ["-fno-slp-vectorize"]}
+# per-unit extras: the split-f16 kernel and the reverse sweep keep scalar f32 VALU beside their
+# MFMAs (packed v_pk_* f32 ops issue slower there; MI355X_MICROARCH.md, price of one filler
+# beside MFMAs)
+UNIT_FLAGS = {u: ["-fno-slp-vectorize"] for u in UNITS
+              if u == "dladmm_fused_x3.hip" or u.startswith("dladmm_reverse")}
+
+
+def deps(path, seen=None):
+    """The file and every local header it includes (recursively): a unit is rebuilt only when
+    one of ITS sources changed."""
+    seen = set() if seen is None else seen
+    if path in seen or not os.path.exists(path):
+        return seen
+    seen.add(path)
+    for line in open(path):
+        line = line.strip()
+        if line.startswith("#include \""):
+            name = line.split('"')[1]
+            for d in (os.path.dirname(path), CSRC, INCLUDE):
+                cand = os.path.join(d, name)
+                if os.path.exists(cand):
+                    deps(cand, seen)
+                    break
+    return seen
 
 
 def hipcc() -> str:
@@ -53,8 +74,10 @@ def _stale(target, deps):
 
 
 def up_to_date() -> bool:
-    deps = [os.path.join(CSRC, u) for u in _units()] + list(HEADERS)
-    return not _stale(OUT, deps)
+    srcs = set()
+    for u in _units():
+        srcs |= deps(os.path.join(CSRC, u))
+    return not _stale(OUT, sorted(srcs))
 
 
 def build(force: bool = False, verbose: bool = True, extra_flags=()) -> str:
@@ -68,7 +91,7 @@ def build(force: bool = False, verbose: bool = True, extra_flags=()) -> str:
         src = os.path.join(CSRC, u)
         obj = os.path.join(OBJ, u.replace(".hip", ".o"))
         objs.append(obj)
-        if force or extra_flags or _stale(obj, [src] + list(HEADERS)):
+        if force or extra_flags or _stale(obj, sorted(deps(src))):
             jobs.append([cc] + FLAGS + UNIT_FLAGS.get(u, []) + list(extra_flags) +
                         ["-c", src, "-o", obj])
 
@@ -77,7 +100,9 @@ def build(force: bool = False, verbose: bool = True, extra_flags=()) -> str:
             print("[dladmm build]", " ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
 
-    with ThreadPoolExecutor(max_workers=max(1, min(len(jobs), 6))) as ex:
+    # the long reverse-sweep units first, so they do not end up last in the pool
+    jobs.sort(key=lambda c: 0 if os.path.basename(c[-3]).startswith("dladmm_reverse_") else 1)
+    with ThreadPoolExecutor(max_workers=max(1, min(len(jobs), os.cpu_count() or 6, 8))) as ex:
         list(ex.map(run, jobs))
     tmp = OUT + ".tmp"
     run([cc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs)

@@ -3,6 +3,8 @@
 // (dladmm_layered.hip) kernels.
 #include <stdlib.h>
 
+#include <vector>
+
 #include "dladmm_common.h"
 #include "dladmm_internal.h"
 
@@ -713,7 +715,7 @@ struct BwdPlan {
   bool rev;
   int rtiles, rncg;
   int64_t Rn2, Rm2;
-  size_t off_ratp, off_rmtp, off_gu, off_rvar, off_rpart;
+  size_t off_ratp, off_rmtp, off_gu, off_rvar, off_rpart, off_rptab;
 };
 
 // DLADMM_BWD_ZMASK=0: V2 / V3 form q = W_k Var_k in BK2 (PH 2) instead of reading the shrink
@@ -807,10 +809,12 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   // (the conditions include/dladmm.h documents at dladmm_bwd_path)
   p->rev = false;
   // (E0 / L0 addressed with the outputs' row stride)
-  // Z cotangents (a torch-op loss over the returned Z_k) ride along when they share the
-  // outputs' row stride and their pointer table fits the kernel arguments
-  const bool gz_ok = !d->gZ || (d->ld_g == f.ld_out && f.layers <= kRevMaxGZ);
-  if (p->saved_p && reverse_supports(f.variant) && gz_ok && !d->gE && !d->gL && !d->gT &&
+  // upstream cotangents (a torch-op loss over the returned Z_k / E_k / L_k / T_k, as the
+  // reference's training loops build it) ride along when they share the outputs' row stride;
+  // V1's per-sample betas and their gradients too
+  const bool cot_ok = !(d->gZ || d->gE || d->gL || d->gT) || d->ld_g == f.ld_out;
+  const bool v1_ok = f.variant != DLADMM_V1_LENA || f.ld_beta == f.ld_out;
+  if (p->saved_p && reverse_supports(f.variant) && cot_ok && v1_ok &&
       f.ld_e0 == f.ld_out && f.ld_l0 == f.ld_out && rev_enabled()) {
     const int MP = kShapeMP[p->fwd.shape], NP = kShapeNP[p->fwd.shape];
     p->Rn2 = round_up(NP, 128);
@@ -852,6 +856,7 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
     p->off_rpart = o; o += align256(sizeof(float) * DLADMM_NSCALAR * K * p->rncg);
     p->off_wpart = o; o += align256(sizeof(float) * (size_t)p->nchunks * n * m);
     p->off_s1dot = o; o += align256(sizeof(double) * (size_t)s1_dot_blocks(n, m) * K);
+    p->off_rptab = o; o += align256(sizeof(void*) * (size_t)(RT_NTAB * K + 1));
     p->total = o;
     return 0;
   }
@@ -921,8 +926,29 @@ inline int run_reverse(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hip
   r.GU = GU; r.VAR = VAR; r.ldw = ldw; r.gus = gus; r.vas = vas;
   r.aer = p.Rm2;
   r.part = rpart;
+  // the sweep's pointer table (cotangents, V1's betas and their gradients), written by a kernel
+  // whose arguments carry the pointers (graph-capturable; the host array dies with this call)
+  {
+    std::vector<const void*> tab((size_t)RT_NTAB * K + 1, nullptr);
+    auto put = [&](int t, const void* const* src, int cnt) {
+      for (int k = 0; src && k < cnt; ++k) tab[rev_tab_at(t, K, k)] = src[k];
+    };
+    put(RT_GZ, (const void* const*)d->gZ, K);
+    put(RT_GE, (const void* const*)d->gE, K);
+    put(RT_GL, (const void* const*)d->gL, K);
+    put(RT_GT, (const void* const*)d->gT, K + 1);
+    if (f.variant == DLADMM_V1_LENA) {
+      put(RT_B1, (const void* const*)f.beta1_elem, K);
+      put(RT_B2, (const void* const*)f.beta2_elem, K);
+      put(RT_GB1, (const void* const*)d->g_beta1_elem, K);
+      put(RT_GB2, (const void* const*)d->g_beta2_elem, K);
+    }
+    const void** ptab = (const void**)(ws + p.off_rptab);
+    if (hipError_t e = write_ptr_table(tab.data(), (int)tab.size(), ptab, s)) return (int)e;
+    r.ptab = (const float* const*)ptab;
+  }
   r.has_gz = d->gZ ? 1 : 0;
-  for (int k = 0; k < K && d->gZ; ++k) r.gz[k] = d->gZ[k];
+  r.has_cot = (d->gE || d->gL || d->gT) ? 1 : 0;
   if (hipError_t e = launch_reverse_shape(shape, f.variant, r, p.rtiles, s)) return (int)e;
   // weight gradients gW_k = -s1 gU_k Var_k^T (split-K over the batch, fixed-order reduction),
   // layers K-1 .. 0 as the per-layer sweep visits them (a tied weight sums them in that order);
@@ -945,10 +971,13 @@ inline int run_reverse(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hip
                                            v5 ? s1dot + (int64_t)k * nbd : nullptr))
       return (int)e;
   }
-  // parameter slots of every layer: fixed-order fp64 sums of the per-wave partials
-  hipLaunchKernelGGL(loss_reduce_kernel, dim3((unsigned)(DLADMM_NSCALAR * K)), dim3(1024), 0, s,
-                     (const float*)rpart, p.rncg, d->g_scalar);
-  if (hipError_t e = hipGetLastError()) return (int)e;
+  // parameter slots of every layer: fixed-order fp64 sums of the per-wave partials (V1: its
+  // per-sample beta gradients were written elementwise by the sweep)
+  if (f.variant != DLADMM_V1_LENA) {
+    hipLaunchKernelGGL(loss_reduce_kernel, dim3((unsigned)(DLADMM_NSCALAR * K)), dim3(1024), 0,
+                       s, (const float*)rpart, p.rncg, d->g_scalar);
+    if (hipError_t e = hipGetLastError()) return (int)e;
+  }
   for (int k = 0; k < K && v5; ++k)
     if (hipError_t e = launch_s1_dot_finish(s1dot + (int64_t)k * nbd, n, m,
                                             d->g_scalar + (int64_t)k * DLADMM_NSCALAR +

@@ -172,9 +172,16 @@ static_assert(sizeof(BwdArgs) <= 2048, "kernel argument size");
 static_assert(sizeof(WgradArgs) <= 2048, "kernel argument size");
 hipError_t launch_wgrad(const WgradArgs& a, int tiles, hipStream_t s);
 
-// ---- backward as one reverse sweep (dladmm_reverse.hip): V4 / V6 after a saved-product fused
-// forward, register-resident shapes (kShapeMP / kShapeNP), no upstream output cotangents
-constexpr int kRevMaxGZ = 128;  // layers whose Z cotangents fit the kernel-argument table
+// ---- backward as one reverse sweep (dladmm_reverse.hip): V1 / V4 / V5 / V6 after a saved-
+// product fused forward, register-resident shapes (kShapeMP / kShapeNP), optional upstream
+// cotangents of Z, E, L, T
+// Device pointer table of the sweep (written per call by write_ptr_table, graph-capturable):
+// entry blocks of K (gT: K + 1) pointers, NULL = absent / zero
+enum RevTab { RT_GZ = 0, RT_GE = 1, RT_GL = 2, RT_GT = 3, RT_B1 = 4, RT_B2 = 5, RT_GB1 = 6,
+              RT_GB2 = 7, RT_NTAB = 8 };
+__host__ __device__ constexpr int rev_tab_at(int tab, int K, int k) {
+  return tab * K + (tab > RT_GT ? 1 : 0) + k;   // gT holds K + 1 entries
+}
 struct RevArgs {
   int m, n, B, K;
   int loss_kind, ncg;              // ncg: waves (column groups) = partial entries per slot
@@ -183,7 +190,9 @@ struct RevArgs {
   const float* E0; int64_t lde0;
   const float* L0; int64_t ldl0;
   const float* Z; const float* E; const float* L; const float* T; const float* P;
-  int64_t ldo;                     // the forward's outputs: Z, E, L, P [K][.][ldo], T [K+1]
+  int64_t ldo;                     // the forward's outputs: Z, E, L, P [K][.][ldo], T [K+1];
+                                   // also the row stride of the betas, their gradients and the
+                                   // cotangents (host: make_bwd_plan)
   const float* Atp;                // packed A^T            [NB/2][MB][2] fragments (pair order)
   const float* Mtp;                // packed (-s1 W_k)^T [K][MB/2][NB][2]
   const float* scal;               // [K][8]
@@ -192,8 +201,8 @@ struct RevArgs {
   int64_t aer;                     // V4: rows aer.. of layer k's Var block hold the adjoint of
                                    // E_{k-1} (carried from BK1(k) to BK1(k-1))
   float* part;                     // parameter partials [K][8][ncg]
-  int has_gz;                      // per-layer cotangents of Z (row stride ldo), NULL = 0
-  const float* gz[kRevMaxGZ];
+  const float* const* ptab;        // RevTab pointer table (device)
+  int has_gz, has_cot;             // cotangents of Z; of E / L / T
 };
 static_assert(sizeof(RevArgs) <= 2048, "kernel argument size");
 bool reverse_supports(int variant);

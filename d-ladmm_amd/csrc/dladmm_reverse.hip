@@ -1,704 +1,43 @@
-// dladmm_reverse.hip -- MI355X (gfx950 / CDNA4) backward of the K-layer D-LADMM forward as ONE
-// reverse sweep: the vector-Jacobian product torch autograd forms
-// for total_loss.backward() (main_syn_l1l1_scalar.py:298, main_syn_lasso_scalar.py:285) through
-// DLADMMNet.forward, for the scalar-parameter variants V4 / V6 after a training forward of the
-// fused kernel (which saved P_k = A Z_k, fwd_desc.P).
-//
-// The per-layer backward (dladmm_backward.hip, phases 4 / 5 / 6) runs a layer as two GEMM
-// launches whose adjoints round-trip through HBM.  This kernel has the forward's structure
-// (dladmm_fused_kernel.h) instead:
-//  * one workgroup = 4 waves = 64 batch columns, wave w owns 16.  The adjoint state -- of Z
-//    (n rows) and the partial adjoint of L_{k-1} (m rows) -- and gP (m rows) stay in registers
-//    for all K layers, in the C/D layout of v_mfma_f32_16x16x4_f32 (lane l: column l & 15, rows
-//    16 b + 4 (l >> 4) + r); X sits in LDS.  The adjoint of E_{k-1} (V4 only; V6's E-step has
-//    no E term) round-trips through the workspace rows after Var_k's, read one block ahead with
-//    the saved state: in registers it would push the kernel past the 512-register budget;
-//  * per layer k = K-1 .. 0, two products shaped exactly like the forward's two:
-//      G1'(k)  R    = A^T gP_k     rows n, contraction m  (B operand gP_k, registers)
-//      G2'(k)  gVar = M_k^T gU_k   rows m, contraction n  (B operand gU_k, registers)
-//    with M_k = -s1 W_k.  A^T and every M_k^T are packed once per call in the forward's paired
-//    fragment order and stream through the same 4-slot LDS-DMA ring.  Each output block is one
-//    fma chain over the contraction in k order -- the order of the slice kernels -- so R and
-//    gVar are the per-layer backward's bit for bit;
-//  * G1'(k)'s epilogue is BK2(k) (phase 5): gU_k = adjoint of Z_{k-1}, with S'(U_k) from the
-//    saved Z_k (for theta_z < 0 too: the forward's shrink is monotone, |Z| < 2|theta| exactly
-//    where both relus are open).  G2'(k)'s is BK3(k) + BK1(k-1) on the saved P_{k-1} (phase 6).
-//    Same expressions in the same order as those phases (the elementwise adjoints, gU and Var
-//    are the per-layer sweep's values; only the sign of a zero may differ, where that sweep
-//    adds a zero upstream cotangent);
-//  * each output pair's epilogue rows are spread over the MFMA steps of the next pair; their
-//    operands from the saved forward state (Z_k for BK2; P, E, L, T for BK1) are loaded one pair
-//    ahead and stay in flight across the ring barriers (counted vmcnt, RevWin);
-//  * the epilogues write gU_k and Var_k of every layer to the workspace; the weight gradient
-//    gW_k = -s1 gU_k Var_k^T runs afterwards as split-K GEMMs (wgrad_kernel).  Parameter partials
-//    go per (layer, slot, wave) to a buffer summed in fp64 in a fixed order.
+// dladmm_reverse.hip -- dispatch of the reverse-sweep backward (dladmm_reverse_kernel.h) to its
+// instantiations: one translation unit per E-step form for the 256 x 512 shape and one for the
+// two small shapes (dladmm_reverse_{v1,vvar,lasso}[_small].hip).
 #include "dladmm_common.h"
 #include "dladmm_internal.h"
 
-#ifndef REV_ABL
-#define REV_ABL 0  // timing / register-pressure experiments only (WRONG results): 1 no prologue
-                   // rows, 2 no G2' rows, 4 no G1' rows, 8 no Z_k loads, 16 no gU stores, 32 no
-                   // G2' operand loads, 64 no Var / adjoint-of-E stores
-#endif
-
 namespace dladmm {
 
-template <int MP, int NP>
-struct Rev {
-  static constexpr int MB = MP / 16;
-  static constexpr int NB = NP / 16;
-  static constexpr int GF = MB * NB;                       // fragments per product
-  static constexpr int CF = GF < 16 ? GF : 16;             // fragments per ring chunk
-  static constexpr int NCH = GF / CF;                      // chunks per product
-  static constexpr int SLOTS = 4;                          // ring slots (3 chunks in flight)
-  static constexpr int RING_F4 = SLOTS * CF * 64;
-  static constexpr int X_F4 = kWaves * MB * 64;            // the tile's X, resident in LDS
-  static_assert(MB % 2 == 0 && NB % 2 == 0, "output blocks are processed in pairs");
-  static_assert(GF % CF == 0 && CF % 2 == 0, "chunking");
-  static_assert((RING_F4 + X_F4) * 16 <= 160 * 1024, "LDS budget");
-};
-
-// epilogue row i (0..7: block half i / 4, row i % 4) of a pair runs at step (i * SP) / 8 of the
-// next pair's SP steps; part i of a pass's first-pair operand loads at step (i * SP) / 16
-constexpr bool rev_rows_at(int step, int SP, int i) { return (i * SP) / 8 == step; }
-constexpr int rev_part_step(int part, int SP) { return (part * SP) / 16; }
-
-// VM operations (buffer stores and loads) each step's body issues, for the counted vmcnt of the
-// ring barriers (the scheme of the forward's WinCount): with 4 slots a barrier waits for the
-// chunk DMA issued two barriers back; the bodies of the 2 * SPC steps since and the one chunk
-// DMA group issued in between are newer and stay in flight.
-//   G1' pass, pair 0: rows of the previous G2' pass's last pair (ST2 stores; the first block's
-//     rows also load the second block's LD2 operands; none in the first pass) + the Z_k loads of
-//     pair 0 (one per part); pair p > 0: rows of pair p - 1 (gU store + the Z_k load of pair p).
-//   G2' pass, pair 0: rows of G1''s last pair (gU store) + the LD2 loads of block 0's rows (parts
-//     0..3); pair p > 0: rows of pair p - 1 (ST2 stores + the LD2 loads of the next block).
-// ST2 / LD2: Var (+ V4's adjoint of E) stores; P, E, L, T (+ V4's adjoint of E) loads.
-// The parameter-partial stores of the pass boundaries are not counted (fewer counted = a
-// longer wait only).
-template <int MB, int NB, int CF, int ST2, int LD2>
-struct RevWin {
-  static constexpr int SPC = CF / 2;            // steps per chunk
-  static constexpr int WSTEPS = 2 * SPC;
-  static constexpr int DMAG = (CF + 3) / 4;     // VM operations of one chunk DMA per wave
-  static constexpr int T1 = (NB / 2) * MB, T2 = (MB / 2) * NB;  // steps of a G1' / G2' pass
-  static constexpr int rows_in(int step, int SP) {
-    int c = 0;
-    for (int i = 0; i < 8; ++i) c += rev_rows_at(step, SP, i) ? 1 : 0;
-    return c;
-  }
-  static constexpr int rows_h(int step, int SP, int h) {
-    int c = 0;
-    for (int i = 4 * h; i < 4 * h + 4; ++i) c += rev_rows_at(step, SP, i) ? 1 : 0;
-    return c;
-  }
-  static constexpr int parts_at(int step, int SP, int np) {
-    int c = 0;
-    for (int q = 0; q < np; ++q) c += rev_part_step(q * (8 / np), SP) == step ? 1 : 0;
-    return c;
-  }
-  static constexpr int ops1(int t, bool first) {
-    const int p = t / MB, s = t % MB;
-    if (p == 0)
-      return (first ? 0 : (ST2 + LD2) * rows_h(s, MB, 0) + ST2 * rows_h(s, MB, 1)) +
-             parts_at(s, MB, 8);
-    return 2 * rows_in(s, MB);
-  }
-  static constexpr int ops2(int t) {
-    const int p = t / NB, s = t % NB;
-    if (p == 0) return rows_in(s, NB) + LD2 * parts_at(s, NB, 4);
-    return (ST2 + LD2) * rows_in(s, NB);
-  }
-  template <int S, bool FIRST>
-  static constexpr int g1() {
-    if constexpr (S % SPC != SPC - 1) return 0;
-    int n = DMAG;
-    for (int t = S - WSTEPS; t < S; ++t) {
-      if (t >= 0) n += ops1(t, FIRST);
-      else if (!FIRST && T2 + t >= 0) n += ops2(T2 + t);  // the first pass follows a drain
-    }
-    return n < 63 ? n : 63;
-  }
-  template <int S>
-  static constexpr int g2() {
-    if constexpr (S % SPC != SPC - 1) return 0;
-    int n = DMAG;
-    for (int t = S - WSTEPS; t < S; ++t) {
-      if (t >= 0) n += ops2(t);
-      else if (T1 + t >= 0) n += ops1(T1 + t, true);  // the smaller of the two G1' forms
-    }
-    return n < 63 ? n : 63;
-  }
-};
-
-// GZ: per-layer output cotangents of Z (a loss built from the returned Z_k with torch ops, as
-// the reference's training loops do): one more load per G1' element, added where the per-layer
-// BK2 adds it ((adjoint + gZ_k) + A^T gP)
-template <int MP, int NP, int EMODE, bool GZ>
-__global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
-  using F = Rev<MP, NP>;
-  constexpr int MB = F::MB, NB = F::NB, CF = F::CF, NCH = F::NCH;
-  constexpr bool kAE = EMODE == EM_VVAR;  // the adjoint of E is state (workspace rows)
-  using Win = RevWin<MB, NB, CF, kAE ? 2 : 1, kAE ? 5 : 4>;
-  __shared__ f32x4 smem[F::RING_F4 + F::X_F4];
-  f32x4* ring = smem;
-  f32x4* xs = smem + F::RING_F4;  // xs[w][b][lane] = X rows 16b+4g+0..3 of this lane's column
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4;
-  const int64_t col = (int64_t)blockIdx.x * kTileCols + w * 16 + (lane & 15);
-  const bool cv = col < a.B;
-  const int m = a.m, K = a.K;
-  const int cg = blockIdx.x * kWaves + w;  // column group (wave) index of the partials
-  const uint32_t lqm = __builtin_amdgcn_readfirstlane(a.loss_kind) == DLADMM_LOSS_LASSO ? ~0u : 0u;
-  const int64_t ldo = a.ldo, ml = (int64_t)m * ldo, zl = (int64_t)a.n * ldo;
-  auto lane_off = [&](int64_t ld, bool ok) -> uint32_t {
-    return ok ? (uint32_t)((col + (int64_t)(4 * g) * ld) * 4) : kOOB;
-  };
-  const uint32_t vo = lane_off(ldo, cv);          // saved forward state
-  const uint32_t vw = lane_off(a.ldw, col < a.Bw);  // gU / Var workspaces (padding: zeros)
-  const rsrc_t none = mkrsrc(nullptr, 0u);
-  // buffer view of a wave-uniform (pointer, size) formed by runtime selects: readfirstlane keeps
-  // both in SGPRs (otherwise a select lands in VGPRs and every access becomes a waterfall loop)
-  auto urs = [](const float* p, uint32_t bytes) -> rsrc_t {
-    const uint64_t v = (uint64_t)p;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return mkrsrc((const float*)(((uint64_t)hi << 32) | lo), __builtin_amdgcn_readfirstlane(bytes));
-  };
-
-  // adjoint state: of Z (AZ; gU once G1' formed it), of E_{k-1} (AE), partial adjoint of
-  // L_{k-1} (AL), and gP (the G1' B operand).  AZ and GP are MFMA operands: AGPRs
-  float AZ[NB][4], GP[MB][4], AL[MB][4];
-  float pz[2][4];      // Z_k rows of the G1' pair being computed
-  float pg[2][4];      // GZ: the cotangent of Z_k at those rows
-  float pv[4][5];      // P_{k-1}, E_{k-2}, L_{k-2}, T_{k-1}, AE: row r of the next G2' block
-  float psz = 0.f, psb1 = 0.f, ps[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // parameter partials
-
-  // ---------------------------------------------------------------- ring (LDS-DMA) stream
-  // GEMM gi: 2 (K-1-k) = G1'(k) (A^T), 2 (K-1-k) + 1 = G2'(k) (M_k^T); past the end: A^T filler
-  const int64_t wl = (int64_t)F::GF * kFrag;  // floats per packed M_k^T
-  auto gsrc = [&](int gi) -> const float* {
-    const int kk = K - 1 - (gi >> 1);
-    return ((gi & 1) && kk >= 0) ? a.Mtp + (int64_t)kk * wl : a.Atp;
-  };
-  auto chunk_src = [&](int gi, int ch) -> const float* {
-    uint64_t sb = (uint64_t)gsrc(gi + ch / NCH);
-    asm volatile("" : "+s"(sb));
-    return (const float*)sb + (ch % NCH) * CF * kFrag;
-  };
-  auto issue = [&](const float* base, int slot) {
-    f32x4* dst = ring + slot * (CF * 64);
-    if constexpr (DLADMM_DMA4 && CF % 16 == 0) {
-#pragma unroll
-      for (int i = 0; i < CF / 16; ++i)
-        glds16x4(base + (16 * i + 4 * w) * kFrag, lane * 16, dst + (16 * i + 4 * w) * 64);
-    } else {
-#pragma unroll
-      for (int i = 0; i < (CF + 3) / 4; ++i) {
-        const int f = i * 4 + w;
-        if (CF % 4 == 0 || f < CF) glds16(base + f * kFrag, lane * 16, dst + f * 64);
-      }
-    }
-  };
-  auto slot_add = [](int s, int d) -> int {
-    s += d;
-    return s >= F::SLOTS ? s - F::SLOTS : s;
-  };
-  int cur = 0;
-  auto frag = [&](int slot, int fc) -> f32x4 { return ring[(slot * CF + fc) * 64 + lane]; };
-  // prime the ring first: its DMA overlaps the X staging and the prologue
-#pragma unroll
-  for (int c = 0; c < F::SLOTS - 1; ++c) issue(chunk_src(0, c), c);
-
-  // ---------------------------------------------------------------- initial state
-  {
-    const rsrc_t rx = mkrsrc(a.X, (uint32_t)(m * a.ldx * 4));
-    const uint32_t ox = lane_off(a.ldx, cv);
-#pragma unroll
-    for (int b = 0; b < MB; ++b) {
-      f32x4 xv;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) xv[r] = bload(rx, ox + (uint32_t)((16 * b + r) * a.ldx * 4));
-      xs[(w * MB + b) * 64 + lane] = xv;  // read back only by this wave
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        AZ[b][r] = 0.f;
-        pin_agpr(AZ[b][r]);
-      }
-#pragma unroll
-    for (int b = 0; b < MB; ++b)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) AL[b][r] = 0.f;
-  }
-
-  // ---------------------------------------------------------------- parameters
-  cfloat_p sp = (cfloat_p)a.scal;
-  // G2'(k): beta1 of BK3's layer k; BK1's layer j = k - 1 (the prologue: j = K - 1)
-  struct LP2 { float b1k, b1, b2, b3, ss2, ss2b, the, cf; };
-  auto lp2 = [&](int k, int jl) -> LP2 {
-    LP2 p;
-    const int kk = k < K ? k : K - 1;
-    const int jj = jl < 0 ? 0 : jl;
-    p.b1k = sp[kk * DLADMM_NSCALAR + DLADMM_P_BETA1];
-    p.b1 = sp[jj * DLADMM_NSCALAR + DLADMM_P_BETA1];
-    p.b2 = sp[jj * DLADMM_NSCALAR + DLADMM_P_BETA2];
-    p.b3 = sp[jj * DLADMM_NSCALAR + DLADMM_P_BETA3];
-    p.ss2 = sp[jj * DLADMM_NSCALAR + DLADMM_P_SS2];
-    p.ss2b = sp[jj * DLADMM_NSCALAR + DLADMM_P_SS2B];
-    p.the = sp[jj * DLADMM_NSCALAR + DLADMM_P_THETA_E];
-    p.cf = a.loss_kind ? ((cfloat_p)a.lcoef)[2 * jj + 1] : 0.f;
-    return p;
-  };
-  // G1'(k): the mask bound c from theta_z (0 for theta_z >= 0, else 2|theta_z|) and cz_k
-  struct LP1 { float c, cz; };
-  auto lp1 = [&](int k) -> LP1 {
-    const float th = sp[k * DLADMM_NSCALAR + DLADMM_P_THETA_Z];
-    return LP1{th >= 0.f ? 0.f : -2.0f * th, a.loss_kind ? ((cfloat_p)a.lcoef)[2 * k] : 0.f};
-  };
-
-  // ---------------------------------------------------------------- operand views
-  // BK1 of layer j reads P_j, E_{j-1}, L_{j-1} (E0 / L0 for j = 0, their own strides), T_j;
-  // the last G2' pass (BK3 of layer 0 alone) reads T_0 through the P slot
-  struct R2 { rsrc_t P, E, L, T; };
-  const uint32_t mbytes = (uint32_t)(ml * 4), ldo4 = (uint32_t)(ldo * 4);
-  auto res2 = [&](int j) -> R2 {
-    R2 o;
-    o.P = urs(a.P + j * ml, mbytes);
-    o.T = urs(a.T + j * ml, mbytes);
-    // E0 / L0 share the outputs' row stride (host: dladmm_capi.hip make_bwd_plan)
-    o.E = urs(j >= 1 ? a.E + (j - 1) * ml : a.E0, mbytes);
-    o.L = urs(j >= 1 ? a.L + (j - 1) * ml : a.L0, mbytes);
-    return o;
-  };
-  auto res2_last = [&]() -> R2 {
-    return R2{mkrsrc(a.T, mbytes), none, none, none};
-  };
-  struct R1 { rsrc_t z, gz; };  // Z_k and (GZ) its cotangent, same row stride (host: ld_g = ldo)
-  auto rz = [&](int k) -> R1 {
-    R1 o;
-    o.z = urs(a.Z + k * zl, (uint32_t)(zl * 4));
-    if constexpr (GZ) {
-      const float* gp = a.gz[k];  // kernel-argument table: scalar load
-      o.gz = urs(gp, gp ? (uint32_t)(zl * 4) : 0u);
-    } else {
-      o.gz = o.z;
-    }
-    return o;
-  };
-  auto rgu = [&](int k) { return urs(a.GU + k * a.gus, (uint32_t)(NP * a.ldw * 4)); };
-  // Var_j (rows 0..) and the adjoint of E_{j-1} (rows aeo / 4 / ldw ..) of layer j, plus the
-  // next layer's block, which holds the adjoint of E_j that BK1(j) reads
-  auto rvar = [&](int j) {
-    return urs(a.VAR + j * a.vas, (uint32_t)((j + 1 < K ? 2 : 1) * a.vas * 4));
-  };
-
-  // uniform row offsets: loads of the pair being fetched, stores of the rows being finished
-  SWalk wZ{0u, ldo4}, wPT{0u, ldo4};
-  const uint32_t ldw4 = (uint32_t)(a.ldw * 4);
-  const uint32_t aeo = (uint32_t)(a.aer * a.ldw * 4);  // byte offset of the adjoint-of-E rows
-  const uint32_t vas4 = (uint32_t)(a.vas * 4);
-  SWalk wG{0u, ldw4}, wV{0u, ldw4}, wA{0u, ldw4};
-  auto ld = [](rsrc_t r, uint32_t voff, uint32_t soff) -> float {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
-  };
-  auto pre1 = [&](const R1& r, int h, int rr) {
-    if constexpr (REV_ABL & 8) { pz[h][rr] = 0.5f; return; }
-    pz[h][rr] = ld(r.z, vo, wZ.at(rr));
-    if constexpr (GZ) pg[h][rr] = ld(r.gz, vo, wZ.at(rr));
-    if (rr == 3) wZ.next();
-  };
-  // G2' operands, one block ahead: slot rr <- row rr of the next block (rv: this pass's Var
-  // view, whose next-layer block holds the incoming adjoint of E)
-  auto pre2 = [&](const R2& o, rsrc_t rv, int rr) {
-    if constexpr (REV_ABL & 32) {
-      pv[rr][0] = 0.5f; pv[rr][1] = 0.25f; pv[rr][2] = 0.125f; pv[rr][3] = 1.f; pv[rr][4] = 0.f;
-      return;
-    }
-    const uint32_t so = wPT.at(rr);
-    pv[rr][0] = ld(o.P, vo, so);
-    pv[rr][1] = ld(o.E, vo, so);
-    pv[rr][2] = ld(o.L, vo, so);
-    pv[rr][3] = ld(o.T, vo, so);
-    if constexpr (kAE) pv[rr][4] = ld(rv, vw, wA.at(rr));
-    if (rr == 3) { wPT.next(); wA.next(); }
-  };
-  auto reset2 = [&]() {
-    wPT.reset();
-    wA.cur = __builtin_amdgcn_readfirstlane(vas4 + aeo);
-    asm volatile("" : "+s"(wA.cur));
-  };
-
-  // partial of (layer, slot): one fixed-order sum per wave, written by lane 0
-  auto flush = [&](int layer, int slot, float v) {
-    const float s = wave_sum(v);
-    if (lane == 0) a.part[((int64_t)layer * DLADMM_NSCALAR + slot) * a.ncg + cg] = s;
-  };
-  auto flush_bk1 = [&](int j) {
-    flush(j, DLADMM_P_BETA3, ps[0]);
-    if constexpr (EMODE == EM_VVAR) {
-      flush(j, DLADMM_P_BETA2, ps[1]);
-      flush(j, DLADMM_P_THETA_E, ps[2]);
-      flush(j, DLADMM_P_SS2, ps[3]);
-    } else {
-      flush(j, DLADMM_P_SS2, ps[3]);
-      flush(j, DLADMM_P_SS2B, ps[4]);
-    }
-#pragma unroll
-    for (int i = 0; i < 5; ++i) ps[i] = 0.f;
-  };
-
-  // ---------------------------------------------------------------- per-row epilogues
-  // BK2 of layer k, block b row r (dladmm_backward.hip phase 5): q = R = A^T gP_k, pz = Z_k
-  auto epi1_row = [&](const LP1& P1, rsrc_t rg, int b, int h, int r, const f32x4& q) {
-    if constexpr (REV_ABL & 4) { AZ[b][r] = q[r]; pin_agpr(AZ[b][r]); return; }
-    const float zk = pz[h][r];
-    float gZt = (GZ ? AZ[b][r] + pg[h][r] : AZ[b][r]) + q[r];
-    // + d/dZ_k of cz_k sum|Z_k|: cz_k sgn(Z_k) is exact, so the fma is phase 5's mul + add
-    const float sg = (zk > 0.f ? 1.f : 0.f) - (zk < 0.f ? 1.f : 0.f);
-    gZt = __builtin_fmaf(P1.cz, sg, gZt);
-    // S'(U) = [U - th > 0] + [-U - th > 0] in {0, 1, 2}, from Z_k = S(U, th); gZt * S' as a
-    // sum of selected gZt (exact), d/dth = [-U - th > 0] - [U - th > 0]
-    const float ga = zk > -P1.c ? gZt : 0.f, gb = zk < P1.c ? gZt : 0.f;
-    const float gU = ga + gb;
-    psz += gb - ga;
-    asm volatile("" : "+v"(psz));
-    AZ[b][r] = gU;  // adjoint of Z_{k-1}
-    pin_agpr(AZ[b][r]);
-    if constexpr (!(REV_ABL & 16)) bstore_s(rg, vw, wG.at(r), gU);
-    if (r == 3) wG.next();
-  };
-  // BK3 of layer k, then (MODE 0) BK1 of layer k - 1, block b row r (phase 6); q = gVar =
-  // M_k^T gU_k.  MODE 1: BK3 of layer 0 alone (pv[r][0] = T_0).  MODE 2: the prologue, BK1 of
-  // layer K-1 with zero incoming adjoints (q = 0).  Operands: pv[r] (block b's row r).
-  auto epi2_row = [&](auto MODE_, const LP2& P, rsrc_t rv, int b, int r, const f32x4& q,
-                      const f32x4& xv) {
-    constexpr int MODE = decltype(MODE_)::value;
-    const float gVar = q[r];
-    if constexpr ((REV_ABL & 2) && MODE != 2) { GP[b][r] = gVar; pin_agpr(GP[b][r]); return; }
-    if constexpr (MODE == 1) {
-      psb1 += gVar * pv[r][0];
-      asm volatile("" : "+v"(psb1));
-      bstore_s(rv, vw, wV.at(r), 0.f);  // keeps the row's VM count (rv: no records)
-      if constexpr (kAE) bstore_s(rv, vw, wV.at(r) + aeo, 0.f);
-      if (r == 3) wV.next();
-      return;
-    } else {
-      const float aL = AL[b][r] + gVar;   // complete adjoint of L_{k-1}
-      const float aT = P.b1k * gVar;      // adjoint of T_k (main_syn_l1l1_scalar.py:117)
-      // incoming adjoint of E_{k-1}: zero in the prologue (the buffer is not yet written)
-      const float aE = (kAE && MODE == 0) ? pv[r][4] : 0.f;
-      const float Pv = pv[r][0], ep = pv[r][1], lp = pv[r][2], tk = pv[r][3];
-      const float x = xv[r];
-      float gP, gEp = 0.f, gLp, t;
-      (void)gEp;
-      float p3 = 0.f, p2 = 0.f, pe = 0.f, ps2 = 0.f, ps2b = 0.f;
-      if constexpr (EMODE == EM_VVAR) {
-        const float r0 = (Pv + ep) - x;
-        const float vv = lp + P.b2 * r0;                  // main_syn_l1l1_scalar.py:114
-        const float eh = ep - P.ss2 * vv;                 // :115
-        const float e = shrink(eh, P.the);
-        t = (Pv + e) - x;                                 // T_k
-        const float gTn = aT + P.b3 * aL;
-        p3 = aL * t;
-        const float gEt = aE + gTn;
-        // shrink' = [eh - th > 0] + [-eh - th > 0]: gEt times it as a sum of selected gEt
-        const float ga = (eh - P.the) > 0.0f ? gEt : 0.f;
-        const float gb = (-eh - P.the) > 0.0f ? gEt : 0.f;
-        const float gEh = ga + gb;
-        pe = gb - ga;
-        const float gVV = -P.ss2 * gEh;
-        ps2 = -gEh * vv;
-        gLp = aL + gVV;
-        p2 = gVV * r0;
-        gP = gTn + P.b2 * gVV;
-        gEp = gEh + P.b2 * gVV;
-      } else {
-        const float e = P.ss2 * (x - Pv) - P.ss2b * lp;   // main_syn_lasso_scalar.py:102-103
-        t = (Pv + e) - x;
-        const float gTn = aT + P.b3 * aL;
-        p3 = aL * t;
-        const float gEt = aE + gTn;
-        ps2 = gEt * (x - Pv);
-        gP = gTn - P.ss2 * gEt;
-        ps2b = -gEt * lp;
-        gLp = aL - P.ss2b * gEt;
-      }
-      {  // d/dP of cf * fit (fit = sum|X - P|, torch sgn(0) = 0, or 0.5 sum (X - P)^2)
-        const float res = x - Pv;
-        const float sg = (res > 0.f ? 1.f : 0.f) - (res < 0.f ? 1.f : 0.f);
-        // uniform select by bit mask (a per-row branch here splits the unrolled body)
-        const float dfit = __builtin_bit_cast(
-            float, (lqm & __builtin_bit_cast(uint32_t, res)) | (~lqm & __builtin_bit_cast(uint32_t, sg)));
-        gP = gP - P.cf * dfit;
-      }
-      if constexpr (MODE == 0) {
-        psb1 += gVar * t;  // beta1 of layer k: gVar * T_k
-        asm volatile("" : "+v"(psb1));
-      }
-      ps[0] += p3; ps[1] += p2; ps[2] += pe; ps[3] += ps2; ps[4] += ps2b;
-      asm volatile("" : "+v"(ps[0]), "+v"(ps[3]));
-      if constexpr (EMODE == EM_VVAR) asm volatile("" : "+v"(ps[1]), "+v"(ps[2]));
-      else asm volatile("" : "+v"(ps[4]));
-      GP[b][r] = gP;
-      pin_agpr(GP[b][r]);
-      AL[b][r] = gLp;
-      if constexpr (!(REV_ABL & 64)) {
-        bstore_s(rv, vw, wV.at(r), lp + P.b1 * tk);  // Var_{k-1} = L_{k-2} + b1 T_{k-1}
-        if constexpr (kAE) bstore_s(rv, vw, wV.at(r) + aeo, gEp);  // adjoint of E_{k-2}
-      } else {
-        asm volatile("" ::"v"(gEp), "v"(lp + P.b1 * tk));
-      }
-      if (r == 3) wV.next();
-    }
-  };
-
-  // ---------------------------------------------------------------- one MFMA step
-  f32x4 fr[4];
-  auto step_head = [&](auto S_, int gi, auto WIN_) {
-    constexpr int s = decltype(S_)::value;
-    constexpr int WIN = decltype(WIN_)::value;
-    constexpr int fi = 2 * s, fc = fi % CF, ch = fi / CF;
-    if constexpr (fc + 2 < CF) {
-      fr[(fi + 2) % 4] = frag(cur, fc + 2);
-      fr[(fi + 3) % 4] = frag(cur, fc + 3);
-    } else {
-      if constexpr (WIN > 0) ring_barrier_cnt<WIN>();
-      else ring_barrier();
-      issue(chunk_src(gi, ch + F::SLOTS - 1), slot_add(cur, F::SLOTS - 1));
-      const int nx = slot_add(cur, 1);
-      fr[(fi + 2) % 4] = frag(nx, 0);
-      fr[(fi + 3) % 4] = frag(nx, 1);
-    }
-  };
-  auto step_tail = [&](auto S_) {
-    constexpr int s = decltype(S_)::value;
-    constexpr int fc = (2 * s) % CF;
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (fc + 2 >= CF) cur = slot_add(cur, 1);
-  };
-
-  f32x4 qa = {0.f, 0.f, 0.f, 0.f}, qb = {0.f, 0.f, 0.f, 0.f};  // pending pair accumulators
-  f32x4 xa, xb;  // X rows of the pending G2' pair
-  auto load_x = [&](int p) {
-    xa = xs[(w * MB + 2 * p) * 64 + lane];
-    xb = xs[(w * MB + 2 * p + 1) * 64 + lane];
-  };
-  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
-
-  // ---------------------------------------------------------------- prologue: BK1(K-1)
-  // On the saved P_{K-1} with zero incoming adjoints; no product, so the operand loads of
-  // pair p + 1 are issued behind each row of pair p.
-  {
-    const LP2 P = lp2(K, K - 1);
-    const R2 o = res2(K - 1);
-    const rsrc_t rv = rvar(K - 1);
-    reset2();
-    wV.reset();
-    static_for<4>([&](auto R_) { pre2(o, rv, decltype(R_)::value); });
-    static_for<MB / 2>([&](auto P_) {
-      constexpr int p = decltype(P_)::value;
-      load_x(p);
-      static_for<8>([&](auto I_) {
-        constexpr int i = decltype(I_)::value;
-        constexpr int h = i / 4, r = i % 4;
-        if constexpr (!(REV_ABL & 1))
-        epi2_row(std::integral_constant<int, 2>{}, P, rv, 2 * p + h, r, zero4, h ? xb : xa);
-        if constexpr (2 * p + h + 1 < MB) pre2(o, rv, r);  // block 2p+h+1's row r
-      });
-    });
-    flush_bk1(K - 1);
-  }
-  ring_barrier();  // the primed chunks (and every prologue load / store) are complete
-  fr[0] = frag(0, 0);
-  fr[1] = frag(0, 1);
-
-  // ---------------------------------------------------------------- the product passes
-  // G1'(k): A^T gP_k over blocks (2p, 2p+1), contraction jb = 0..MB-1.  Pair 0 runs the rows of
-  // G2'(k+1)'s last pair (Pp, rvp; none in the first pass), then flushes layer k+1's beta1 and
-  // layer k's BK1 partials.
-  auto g1_pass = [&](auto FIRST_, int k, const LP1& P1, const R1& rzk, rsrc_t rg, const LP2& Pp,
-                     const R2& op, rsrc_t rvp) {
-    constexpr bool FIRST = decltype(FIRST_)::value;
-    const int gi = 2 * (K - 1 - k);
-    wZ.reset();
-    wG.reset();
-    static_for<NB / 2>([&](auto P_) {
-      constexpr int p = decltype(P_)::value;
-      f32x4 ca = zero4, cb = zero4;
-      if constexpr (p == 0 && !FIRST) load_x(MB / 2 - 1);
-      static_for<MB>([&](auto J_) {
-        constexpr int jb = decltype(J_)::value;
-        constexpr int s = p * MB + jb;
-        step_head(std::integral_constant<int, s>{}, gi,
-                  std::integral_constant<int, Win::template g1<s, FIRST>()>{});
-        static_for<8>([&](auto I_) {
-          constexpr int i = decltype(I_)::value;
-          constexpr int h = i / 4, r = i % 4;
-          if constexpr (rev_rows_at(jb, MB, i)) {
-            if constexpr (p == 0) {
-              if constexpr (!FIRST) {
-                epi2_row(std::integral_constant<int, 0>{}, Pp, rvp, MB - 2 + h, r,
-                         h ? qb : qa, h ? xb : xa);
-                if constexpr (h == 0) pre2(op, rvp, r);  // the last block's row r
-                if constexpr (i == 7) {
-                  flush(k + 1, DLADMM_P_BETA1, psb1);
-                  psb1 = 0.f;
-                  flush_bk1(k);
-                }
-              }
-            } else {
-              epi1_row(P1, rg, 2 * p - 2 + h, h, r, h ? qb : qa);
-              pre1(rzk, h, r);  // this row's Z_k slot, for pair p
-            }
-          }
-        });
-        if constexpr (p == 0) {
-          static_for<8>([&](auto PT_) {
-            constexpr int part = decltype(PT_)::value;
-            if constexpr (rev_part_step(part, MB) == jb) pre1(rzk, part / 4, part % 4);
-          });
-        }
-        const f32x4 wa = fr[(2 * s) % 4], wb = fr[(2 * s + 1) % 4];
-        ca = mfma4(wa.x, GP[jb][0], ca);
-        cb = mfma4(wb.x, GP[jb][0], cb);
-        ca = mfma4(wa.y, GP[jb][1], ca);
-        cb = mfma4(wb.y, GP[jb][1], cb);
-        ca = mfma4(wa.z, GP[jb][2], ca);
-        cb = mfma4(wb.z, GP[jb][2], cb);
-        ca = mfma4(wa.w, GP[jb][3], ca);
-        cb = mfma4(wb.w, GP[jb][3], cb);
-        step_tail(std::integral_constant<int, s>{});
-      });
-      qa = ca;
-      qb = cb;
-    });
-  };
-  // G2'(k): M_k^T gU_k over blocks (2p, 2p+1), contraction kb = 0..NB-1.  Pair 0 runs the rows
-  // of G1'(k)'s last pair and then flushes layer k's theta_z partial; pair p > 0 those of pair
-  // p - 1 (LAST: BK3 of layer 0 alone).
-  auto g2_pass = [&](auto LAST_, int k, const LP2& P, const R2& o, rsrc_t rv, const LP1& P1,
-                     rsrc_t rg) {
-    constexpr bool LAST = decltype(LAST_)::value;
-    const int gi = 2 * (K - 1 - k) + 1;
-    wV.reset();
-    reset2();
-    static_for<MB / 2>([&](auto P_) {
-      constexpr int p = decltype(P_)::value;
-      f32x4 ca = zero4, cb = zero4;
-      if constexpr (p > 0) load_x(p - 1);
-      static_for<NB>([&](auto K_) {
-        constexpr int kb = decltype(K_)::value;
-        constexpr int s = p * NB + kb;
-        step_head(std::integral_constant<int, s>{}, gi,
-                  std::integral_constant<int, Win::template g2<s>()>{});
-        static_for<8>([&](auto I_) {
-          constexpr int i = decltype(I_)::value;
-          constexpr int h = i / 4, r = i % 4;
-          if constexpr (rev_rows_at(kb, NB, i)) {
-            if constexpr (p == 0) {
-              epi1_row(P1, rg, NB - 2 + h, h, r, h ? qb : qa);
-              if constexpr (i == 7) {
-                flush(k, DLADMM_P_THETA_Z, psz);
-                psz = 0.f;
-              }
-            } else {
-              epi2_row(std::integral_constant<int, LAST ? 1 : 0>{}, P, rv, 2 * p - 2 + h, r,
-                       h ? qb : qa, h ? xb : xa);
-              pre2(o, rv, r);  // row r of block 2p - 1 + h
-            }
-          }
-        });
-        if constexpr (p == 0) {
-          static_for<4>([&](auto PT_) {  // block 0's rows, one per part
-            constexpr int part = decltype(PT_)::value;
-            if constexpr (rev_part_step(2 * part, NB) == kb) pre2(o, rv, part);
-          });
-        }
-        const f32x4 wa = fr[(2 * s) % 4], wb = fr[(2 * s + 1) % 4];
-        ca = mfma4(wa.x, AZ[kb][0], ca);
-        cb = mfma4(wb.x, AZ[kb][0], cb);
-        ca = mfma4(wa.y, AZ[kb][1], ca);
-        cb = mfma4(wb.y, AZ[kb][1], cb);
-        ca = mfma4(wa.z, AZ[kb][2], ca);
-        cb = mfma4(wb.z, AZ[kb][2], cb);
-        ca = mfma4(wa.w, AZ[kb][3], ca);
-        cb = mfma4(wb.w, AZ[kb][3], cb);
-        step_tail(std::integral_constant<int, s>{});
-      });
-      qa = ca;
-      qb = cb;
-    });
-  };
-
-  // ---------------------------------------------------------------- K layers, last to first
-  LP1 P1 = lp1(K - 1);
-  g1_pass(std::true_type{}, K - 1, P1, rz(K - 1), rgu(K - 1), lp2(K, K - 1), res2_last(), none);
-  for (int k = K - 1; k >= 1; --k) {
-    const LP2 P = lp2(k, k - 1);
-    const R2 o = res2(k - 1);
-    const rsrc_t rv = rvar(k - 1);
-    g2_pass(std::false_type{}, k, P, o, rv, P1, rgu(k));
-    P1 = lp1(k - 1);
-    g1_pass(std::false_type{}, k - 1, P1, rz(k - 1), rgu(k - 1), P, o, rv);
-  }
-  const LP2 P0 = lp2(0, -1);
-  const R2 o0 = res2_last();
-  g2_pass(std::true_type{}, 0, P0, o0, none, P1, rgu(0));
-  // rows of layer 0's last G2' pair
-  load_x(MB / 2 - 1);
-  static_for<8>([&](auto I_) {
-    constexpr int i = decltype(I_)::value;
-    constexpr int h = i / 4, r = i % 4;
-    epi2_row(std::integral_constant<int, 1>{}, P0, none, MB - 2 + h, r, h ? qb : qa,
-             h ? xb : xa);
-    if constexpr (h == 0) pre2(o0, none, r);
-  });
-  flush(0, DLADMM_P_BETA1, psb1);
-  // drain: the ring's last LDS-DMA must land before the workgroup's LDS is released
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-template <int MP, int NP, int EM>
-hipError_t launch_rev(const RevArgs& a, int grid, hipStream_t s) {
-  if (a.has_gz)
-    hipLaunchKernelGGL((reverse_kernel<MP, NP, EM, true>), dim3(grid), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((reverse_kernel<MP, NP, EM, false>), dim3(grid), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
-
-template <int MP, int NP>
-hipError_t launch_rev_v(int variant, const RevArgs& a, int grid, hipStream_t s) {
-  switch (variant) {
-    case DLADMM_V4_SCALAR:
-    case DLADMM_V5_TIED: return launch_rev<MP, NP, EM_VVAR>(a, grid, s);
-    case DLADMM_V6_LASSO: return launch_rev<MP, NP, EM_LASSO>(a, grid, s);
-  }
-  return hipErrorInvalidValue;
-}
+// defined by the instantiation units: shape 2 (`_s2`) and shapes 0 / 1 (`_s01`)
+#define DLADMM_REV_DECL(NAME)                                                                \
+  hipError_t launch_rev_##NAME##_s2(const RevArgs& a, int grid, hipStream_t s);             \
+  hipError_t launch_rev_##NAME##_s01(int shape, const RevArgs& a, int grid, hipStream_t s);
+DLADMM_REV_DECL(v1)
+DLADMM_REV_DECL(vvar)
+DLADMM_REV_DECL(lasso)
+#undef DLADMM_REV_DECL
 
 // V5 (tied, a trainable step ss1_k on W Var): M_k^T packs -ss1_k W^T, the masks come from Z_k as
 // for V4, and ss1_k's gradient -<W, gU_k Var_k^T> is taken from the weight gradient's sums
-// (wgrad_reduce_kernel), so the sweep needs no q = W Var_k
+// (wgrad_reduce_kernel), so the sweep needs no q = W Var_k.  V1: per-sample betas, fixed
+// thresholds (scalar table: theta_z, theta_e, s1 = 1)
 bool reverse_supports(int variant) {
-  return variant == DLADMM_V4_SCALAR || variant == DLADMM_V5_TIED ||
-         variant == DLADMM_V6_LASSO;
+  return variant == DLADMM_V1_LENA || variant == DLADMM_V4_SCALAR ||
+         variant == DLADMM_V5_TIED || variant == DLADMM_V6_LASSO;
 }
 
 hipError_t launch_reverse_shape(int shape, int variant, const RevArgs& a, int grid,
                                 hipStream_t s) {
   static_assert(kNumShapes == 3, "one case per register-resident shape");
-  switch (shape) {
-#ifndef REV_ONLY_SHAPE2
-    case 0: return launch_rev_v<kShapeMP[0], kShapeNP[0]>(variant, a, grid, s);
-    case 1: return launch_rev_v<kShapeMP[1], kShapeNP[1]>(variant, a, grid, s);
-#endif
-    case 2: return launch_rev_v<kShapeMP[2], kShapeNP[2]>(variant, a, grid, s);
+  if (shape < 0 || shape > 2) return hipErrorInvalidValue;
+  switch (variant) {
+    case DLADMM_V1_LENA:
+      return shape == 2 ? launch_rev_v1_s2(a, grid, s) : launch_rev_v1_s01(shape, a, grid, s);
+    case DLADMM_V4_SCALAR:
+    case DLADMM_V5_TIED:
+      return shape == 2 ? launch_rev_vvar_s2(a, grid, s)
+                        : launch_rev_vvar_s01(shape, a, grid, s);
+    case DLADMM_V6_LASSO:
+      return shape == 2 ? launch_rev_lasso_s2(a, grid, s)
+                        : launch_rev_lasso_s01(shape, a, grid, s);
   }
   return hipErrorInvalidValue;
 }

@@ -1,0 +1,12 @@
+// dladmm_reverse_lasso_small.hip -- reverse-sweep instantiations: E-step form EM_LASSO, the two
+// small shapes (dladmm_reverse_kernel.h; dispatch: dladmm_reverse.hip).
+#include "dladmm_reverse_kernel.h"
+
+namespace dladmm {
+
+hipError_t launch_rev_lasso_s01(int shape, const RevArgs& a, int grid, hipStream_t s) {
+  if (shape == 0) return launch_rev<kShapeMP[0], kShapeNP[0], EM_LASSO>(a, grid, s);
+  return launch_rev<kShapeMP[1], kShapeNP[1], EM_LASSO>(a, grid, s);
+}
+
+}  // namespace dladmm

@@ -6,7 +6,8 @@ block, k in the same order) and every elementwise adjoint with the same expressi
   * the weight gradients -- built from gU_k and Var_k -- are equal bit for bit;
   * the parameter-slot gradients agree to the rounding of their fp32 per-wave partials (the
     kernels group the terms by wave differently): 2e-6 norm-relative per layer.
-Covered: V4 (L1L1 and LASSO objective) and V6, the three register-resident shapes with ragged
+Covered: V4 (L1L1 and LASSO objective), V6 and V1 (per-sample betas: their gradients equal bit
+for bit too), upstream cotangents of Z, E, L and T, the three register-resident shapes with ragged
 rows and columns, K = 1, theta < 0 layers (the shrink masks come from the saved Z_k), a batch
 that is not a multiple of 16 (zero padding of the gU / Var rows the weight gradient reads).
 Against the reference: tests/test_gpu_backward.py::test_fused_training_loss runs V4 / V6
@@ -108,7 +109,7 @@ def test_z_cotangents_on_the_reverse_sweep(dl, monkeypatch):
     """A torch-op loss over the returned Z_k (the reference's own training loop) hands the
     backward per-layer Z cotangents only: the reverse sweep adds them where the per-layer BK2
     does ((adjoint + gZ_k) + A^T gP), so both paths agree bit for bit on the weight gradients;
-    an unread layer's cotangent may be None.  E / L / T cotangents keep the per-layer kernels."""
+    an unread layer's cotangent may be None."""
     ops, args, r, tables = saved_forward(dl, "v4", 64, 200, 333, 3, 9960, lk=dl._lib.LOSS_L1L1)
     g = torch.Generator(device="cuda").manual_seed(9961)
     gz = [torch.randn(200, 333, device="cuda", generator=g), None,
@@ -120,9 +121,81 @@ def test_z_cotangents_on_the_reverse_sweep(dl, monkeypatch):
     per = ops.dladmm_backward(*args, r, gz, **kw)
     monkeypatch.delenv("DLADMM_BWD_REV")
     check_equal(rev, per, 3)
-    ge = [torch.ones(64, 333, device="cuda") for _ in range(3)]
-    res = ops.dladmm_backward(*args, r, gz, ge, **tables)
-    assert res.path == 0
+
+
+def _cotangents(m, n, B, K, seed, which):
+    """Random upstream cotangents of the outputs named in `which` (subset of "ZELT"), one layer
+    of each left None (an output the loss never reads)."""
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    rows = dict(Z=n, E=m, L=m, T=m)
+    out = {}
+    for nm in "ZELT":
+        if nm not in which:
+            out[nm] = None
+            continue
+        cnt = K + 1 if nm == "T" else K
+        out[nm] = [None if j == 1 % cnt else
+                   torch.randn(rows[nm], B, device="cuda", generator=g) for j in range(cnt)]
+    return out
+
+
+def both_cot(dl, variant, m, n, B, K, seed, monkeypatch, which, fused_loss):
+    lk = dl._lib.LOSS_L1L1 if fused_loss else 0
+    ops, args, r, tables = saved_forward(dl, variant, m, n, B, K, seed, lk=lk)
+    c = _cotangents(m, n, B, K, seed + 1, which)
+    kw = dict(**tables)
+    if fused_loss:
+        g = torch.Generator(device="cuda").manual_seed(seed + 2)
+        kw.update(loss_kind=lk, loss_coef=(torch.rand(K, 2, device="cuda", generator=g) *
+                                           torch.tensor([1e-2, 1.0], device="cuda")).contiguous())
+    cots = (c["Z"], c["E"], c["L"], c["T"])
+    rev = ops.dladmm_backward(*args, r, *cots, **kw)
+    monkeypatch.setenv("DLADMM_BWD_REV", "0")
+    per = ops.dladmm_backward(*args, r, *cots, **kw)
+    monkeypatch.delenv("DLADMM_BWD_REV")
+    return rev, per
+
+
+@pytest.mark.parametrize("variant", ["v4", "v6"])
+@pytest.mark.parametrize("shape", [(20, 30, 70, 3), (250, 500, 200, 4)])
+def test_elt_cotangents_on_the_reverse_sweep(variant, shape, dl, monkeypatch):
+    """Cotangents of E_k, L_k and T_k (a loss over every returned list) join the sweep in round
+    4: added to the incoming adjoints of BK1 where the per-layer kernels add them, so the two
+    paths agree bit for bit on the weight gradients (with the fused objective too)."""
+    m, n, B, K = shape
+    for which, fused in (("ZELT", False), ("ELT", True), ("L", False)):
+        rev, per = both_cot(dl, variant, m, n, B, K, 9970 + m, monkeypatch, which, fused)
+        check_equal(rev, per, K)
+
+
+def check_equal_v1(rev, per, K):
+    assert rev.path == 1 and per.path == 0
+    assert rev.g_scalar is None and per.g_scalar is None
+    assert torch.equal(rev.gW, per.gW)
+    for k in range(K):
+        assert torch.equal(rev.g_beta1[k], per.g_beta1[k]), f"g_beta1[{k}]"
+        assert torch.equal(rev.g_beta2[k], per.g_beta2[k]), f"g_beta2[{k}]"
+
+
+@pytest.mark.parametrize("shape", [(20, 30, 70, 3), (64, 200, 333, 2), (250, 500, 200, 4),
+                                   (256, 512, 64, 1)])
+@pytest.mark.parametrize("loss", ["lena", "fused", "zonly"])
+def test_reverse_v1_matches_per_layer(shape, loss, dl, monkeypatch):
+    """V1 (main_lena.py:57-98, per-sample betas) on the reverse sweep: its betas and their
+    gradients are per-element operands of the G2' rows; beta1's gradient sums BK1's term (one
+    pass) and BK3's (the next) in the per-layer sweep's order.  Losses: main_lena.py:221-228's
+    (cotangents of Z, E and L), the fused L1L1 objective, a Z-only torch loss.  Weight and
+    beta gradients equal the per-layer path's bit for bit."""
+    m, n, B, K = shape
+    which, fused = {"lena": ("ZEL", False), "fused": ("", True), "zonly": ("Z", False)}[loss]
+    rev, per = both_cot(dl, "v1", m, n, B, K, 9990 + m, monkeypatch, which, fused)
+    check_equal_v1(rev, per, K)
+
+
+def test_reverse_v1_headline_shape(dl, monkeypatch):
+    """V1 at m=256, n=512, K=15 on 4,096 columns with the main_lena.py loss's cotangents."""
+    rev, per = both_cot(dl, "v1", 256, 512, 4096, 15, 9995, monkeypatch, "ZEL", False)
+    check_equal_v1(rev, per, 15)
 
 
 def _zmask_ab(dl, variant, m, n, B, K, seed, monkeypatch, mixed=False):

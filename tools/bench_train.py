@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--alpha", type=float, default=0.001)
     ap.add_argument("--variant", default="v4", choices=["v1", "v2", "v3", "v4", "v5", "v6"],
                     help="model variant (v6: LASSO objective); the torch-op loss is V4's L1L1")
+    ap.add_argument("--lena-loss", action="store_true",
+                    help="V1 with main_lena.py:221-228's loss (torch ops over the returned Z_k, "
+                         "E_k and L_k: cotangents of Z, E and L reach the backward), alpha 0.45")
     ap.add_argument("--fused-loss", action="store_true",
                     help="net.training_loss (objective fused into the kernels) instead of the "
                          "reference's torch-op loss over the returned Z_k")
@@ -53,8 +56,14 @@ def main():
     net = dl.VARIANTS[a.variant](m=m, n=0, d=n, batch_size=B, A=A, Z0=Z0, E0=E0, L0=L0,
                                  layers=K)
     kind = "lasso" if a.variant == "v6" else "l1l1"
-    if not a.fused_loss and a.variant != "v4":
+    if a.lena_loss and a.variant != "v1":
+        raise SystemExit("--lena-loss is main_lena.py's (V1)")
+    if not a.fused_loss and not a.lena_loss and a.variant != "v4":
         raise SystemExit("the torch-op loss leg is V4's (main_syn_l1l1_scalar.py)")
+    At = A.t()
+
+    def dual_gap(x, al):  # main_lena.py:145-147
+        return torch.nn.functional.softplus(x - al) + torch.nn.functional.softplus(-x - al)
     opt = torch.optim.Adam(net.parameters(), lr=0.005)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
 
@@ -67,6 +76,17 @@ def main():
             tot, _ = net.training_loss(X, a.alpha, coeffs, kind)
             if timed:
                 ev[1].record()
+                ev[2].record()
+        elif a.lena_loss:
+            Z, E, L = net(X)
+            if timed:
+                ev[1].record()
+            tot = 0
+            for k in range(K):  # main_lena.py:221-228
+                tot = tot + (0.45 * torch.mean(torch.abs(Z[k])) + torch.mean(torch.abs(E[k])) +
+                             torch.mean(dual_gap(torch.mm(At, L[k]), 0.45)) +
+                             torch.mean(dual_gap(L[k], 1)) + torch.mean(L[k] * X))
+            if timed:
                 ev[2].record()
         else:
             Z, E, L, T = net(X)
@@ -102,9 +122,12 @@ def main():
     flop_b = 6 * K * m * n * B       # performed
     flop_r = 10 * K * m * n * B      # reference-equivalent (recomputing backward)
     res = {
-        "metric": f"training steps/s ({a.variant.upper()} forward + {kind} loss + backward + Adam)",
+        "metric": f"training steps/s ({a.variant.upper()} forward + "
+                  f"{'main_lena' if a.lena_loss else kind} loss + backward + Adam)",
         "variant": a.variant,
-        "loss_path": "fused (net.training_loss)" if a.fused_loss else "torch ops on Z_k",
+        "loss_path": ("fused (net.training_loss)" if a.fused_loss else
+                      "main_lena.py:221-228 torch ops on Z_k, E_k, L_k" if a.lena_loss else
+                      "torch ops on Z_k"),
         "batch": B, "m": m, "n": n, "layers": K,
         "step_ms": med(tot_t) * 1e3,
         "samples_per_s": B / med(tot_t),
