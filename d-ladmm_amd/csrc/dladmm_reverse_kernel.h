@@ -45,6 +45,14 @@
                    // G2' operand loads, 64 no Var / adjoint-of-E stores
 #endif
 
+#ifndef REV_SLOTS
+#define REV_SLOTS 4  // weight-ring slots (6 fit the LDS at 256 x 512 beside the AL tables)
+#endif
+#ifndef REV_DEEP
+#define REV_DEEP 0   // 1: operands two pairs / one pair ahead (needs REV_SLOTS 6); measured no
+                     // faster (7.58 vs 7.53 ms backward, profiles/r04_rev_deep_ab.json)
+#endif
+
 namespace dladmm {
 
 template <int MP, int NP>
@@ -54,7 +62,7 @@ struct Rev {
   static constexpr int GF = MB * NB;                       // fragments per product
   static constexpr int CF = GF < 16 ? GF : 16;             // fragments per ring chunk
   static constexpr int NCH = GF / CF;                      // chunks per product
-  static constexpr int SLOTS = 4;                          // ring slots (3 chunks in flight)
+  static constexpr int SLOTS = REV_SLOTS;                  // ring slots (SLOTS - 1 in flight)
   static constexpr int RING_F4 = SLOTS * CF * 64;
   static constexpr int AL_F4 = kWaves * MB * 64;           // partial adjoints of L, in LDS
   static_assert(MB % 2 == 0 && NB % 2 == 0, "output blocks are processed in pairs");
@@ -63,30 +71,35 @@ struct Rev {
 };
 
 // epilogue row i (0..7: block half i / 4, row i % 4) of a pair runs at step (i * SP) / 8 of the
-// next pair's SP steps; part i of a pass's first-pair operand loads at step (i * SP) / 16
+// next pair's SP steps; part q of the np operand-load parts of a pass's first pair runs at step
+// (q * SP) / (2 np) (the first half of the pair)
 constexpr bool rev_rows_at(int step, int SP, int i) { return (i * SP) / 8 == step; }
-constexpr int rev_part_step(int part, int SP) { return (part * SP) / 16; }
+constexpr int rev_part_step(int q, int SP, int np) { return (q * SP) / (2 * np); }
 
 // VM operations (buffer stores and loads) each step's body issues, for the counted vmcnt of the
-// ring barriers (the scheme of the forward's WinCount): with 4 slots a barrier waits for the
-// chunk DMA issued two barriers back; the bodies of the 2 * SPC steps since and the one chunk
-// DMA group issued in between are newer and stay in flight.
-//   G1' pass, pair 0: rows of the previous G2' pass's last pair (ST2 stores; the first block's
-//     rows also load the second block's LD2 operands; none in the first pass) + the LD1 loads of
-//     pair 0 (Z_k, GZ: its cotangent; one set per part); pair p > 0: rows of pair p - 1 (gU
-//     store + the LD1 loads of pair p).
-//   G2' pass, pair 0: rows of G1''s last pair (gU store) + the LD2 loads of block 0's rows (parts
-//     0..3); pair p > 0: rows of pair p - 1 (ST2 stores + the LD2 loads of the next block).
+// ring barriers (the scheme of the forward's WinCount).  With SLOTS slots a barrier waits for
+// the chunk DMA issued SLOTS - 2 barriers back; the bodies of the (SLOTS - 2) * SPC steps since
+// and the SLOTS - 3 chunk DMA groups issued in between are newer and stay in flight.
+// Operand loads run one block (G2') / one pair (G1') ahead, or with DEEP one pair / two pairs:
+//   G1' pass, pair 0: rows of the previous G2' pass's last pair (ST2 stores; not DEEP: the first
+//     block's rows also load the second block's LD2 operands; none in the first pass) + the LD1
+//     loads (Z_k, GZ: its cotangent) of pair 0 (DEEP: pairs 0 and 1) as parts; pair p > 0:
+//     rows of pair p - 1 (gU store + the LD1 loads of pair p, DEEP: p + 1 while it exists).
+//   G2' pass, pair 0: rows of G1''s last pair (gU store) + the LD2 loads of block 0's rows
+//     (DEEP: blocks 0 and 1) as parts; pair p > 0: rows of pair p - 1 (ST2 stores + the LD2
+//     loads of the next block, DEEP: of block 2p + h).
 // ST2 / LD2: the VM stores / loads of one G2' row (reverse_kernel: Var, V4's adjoint of E, V1's
 // beta gradients; P, L, T, X, E and V4's adjoint of E, V1's betas, the E / L / T cotangents).
 // The parameter-partial stores of the pass boundaries are not counted (fewer counted = a
 // longer wait only).
-template <int MB, int NB, int CF, int ST2, int LD2, int LD1>
+template <int MB, int NB, int CF, int SLOTS, int ST2, int LD2, int LD1, bool DEEP>
 struct RevWin {
   static constexpr int SPC = CF / 2;            // steps per chunk
-  static constexpr int WSTEPS = 2 * SPC;
+  static constexpr int WSTEPS = (SLOTS - 2) * SPC;
   static constexpr int DMAG = (CF + 3) / 4;     // VM operations of one chunk DMA per wave
   static constexpr int T1 = (NB / 2) * MB, T2 = (MB / 2) * NB;  // steps of a G1' / G2' pass
+  // first-pair load parts (G1': pair 1 exists when NB > 2)
+  static constexpr int NP1 = (DEEP && NB / 2 > 1) ? 16 : 8, NP2 = DEEP ? 8 : 4;
   static constexpr int rows_in(int step, int SP) {
     int c = 0;
     for (int i = 0; i < 8; ++i) c += rev_rows_at(step, SP, i) ? 1 : 0;
@@ -99,25 +112,28 @@ struct RevWin {
   }
   static constexpr int parts_at(int step, int SP, int np) {
     int c = 0;
-    for (int q = 0; q < np; ++q) c += rev_part_step(q * (8 / np), SP) == step ? 1 : 0;
+    for (int q = 0; q < np; ++q) c += rev_part_step(q, SP, np) == step ? 1 : 0;
     return c;
   }
   static constexpr int ops1(int t, bool first) {
     const int p = t / MB, s = t % MB;
-    if (p == 0)
-      return (first ? 0 : (ST2 + LD2) * rows_h(s, MB, 0) + ST2 * rows_h(s, MB, 1)) +
-             LD1 * parts_at(s, MB, 8);
-    return (1 + LD1) * rows_in(s, MB);
+    if (p == 0) {
+      const int prev = first ? 0 : DEEP ? ST2 * rows_in(s, MB)
+                                        : (ST2 + LD2) * rows_h(s, MB, 0) + ST2 * rows_h(s, MB, 1);
+      return prev + LD1 * parts_at(s, MB, NP1);
+    }
+    const bool loads = !DEEP || p + 1 < NB / 2;
+    return (1 + (loads ? LD1 : 0)) * rows_in(s, MB);
   }
   static constexpr int ops2(int t) {
     const int p = t / NB, s = t % NB;
-    if (p == 0) return rows_in(s, NB) + LD2 * parts_at(s, NB, 4);
+    if (p == 0) return rows_in(s, NB) + LD2 * parts_at(s, NB, NP2);
     return (ST2 + LD2) * rows_in(s, NB);
   }
   template <int S, bool FIRST>
   static constexpr int g1() {
     if constexpr (S % SPC != SPC - 1) return 0;
-    int n = DMAG;
+    int n = DMAG * (SLOTS - 3);
     for (int t = S - WSTEPS; t < S; ++t) {
       if (t >= 0) n += ops1(t, FIRST);
       else if (!FIRST && T2 + t >= 0) n += ops2(T2 + t);  // the first pass follows a drain
@@ -127,7 +143,7 @@ struct RevWin {
   template <int S>
   static constexpr int g2() {
     if constexpr (S % SPC != SPC - 1) return 0;
-    int n = DMAG;
+    int n = DMAG * (SLOTS - 3);
     for (int t = S - WSTEPS; t < S; ++t) {
       if (t >= 0) n += ops2(t);
       else if (T1 + t >= 0) n += ops1(T1 + t, true);  // the smaller of the two G1' forms
@@ -161,7 +177,12 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   constexpr int LD2 = 4 + (kAE ? 2 : 0) + (kV1 ? 4 : 0) + (COT ? 3 : 0);
   constexpr int ST2 = 1 + (kAE ? 1 : 0) + (kV1 ? 3 : 0);
   constexpr int LD1 = GZ ? 2 : 1;
-  using Win = RevWin<MB, NB, CF, ST2, LD2, LD1>;
+  // DEEP: operands two pairs (G1') / one pair (G2') ahead instead of one pair / one block --
+  // a second register set for them, where the registers allow (the ring's 5 chunks in flight
+  // let the counted barriers keep them in flight)
+  constexpr bool DEEP = REV_DEEP && 4 * NS + (GZ ? 16 : 8) <= 36;
+  constexpr int PV = DEEP ? 2 : 1;   // operand register sets
+  using Win = RevWin<MB, NB, CF, F::SLOTS, ST2, LD2, LD1, DEEP>;
   __shared__ f32x4 smem[F::RING_F4 + F::AL_F4];
   f32x4* ring = smem;
   // als[w][b][lane][r]: partial adjoint of L_{k-1} at rows 16b+4g+r of this lane's column, from
@@ -202,9 +223,11 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   // adjoint state: of Z (AZ; gU once G1' formed it) and gP (the G1' B operand), MFMA operands
   // in AGPRs; the partial adjoint of L_{k-1} in LDS (als), of E_{k-1} (V4) in the workspace
   float AZ[NB][4], GP[MB][4];
-  float pz[2][4];      // Z_k rows of the G1' pair being computed
-  float pg[2][4];      // GZ: the cotangent of Z_k at those rows
-  float pv[4][NS];     // the operands of row r of the next G2' block
+  float pz[PV][2][4];  // Z_k rows of a G1' pair (set: pair parity when DEEP)
+  float pg[PV][2][4];  // GZ: the cotangent of Z_k at those rows
+  float pvs_all[PV][4][NS];  // the operands of row r of a G2' block (set: block parity, DEEP)
+  auto set1 = [](int pair) { return DEEP ? (pair & 1) : 0; };
+  auto set2 = [](int blk) { return DEEP ? (blk & 1) : 0; };
   float psz = 0.f, psb1 = 0.f, ps[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // parameter partials
 
   // ---------------------------------------------------------------- ring (LDS-DMA) stream
@@ -352,39 +375,41 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   auto ld = [](rsrc_t r, uint32_t voff, uint32_t soff) -> float {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
   };
-  auto pre1 = [&](const R1& r, int h, int rr) {
-    if constexpr (REV_ABL & 8) { pz[h][rr] = 0.5f; return; }
-    pz[h][rr] = ld(r.z, vo, wZ.at(rr));
-    if constexpr (GZ) pg[h][rr] = ld(r.gz, vo, wZ.at(rr));
+  auto pre1 = [&](const R1& r, int pair, int h, int rr) {
+    const int st = set1(pair);
+    if constexpr (REV_ABL & 8) { pz[st][h][rr] = 0.5f; return; }
+    pz[st][h][rr] = ld(r.z, vo, wZ.at(rr));
+    if constexpr (GZ) pg[st][h][rr] = ld(r.gz, vo, wZ.at(rr));
     if (rr == 3) wZ.next();
   };
   // G2' operands, one block ahead: slot rr <- row rr of block `blk` (rv: this pass's Var view,
   // whose next-layer block holds the incoming adjoint of E)
   auto pre2 = [&](const R2& o, rsrc_t rv, int blk, int rr) {
-    pv[rr][S_AL] = als[al_at(blk, rr)];
+    auto& pw = pvs_all[set2(blk)];
+    pw[rr][S_AL] = als[al_at(blk, rr)];
     if constexpr (REV_ABL & 32) {
-      pv[rr][S_P] = 0.5f; pv[rr][S_L] = 0.125f; pv[rr][S_T] = 1.f; pv[rr][S_X] = 0.25f;
+      pw[rr][S_P] = 0.5f; pw[rr][S_L] = 0.125f; pw[rr][S_T] = 1.f; pw[rr][S_X] = 0.25f;
       return;
     }
     const uint32_t so = wPT.at(rr);
-    pv[rr][S_P] = ld(o.P, vo, so);
-    pv[rr][S_L] = ld(o.L, vo, so);
-    pv[rr][S_T] = ld(o.T, vo, so);
-    pv[rr][S_X] = ld(rx, vx, wX.at(rr));
+    pw[rr][S_P] = ld(o.P, vo, so);
+    pw[rr][S_L] = ld(o.L, vo, so);
+    pw[rr][S_T] = ld(o.T, vo, so);
+    pw[rr][S_X] = ld(rx, vx, wX.at(rr));
     if constexpr (kAE) {
-      pv[rr][S_E] = ld(o.E, vo, so);
-      pv[rr][S_AE] = ld(rv, vw, wA.at(rr));
+      pw[rr][S_E] = ld(o.E, vo, so);
+      pw[rr][S_AE] = ld(rv, vw, wA.at(rr));
     }
     if constexpr (kV1) {
-      pv[rr][S_B1K] = ld(o.B1K, vo, so);
-      pv[rr][S_B1J] = ld(o.B1J, vo, so);
-      pv[rr][S_B2J] = ld(o.B2J, vo, so);
-      pv[rr][S_GB1] = ld(o.GB1K, vo, so);
+      pw[rr][S_B1K] = ld(o.B1K, vo, so);
+      pw[rr][S_B1J] = ld(o.B1J, vo, so);
+      pw[rr][S_B2J] = ld(o.B2J, vo, so);
+      pw[rr][S_GB1] = ld(o.GB1K, vo, so);
     }
     if constexpr (COT) {
-      pv[rr][S_GE] = ld(o.GE, vo, so);
-      pv[rr][S_GL] = ld(o.GL, vo, so);
-      pv[rr][S_GT] = ld(o.GT, vo, so);
+      pw[rr][S_GE] = ld(o.GE, vo, so);
+      pw[rr][S_GL] = ld(o.GL, vo, so);
+      pw[rr][S_GT] = ld(o.GT, vo, so);
     }
     if (rr == 3) { wPT.next(); wX.next(); wA.next(); }
   };
@@ -419,8 +444,9 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   // BK2 of layer k, block b row r (dladmm_backward.hip phase 5): q = R = A^T gP_k, pz = Z_k
   auto epi1_row = [&](const LP1& P1, rsrc_t rg, int b, int h, int r, const f32x4& q) {
     if constexpr (REV_ABL & 4) { AZ[b][r] = q[r]; pin_agpr(AZ[b][r]); return; }
-    const float zk = pz[h][r];
-    float gZt = (GZ ? AZ[b][r] + pg[h][r] : AZ[b][r]) + q[r];
+    const int st = set1(b / 2);
+    const float zk = pz[st][h][r];
+    float gZt = (GZ ? AZ[b][r] + pg[st][h][r] : AZ[b][r]) + q[r];
     // + d/dZ_k of cz_k sum|Z_k|: cz_k sgn(Z_k) is exact, so the fma is phase 5's mul + add
     const float sg = (zk > 0.f ? 1.f : 0.f) - (zk < 0.f ? 1.f : 0.f);
     gZt = __builtin_fmaf(P1.cz, sg, gZt);
@@ -445,6 +471,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
     constexpr int MODE = decltype(MODE_)::value;
     const float gVar = q[r];
     if constexpr ((REV_ABL & 2) && MODE != 2) { GP[b][r] = gVar; pin_agpr(GP[b][r]); return; }
+    auto& pv = pvs_all[set2(b)];
     if constexpr (MODE == 1) {
       if constexpr (kV1) {
         // beta1_0's gradient: BK1(0)'s term (pv) + gVar T_0
@@ -606,7 +633,11 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
     reset2();
     wV.reset();
     wB.reset();
-    static_for<4>([&](auto R_) { pre2(o, rv, 0, decltype(R_)::value); });
+    constexpr int AHEAD = DEEP ? 2 : 1;   // blocks the operand loads run ahead
+    static_for<4 * AHEAD>([&](auto R_) {
+      constexpr int q = decltype(R_)::value;
+      pre2(o, rv, q / 4, q % 4);
+    });
     static_for<MB / 2>([&](auto P_) {
       constexpr int p = decltype(P_)::value;
       static_for<8>([&](auto I_) {
@@ -614,7 +645,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
         constexpr int h = i / 4, r = i % 4;
         if constexpr (!(REV_ABL & 1))
         epi2_row(std::integral_constant<int, 2>{}, P, o, rv, 2 * p + h, r, zero4);
-        if constexpr (2 * p + h + 1 < MB) pre2(o, rv, 2 * p + h + 1, r);  // the next block
+        if constexpr (2 * p + h + AHEAD < MB) pre2(o, rv, 2 * p + h + AHEAD, r);
       });
     });
     flush_bk1(K - 1);
@@ -649,7 +680,8 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
               if constexpr (!FIRST) {
                 epi2_row(std::integral_constant<int, 0>{}, Pp, op, rvp, MB - 2 + h, r,
                          h ? qb : qa);
-                if constexpr (h == 0) pre2(op, rvp, MB - 1, r);  // the last block's row r
+                // not DEEP: the last block's row r (DEEP: loaded in the G2' pass)
+                if constexpr (h == 0 && !DEEP) pre2(op, rvp, MB - 1, r);
                 if constexpr (i == 7) {
                   flush(k + 1, DLADMM_P_BETA1, psb1);
                   psb1 = 0.f;
@@ -658,14 +690,16 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
               }
             } else {
               epi1_row(P1, rg, 2 * p - 2 + h, h, r, h ? qb : qa);
-              pre1(rzk, h, r);  // this row's Z_k slot, for pair p
+              // this row's Z_k slot, for pair p (DEEP: p + 1)
+              if constexpr (!DEEP) pre1(rzk, p, h, r);
+              else if constexpr (p + 1 < NB / 2) pre1(rzk, p + 1, h, r);
             }
           }
         });
         if constexpr (p == 0) {
-          static_for<8>([&](auto PT_) {
-            constexpr int part = decltype(PT_)::value;
-            if constexpr (rev_part_step(part, MB) == jb) pre1(rzk, part / 4, part % 4);
+          static_for<Win::NP1>([&](auto PT_) {  // pair 0 (DEEP: and 1), one row per part
+            constexpr int q = decltype(PT_)::value;
+            if constexpr (rev_part_step(q, MB, Win::NP1) == jb) pre1(rzk, q / 8, (q / 4) % 2, q % 4);
           });
         }
         const f32x4 wa = fr[(2 * s) % 4], wb = fr[(2 * s + 1) % 4];
@@ -714,14 +748,15 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
             } else {
               epi2_row(std::integral_constant<int, LAST ? 1 : 0>{}, P, o, rv, 2 * p - 2 + h, r,
                        h ? qb : qa);
-              pre2(o, rv, 2 * p - 1 + h, r);  // row r of block 2p - 1 + h
+              // row r of block 2p - 1 + h (DEEP: 2p + h)
+              pre2(o, rv, DEEP ? 2 * p + h : 2 * p - 1 + h, r);
             }
           }
         });
         if constexpr (p == 0) {
-          static_for<4>([&](auto PT_) {  // block 0's rows, one per part
-            constexpr int part = decltype(PT_)::value;
-            if constexpr (rev_part_step(2 * part, NB) == kb) pre2(o, rv, 0, part);
+          static_for<Win::NP2>([&](auto PT_) {  // block 0's (DEEP: and 1's) rows, one per part
+            constexpr int q = decltype(PT_)::value;
+            if constexpr (rev_part_step(q, NB, Win::NP2) == kb) pre2(o, rv, q / 4, q % 4);
           });
         }
         const f32x4 wa = fr[(2 * s) % 4], wb = fr[(2 * s + 1) % 4];
@@ -759,7 +794,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
     constexpr int i = decltype(I_)::value;
     constexpr int h = i / 4, r = i % 4;
     epi2_row(std::integral_constant<int, 1>{}, P0, o0, none, MB - 2 + h, r, h ? qb : qa);
-    if constexpr (h == 0) pre2(o0, none, MB - 1, r);
+    if constexpr (h == 0 && !DEEP) pre2(o0, none, MB - 1, r);
   });
   flush(0, DLADMM_P_BETA1, psb1);
   // drain: the ring's last LDS-DMA must land before the workgroup's LDS is released

@@ -29,7 +29,8 @@ def one(spec):
     os.makedirs(out, exist_ok=True)
     obj = os.path.join(out, UNIT.replace(".hip", ".o"))
     cc = B.hipcc()
-    subprocess.run([cc] + B.FLAGS + flags + ["-c", os.path.join(B.CSRC, UNIT), "-o", obj],
+    subprocess.run([cc] + B.FLAGS + B.UNIT_FLAGS.get(UNIT, []) + flags +
+                   ["-c", os.path.join(B.CSRC, UNIT), "-o", obj],
                    check=True)
     others = [os.path.join(B.OBJ, u.replace(".hip", ".o")) for u in B.UNITS if u != UNIT]
     subprocess.run([cc, "-shared", "-fPIC", f"--offload-arch={B.ARCH}", "-o",
