@@ -22,7 +22,8 @@ UNITS = ("dladmm_capi.hip", "dladmm_fused.hip", "dladmm_fused_savep.hip", "dladm
          # reverse-sweep instantiations: one unit per E-step form and shape group (minutes each)
          "dladmm_reverse_vvar.hip", "dladmm_reverse_v1.hip", "dladmm_reverse_lasso.hip",
          "dladmm_reverse_vvar_small.hip", "dladmm_reverse_v1_small.hip",
-         "dladmm_reverse_lasso_small.hip")
+         "dladmm_reverse_lasso_small.hip", "dladmm_reverse_v2.hip", "dladmm_reverse_v3.hip",
+         "dladmm_reverse_v2_small.hip", "dladmm_reverse_v3_small.hip")
 INCLUDE = os.path.join(ROOT, "include")
 OUT = os.path.join(HERE, "lib", "libdladmm_hip.so")
 OBJ = os.path.join(HERE, "lib", "obj")

@@ -38,11 +38,8 @@ __device__ __forceinline__ SD shrink_d(float x, float th) {
 }
 
 // sum over the 16 lanes that share lane>>4 (the 16 batch columns of one row)
-__device__ __forceinline__ float col16_sum(float v) {
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+// (the reverse sweep forms the same per-row partials with the same function, dladmm_common.h)
+__device__ __forceinline__ float col16_sum(float v) { return row16_sum(v); }
 
 #ifndef BWD_EPI_FENCE
 #define BWD_EPI_FENCE 1

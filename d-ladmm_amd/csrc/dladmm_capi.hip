@@ -236,11 +236,9 @@ __global__ __launch_bounds__(1024) void param_reduce_kernel(const float* part, i
   if (threadIdx.x == 0) sums[sl] = red[0];
 }
 
-// sums[i] = sum_w part[i][w] in fp64, fixed order (bitwise reproducible)
-__global__ __launch_bounds__(1024) void loss_reduce_kernel(const float* part, int nw, double* sums) {
-  __shared__ double red[1024];
-  const int i = blockIdx.x;
-  const float* row = part + (int64_t)i * nw;
+// fp64 sum of row[0 .. nw) by a 1024-thread block in a fixed order (bitwise reproducible);
+// the result is valid in thread 0
+__device__ __forceinline__ double fixed_sum_1024(const float* row, int nw, double* red) {
   // 8 independent running sums per thread (loads in flight), combined in a fixed order
   double acc8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int wv = threadIdx.x;
@@ -258,7 +256,35 @@ __global__ __launch_bounds__(1024) void loss_reduce_kernel(const float* part, in
     if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) sums[i] = red[0];
+  return red[0];
+}
+
+// sums[i] = sum_w part[i][w] in fp64, fixed order (bitwise reproducible)
+__global__ __launch_bounds__(1024) void loss_reduce_kernel(const float* part, int nw, double* sums) {
+  __shared__ double red[1024];
+  const int i = blockIdx.x;
+  const double s = fixed_sum_1024(part + (int64_t)i * nw, nw, red);
+  if (threadIdx.x == 0) sums[i] = s;
+}
+
+// Reverse sweep, per-row parameters (V2 / V3): out[k][slot][row] (row stride ors) = the
+// fixed-order sum of the per-wave partials part[k][slot][row][0 .. nw) (row stride prs >= ors,
+// the kernel's padded rows) for the slots in `mask` and the rows the slot has (theta_z: n, the
+// others: m); every other entry 0
+__global__ __launch_bounds__(1024) void row_reduce_kernel(const float* part, int nw, int prs,
+                                                          int ors, int m, int n, unsigned mask,
+                                                          double* out) {
+  __shared__ double red[1024];
+  const int i = blockIdx.x;                 // over [K][8][ors]
+  const int row = i % ors, ks = i / ors;    // ks = k * 8 + slot
+  const int slot = ks % 8;
+  const bool ok = ((mask >> slot) & 1u) && row < (slot == DLADMM_P_THETA_Z ? n : m);
+  if (!ok) {
+    if (threadIdx.x == 0) out[i] = 0.0;
+    return;
+  }
+  const double s = fixed_sum_1024(part + ((int64_t)ks * prs + row) * nw, nw, red);
+  if (threadIdx.x == 0) out[i] = s;
 }
 
 }  // namespace dladmm
@@ -715,7 +741,7 @@ struct BwdPlan {
   bool rev;
   int rtiles, rncg;
   int64_t Rn2, Rm2;
-  size_t off_ratp, off_rmtp, off_gu, off_rvar, off_rpart, off_rptab;
+  size_t off_ratp, off_rmtp, off_gu, off_rvar, off_rpart, off_rptab, off_rrow;
 };
 
 // DLADMM_BWD_ZMASK=0: V2 / V3 form q = W_k Var_k in BK2 (PH 2) instead of reading the shrink
@@ -804,8 +830,8 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   p->nslots = p->ncg * (p->slices_m > p->slices_n ? p->slices_m : p->slices_n);
   const int64_t rs = f.row_stride > 0 ? f.row_stride : 1;
   const int64_t part_floats = 8 * (p->nslots > rs * p->ncg ? (int64_t)p->nslots : rs * p->ncg);
-  // one reverse-sweep kernel: V4 / V5 / V6 after a saved-product fused forward, no gE / gL / gT
-  // cotangents (gZ allowed, below), 32-bit workspace offsets, workspace under rev_ws_cap()
+  // one reverse-sweep kernel: any variant after a saved-product fused forward, cotangents with
+  // the outputs' row stride, 32-bit workspace offsets, workspace under rev_ws_cap()
   // (the conditions include/dladmm.h documents at dladmm_bwd_path)
   p->rev = false;
   // (E0 / L0 addressed with the outputs' row stride)
@@ -823,8 +849,11 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
     // the sweep keeps gU_k and Var_k of every layer: (Rn2 + Rm2 + MP) x Bpad floats per layer
     // (≈256 MiB per layer at 256 x 512, B = 65,536) where the per-layer phases need O(1) in K;
     // above rev_ws_cap() the per-layer phases run instead of a workspace that may not fit
+    const bool rowv = f.variant == DLADMM_V2_LTHETA || f.variant == DLADMM_V3_FULL;
     const size_t rev_bytes = (size_t)(K_of(f) + 1) * MP * NP * 4 +
-                             (size_t)K_of(f) * (p->Rn2 + p->Rm2 + MP) * p->Bpad * 4;
+                             (size_t)K_of(f) * (p->Rn2 + p->Rm2 + MP) * p->Bpad * 4 +
+                             (rowv ? (size_t)8 * K_of(f) * (MP > NP ? MP : NP) *
+                                         ((B + 63) / 64 * 4) * 4 : 0);
     if ((int64_t)NP * p->Bpad * 4 < lim && 2 * (p->Rm2 + MP) * p->Bpad * 4 < lim &&
         rev_bytes <= rev_ws_cap()) {
       p->rev = true;
@@ -857,6 +886,12 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
     p->off_wpart = o; o += align256(sizeof(float) * (size_t)p->nchunks * n * m);
     p->off_s1dot = o; o += align256(sizeof(double) * (size_t)s1_dot_blocks(n, m) * K);
     p->off_rptab = o; o += align256(sizeof(void*) * (size_t)(RT_NTAB * K + 1));
+    // V2 / V3: per-row partials [K][8][max(MP, NP)][waves] (the kernel's padded rows)
+    const bool rowk = f.variant == DLADMM_V2_LTHETA || f.variant == DLADMM_V3_FULL;
+    p->off_rrow = o;
+    const int RS = kShapeMP[p->fwd.shape] > kShapeNP[p->fwd.shape] ? kShapeMP[p->fwd.shape]
+                                                                    : kShapeNP[p->fwd.shape];
+    if (rowk) o += align256(sizeof(float) * 8 * K * (size_t)RS * p->rncg);
     p->total = o;
     return 0;
   }
@@ -949,6 +984,11 @@ inline int run_reverse(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hip
   }
   r.has_gz = d->gZ ? 1 : 0;
   r.has_cot = (d->gE || d->gL || d->gT) ? 1 : 0;
+  const bool rowk = f.variant == DLADMM_V2_LTHETA || f.variant == DLADMM_V3_FULL;
+  if (rowk) {
+    r.rowp = f.row_params; r.rstride = f.row_stride;
+    r.rpart = (float*)(ws + p.off_rrow);
+  }
   if (hipError_t e = launch_reverse_shape(shape, f.variant, r, p.rtiles, s)) return (int)e;
   // weight gradients gW_k = -s1 gU_k Var_k^T (split-K over the batch, fixed-order reduction),
   // layers K-1 .. 0 as the per-layer sweep visits them (a tied weight sums them in that order);
@@ -973,7 +1013,16 @@ inline int run_reverse(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hip
   }
   // parameter slots of every layer: fixed-order fp64 sums of the per-wave partials (V1: its
   // per-sample beta gradients were written elementwise by the sweep)
-  if (f.variant != DLADMM_V1_LENA) {
+  if (rowk) {
+    // V2: theta_z, beta1 (BK3), beta3 (its L term), beta2, theta_e; V3 also ss2
+    unsigned mask = (1u << DLADMM_P_THETA_Z) | (1u << DLADMM_P_BETA1) | (1u << DLADMM_P_BETA3) |
+                    (1u << DLADMM_P_BETA2) | (1u << DLADMM_P_THETA_E);
+    if (f.variant == DLADMM_V3_FULL) mask |= 1u << DLADMM_P_SS2;
+    hipLaunchKernelGGL(row_reduce_kernel, dim3((unsigned)(8 * K * f.row_stride)), dim3(1024), 0,
+                       s, (const float*)r.rpart, p.rncg, MP > NP ? MP : NP, (int)f.row_stride, m,
+                       n, mask, d->g_row);
+    if (hipError_t e = hipGetLastError()) return (int)e;
+  } else if (f.variant != DLADMM_V1_LENA) {
     hipLaunchKernelGGL(loss_reduce_kernel, dim3((unsigned)(DLADMM_NSCALAR * K)), dim3(1024), 0,
                        s, (const float*)rpart, p.rncg, d->g_scalar);
     if (hipError_t e = hipGetLastError()) return (int)e;

@@ -157,6 +157,18 @@ __device__ __forceinline__ float col_sum(float v) {
   return v;
 }
 
+// sum over the 16 lanes of a DPP row (l & ~15 .. +15: the 16 batch columns of one MFMA C/D row
+// group), every lane of the row receiving it: four v_add_f32 with DPP operands (xor 1, xor 2,
+// the half-row mirror, the row mirror) -- no LDS round trip, no address registers.  The order
+// is fixed, and the two lanes that combine a pair of partial sums add them in the same order.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

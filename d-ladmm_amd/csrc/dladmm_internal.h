@@ -203,6 +203,8 @@ struct RevArgs {
   float* part;                     // parameter partials [K][8][ncg]
   const float* const* ptab;        // RevTab pointer table (device)
   int has_gz, has_cot;             // cotangents of Z; of E / L / T
+  const float* rowp; int64_t rstride;  // V2 / V3: per-row parameter table [K][8][rstride]
+  float* rpart;                    // V2 / V3: per-row partials [K][8][rstride][ncg]
 };
 static_assert(sizeof(RevArgs) <= 2048, "kernel argument size");
 bool reverse_supports(int variant);

@@ -13,15 +13,18 @@ namespace dladmm {
 DLADMM_REV_DECL(v1)
 DLADMM_REV_DECL(vvar)
 DLADMM_REV_DECL(lasso)
+DLADMM_REV_DECL(v2)
+DLADMM_REV_DECL(v3)
 #undef DLADMM_REV_DECL
 
 // V5 (tied, a trainable step ss1_k on W Var): M_k^T packs -ss1_k W^T, the masks come from Z_k as
 // for V4, and ss1_k's gradient -<W, gU_k Var_k^T> is taken from the weight gradient's sums
 // (wgrad_reduce_kernel), so the sweep needs no q = W Var_k.  V1: per-sample betas, fixed
-// thresholds (scalar table: theta_z, theta_e, s1 = 1)
+// thresholds (scalar table: theta_z, theta_e, s1 = 1).  V2 / V3: per-row parameters from the row
+// table, per-row gradient partials
 bool reverse_supports(int variant) {
-  return variant == DLADMM_V1_LENA || variant == DLADMM_V4_SCALAR ||
-         variant == DLADMM_V5_TIED || variant == DLADMM_V6_LASSO;
+  return variant == DLADMM_V1_LENA || variant == DLADMM_V2_LTHETA || variant == DLADMM_V3_FULL ||
+         variant == DLADMM_V4_SCALAR || variant == DLADMM_V5_TIED || variant == DLADMM_V6_LASSO;
 }
 
 hipError_t launch_reverse_shape(int shape, int variant, const RevArgs& a, int grid,
@@ -31,6 +34,10 @@ hipError_t launch_reverse_shape(int shape, int variant, const RevArgs& a, int gr
   switch (variant) {
     case DLADMM_V1_LENA:
       return shape == 2 ? launch_rev_v1_s2(a, grid, s) : launch_rev_v1_s01(shape, a, grid, s);
+    case DLADMM_V2_LTHETA:
+      return shape == 2 ? launch_rev_v2_s2(a, grid, s) : launch_rev_v2_s01(shape, a, grid, s);
+    case DLADMM_V3_FULL:
+      return shape == 2 ? launch_rev_v3_s2(a, grid, s) : launch_rev_v3_s01(shape, a, grid, s);
     case DLADMM_V4_SCALAR:
     case DLADMM_V5_TIED:
       return shape == 2 ? launch_rev_vvar_s2(a, grid, s)

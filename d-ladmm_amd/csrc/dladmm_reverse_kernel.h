@@ -81,6 +81,7 @@ constexpr int rev_part_step(int q, int SP, int np) { return (q * SP) / (2 * np);
 // the chunk DMA issued SLOTS - 2 barriers back; the bodies of the (SLOTS - 2) * SPC steps since
 // and the SLOTS - 3 chunk DMA groups issued in between are newer and stay in flight.
 // Operand loads run one block (G2') / one pair (G1') ahead, or with DEEP one pair / two pairs:
+// ST1: the VM stores of one G1' row (gU; ROWP: theta_z's per-row partial).
 //   G1' pass, pair 0: rows of the previous G2' pass's last pair (ST2 stores; not DEEP: the first
 //     block's rows also load the second block's LD2 operands; none in the first pass) + the LD1
 //     loads (Z_k, GZ: its cotangent) of pair 0 (DEEP: pairs 0 and 1) as parts; pair p > 0:
@@ -92,7 +93,7 @@ constexpr int rev_part_step(int q, int SP, int np) { return (q * SP) / (2 * np);
 // beta gradients; P, L, T, X, E and V4's adjoint of E, V1's betas, the E / L / T cotangents).
 // The parameter-partial stores of the pass boundaries are not counted (fewer counted = a
 // longer wait only).
-template <int MB, int NB, int CF, int SLOTS, int ST2, int LD2, int LD1, bool DEEP>
+template <int MB, int NB, int CF, int SLOTS, int ST1, int ST2, int LD2, int LD1, bool DEEP>
 struct RevWin {
   static constexpr int SPC = CF / 2;            // steps per chunk
   static constexpr int WSTEPS = (SLOTS - 2) * SPC;
@@ -123,11 +124,11 @@ struct RevWin {
       return prev + LD1 * parts_at(s, MB, NP1);
     }
     const bool loads = !DEEP || p + 1 < NB / 2;
-    return (1 + (loads ? LD1 : 0)) * rows_in(s, MB);
+    return (ST1 + (loads ? LD1 : 0)) * rows_in(s, MB);
   }
   static constexpr int ops2(int t) {
     const int p = t / NB, s = t % NB;
-    if (p == 0) return rows_in(s, NB) + LD2 * parts_at(s, NB, NP2);
+    if (p == 0) return ST1 * rows_in(s, NB) + LD2 * parts_at(s, NB, NP2);
     return (ST2 + LD2) * rows_in(s, NB);
   }
   template <int S, bool FIRST>
@@ -159,30 +160,43 @@ struct RevWin {
 // them.  EMODE EM_V1: V1 (main_lena.py:57-98), per-sample betas (m, B) -- their values and
 // gradients are per-element operands of the G2' rows; beta1's gradient sums BK1's term (one G2'
 // pass) and BK3's (the next), so it goes through HBM between the two passes as in the per-layer
-// sweep.
-template <int MP, int NP, int EMODE, bool GZ, bool COT>
+// sweep.  ROWP: V2 / V3 (main_syn_l1l1_ltheta.py, main_syn_l1l1_full.py), per-row parameters:
+// their values are per-row operands (a row-table load whose 16 lanes of a row share the address)
+// and their gradients per-row partials -- the 16 columns of a wave summed (col16_sum) and written
+// per (layer, slot, row, wave) exactly as the per-layer kernels write them, then reduced in fp64
+// in a fixed order.
+template <int MP, int NP, int EMODE, bool GZ, bool COT, bool ROWP>
 __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   using F = Rev<MP, NP>;
   constexpr int MB = F::MB, NB = F::NB, CF = F::CF, NCH = F::NCH;
-  constexpr bool kAE = EMODE == EM_VVAR;  // the adjoint of E is state (workspace rows)
-  constexpr bool kV1 = EMODE == EM_V1;    // per-sample betas
+  constexpr bool kAE = EMODE == EM_VVAR;             // the adjoint of E is state (workspace rows)
+  constexpr bool kV1 = EMODE == EM_V1 && !ROWP;      // V1: per-sample betas
+  constexpr bool kSC = !kV1 && !ROWP;                // scalar parameters (V4 / V5 / V6)
   // operands of one G2' row (pv slots): saved state, X, the partial adjoint of L (LDS), then the
   // variant's own and the cotangents
   constexpr int S_P = 0, S_L = 1, S_T = 2, S_X = 3, S_AL = 4;
-  constexpr int S_E = 5, S_AE = 6;                              // V4
+  constexpr int S_E = 5, S_AE = 6;                              // V3 / V4 / V5
   constexpr int S_B1K = 5, S_B1J = 6, S_B2J = 7, S_GB1 = 8;     // V1
-  constexpr int S_C = kAE ? 7 : (kV1 ? 9 : 5);
+  constexpr int S_R = kAE ? 7 : 5;                              // ROWP: per-row parameters
+  constexpr int S_RB1K = S_R, S_RB1J = S_R + 1, S_RB2J = S_R + 2, S_RTHE = S_R + 3;
+  constexpr int S_RB3J = S_R + 4, S_RSS2J = S_R + 5;            // ROWP with the VVar E-step
+  constexpr int NR = ROWP ? (kAE ? 6 : 4) : 0;
+  constexpr int S_C = kV1 ? 9 : (kAE ? 7 : 5) + NR;
   constexpr int S_GE = S_C, S_GL = S_C + 1, S_GT = S_C + 2;     // COT
   constexpr int NS = S_C + (COT ? 3 : 0);
-  constexpr int LD2 = 4 + (kAE ? 2 : 0) + (kV1 ? 4 : 0) + (COT ? 3 : 0);
-  constexpr int ST2 = 1 + (kAE ? 1 : 0) + (kV1 ? 3 : 0);
-  constexpr int LD1 = GZ ? 2 : 1;
+  // per-row parameter gradient slots a G2' row stores (BK3's beta1 of layer k; BK1's of layer
+  // k - 1): V2 beta3 (= beta1's L term), beta2, theta_e; V3 also ss2
+  constexpr int NRS = ROWP ? (kAE ? 5 : 4) : 0;
+  constexpr int LD2 = 4 + (kAE ? 2 : 0) + (kV1 ? 4 : 0) + NR + (COT ? 3 : 0);
+  constexpr int ST2 = 1 + (kAE ? 1 : 0) + (kV1 ? 3 : 0) + NRS;
+  constexpr int LD1 = 1 + (GZ ? 1 : 0) + (ROWP ? 1 : 0);
   // DEEP: operands two pairs (G1') / one pair (G2') ahead instead of one pair / one block --
   // a second register set for them, where the registers allow (the ring's 5 chunks in flight
   // let the counted barriers keep them in flight)
   constexpr bool DEEP = REV_DEEP && 4 * NS + (GZ ? 16 : 8) <= 36;
   constexpr int PV = DEEP ? 2 : 1;   // operand register sets
-  using Win = RevWin<MB, NB, CF, F::SLOTS, ST2, LD2, LD1, DEEP>;
+  constexpr int ST1 = ROWP ? 2 : 1;
+  using Win = RevWin<MB, NB, CF, F::SLOTS, ST1, ST2, LD2, LD1, DEEP>;
   __shared__ f32x4 smem[F::RING_F4 + F::AL_F4];
   f32x4* ring = smem;
   // als[w][b][lane][r]: partial adjoint of L_{k-1} at rows 16b+4g+r of this lane's column, from
@@ -225,6 +239,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   float AZ[NB][4], GP[MB][4];
   float pz[PV][2][4];  // Z_k rows of a G1' pair (set: pair parity when DEEP)
   float pg[PV][2][4];  // GZ: the cotangent of Z_k at those rows
+  float pt[PV][2][4];  // ROWP: theta_z of those rows
   float pvs_all[PV][4][NS];  // the operands of row r of a G2' block (set: block parity, DEEP)
   auto set1 = [](int pair) { return DEEP ? (pair & 1) : 0; };
   auto set2 = [](int blk) { return DEEP ? (blk & 1) : 0; };
@@ -284,9 +299,11 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   // G2'(k): beta1 of BK3's layer k; BK1's layer j = k - 1 (the prologue: j = K - 1)
   struct LP2 { float b1k, b1, b2, b3, ss2, ss2b, the, cf; };
   auto lp2 = [&](int k, int jl) -> LP2 {
-    LP2 p;
+    LP2 p{};
     const int kk = k < K ? k : K - 1;
     const int jj = jl < 0 ? 0 : jl;
+    p.cf = a.loss_kind ? ((cfloat_p)a.lcoef)[2 * jj + 1] : 0.f;
+    if constexpr (ROWP) return p;  // per-row parameters: row-table operands (no scalar table)
     p.b1k = sp[kk * DLADMM_NSCALAR + DLADMM_P_BETA1];
     p.b1 = sp[jj * DLADMM_NSCALAR + DLADMM_P_BETA1];
     p.b2 = sp[jj * DLADMM_NSCALAR + DLADMM_P_BETA2];
@@ -294,13 +311,12 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
     p.ss2 = sp[jj * DLADMM_NSCALAR + DLADMM_P_SS2];
     p.ss2b = sp[jj * DLADMM_NSCALAR + DLADMM_P_SS2B];
     p.the = sp[jj * DLADMM_NSCALAR + DLADMM_P_THETA_E];
-    p.cf = a.loss_kind ? ((cfloat_p)a.lcoef)[2 * jj + 1] : 0.f;
     return p;
   };
   // G1'(k): the mask bound c from theta_z (0 for theta_z >= 0, else 2|theta_z|) and cz_k
   struct LP1 { float c, cz; };
   auto lp1 = [&](int k) -> LP1 {
-    const float th = sp[k * DLADMM_NSCALAR + DLADMM_P_THETA_Z];
+    const float th = ROWP ? 0.f : sp[k * DLADMM_NSCALAR + DLADMM_P_THETA_Z];
     return LP1{th >= 0.f ? 0.f : -2.0f * th, a.loss_kind ? ((cfloat_p)a.lcoef)[2 * k] : 0.f};
   };
 
@@ -309,7 +325,32 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   // V1: beta1_{j+1} (BK3's), beta1_j, beta2_j and the BK1 part of beta1_{j+1}'s gradient; COT:
   // the cotangents of E_j, L_j and T_{j+1}.  The last G2' pass (BK3 of layer 0 alone) reads T_0
   // through the P slot (V1: and beta1_0's gradient so far)
-  struct R2 { rsrc_t P, E, L, T, B1K, B1J, B2J, GB1K, GB1J, GB2J, GE, GL, GT; };
+  // ROWP: the row table [K][8][rstride] (lane: rows 4g.. of a block, the 16 lanes of a row on
+  // one address; rows past m / n read finite table entries that meet zero adjoints) and the
+  // per-row partials [K][8][RS][ncg], RS = max(MP, NP) rows so that the padded rows' partials
+  // land in the buffer too -- a per-lane row test here would be hoisted out of the unrolled
+  // passes as one live register per (block, row); the reduction reads rows < m / n only
+  constexpr int RS = MP > NP ? MP : NP;
+  const int64_t rst = ROWP ? a.rstride : 0;
+  const rsrc_t rrow = ROWP ? mkrsrc(a.rowp, (uint32_t)(K * 8 * rst * 4)) : none;
+  const uint32_t vr = (uint32_t)(16 * g);
+  auto rbase = [&](int k, int slot) -> uint32_t {
+    return __builtin_amdgcn_readfirstlane((uint32_t)(((int64_t)k * 8 + slot) * rst * 4));
+  };
+  const int64_t pslot = (int64_t)RS * a.ncg;   // floats per (layer, slot) of the partials
+  auto rpart = [&](int k) {
+    return urs(a.rpart + (int64_t)k * 8 * pslot, (uint32_t)(8 * pslot * 4));
+  };
+  const uint32_t vpr = (lane & 15) == 0 ? (uint32_t)(((int64_t)(4 * g) * a.ncg + cg) * 4) : kOOB;
+  auto pso = [&](int slot) -> uint32_t {
+    return __builtin_amdgcn_readfirstlane((uint32_t)(slot * pslot * 4));
+  };
+  const uint32_t ldp4 = (uint32_t)(a.ncg * 4);
+  struct R2 {
+    rsrc_t P, E, L, T, B1K, B1J, B2J, GB1K, GB1J, GB2J, GE, GL, GT;
+    rsrc_t PK, PJ;                              // ROWP: per-row partials of layers k and j
+    uint32_t rb1k, rb1j, rb2j, rthe, rb3j, rss2; // ROWP: row-table offsets
+  };
   const uint32_t mbytes = (uint32_t)(ml * 4), ldo4 = (uint32_t)(ldo * 4);
   auto tview = [&](int t, int k) -> rsrc_t {
     const float* p = tptr(t, k);
@@ -336,6 +377,17 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
       o.GL = tview(RT_GL, j);
       o.GT = tview(RT_GT, j + 1);
     }
+    if constexpr (ROWP) {
+      const bool bk3 = j + 1 < K;
+      o.PK = bk3 ? rpart(j + 1) : none;
+      o.PJ = rpart(j);
+      o.rb1k = rbase(bk3 ? j + 1 : j, DLADMM_P_BETA1);
+      o.rb1j = rbase(j, DLADMM_P_BETA1);
+      o.rb2j = rbase(j, DLADMM_P_BETA2);
+      o.rthe = rbase(j, DLADMM_P_THETA_E);
+      o.rb3j = rbase(j, DLADMM_P_BETA3);
+      o.rss2 = rbase(j, DLADMM_P_SS2);
+    }
     return o;
   };
   auto res2_last = [&]() -> R2 {
@@ -344,13 +396,24 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
     o.E = o.L = o.T = none;
     o.B1K = o.B1J = o.B2J = o.GB1J = o.GB2J = o.GE = o.GL = o.GT = none;
     o.GB1K = kV1 ? tview(RT_GB1, 0) : none;
+    if constexpr (ROWP) {
+      o.PK = rpart(0);
+      o.PJ = none;
+      o.rb1k = o.rb1j = o.rb2j = o.rthe = o.rb3j = o.rss2 = rbase(0, DLADMM_P_BETA1);
+    }
     return o;
   };
   const rsrc_t rx = mkrsrc(a.X, (uint32_t)(m * a.ldx * 4));
-  struct R1 { rsrc_t z, gz; };  // Z_k and (GZ) its cotangent, same row stride (host: ld_g = ldo)
+  // Z_k and (GZ) its cotangent, same row stride (host: ld_g = ldo); ROWP: theta_z's row-table
+  // offset and the layer's per-row partials
+  struct R1 { rsrc_t z, gz, pk; uint32_t rthz; };
   auto rz = [&](int k) -> R1 {
     R1 o;
     o.z = urs(a.Z + k * zl, (uint32_t)(zl * 4));
+    if constexpr (ROWP) {
+      o.pk = rpart(k);
+      o.rthz = rbase(k, DLADMM_P_THETA_Z);
+    }
     if constexpr (GZ) {
       const float* gp = tptr(RT_GZ, k);
       o.gz = urs(gp, gp ? (uint32_t)(zl * 4) : 0u);
@@ -372,6 +435,14 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   const uint32_t aeo = (uint32_t)(a.aer * a.ldw * 4);  // byte offset of the adjoint-of-E rows
   const uint32_t vas4 = (uint32_t)(a.vas * 4);
   SWalk wG{0u, ldw4}, wV{0u, ldw4}, wA{0u, ldw4}, wB{0u, ldo4};
+  // ROWP: row-table loads (G1' / G2' operand rows) and per-row partial stores (G1' / G2' rows)
+  SWalk wR1{0u, 4u}, wR2{0u, 4u}, wP1{0u, ldp4}, wP2{0u, ldp4};
+  // per-row partial of one element row: the wave's 16 columns summed (the per-layer kernels'
+  // col16_sum), stored by lanes l & 15 == 0
+  auto pstore = [&](rsrc_t r, uint32_t soff, int row, int nrows, float v) {
+    (void)row; (void)nrows;
+    bstore_s(r, vpr, soff, row16_sum(v));
+  };
   auto ld = [](rsrc_t r, uint32_t voff, uint32_t soff) -> float {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
   };
@@ -380,7 +451,11 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
     if constexpr (REV_ABL & 8) { pz[st][h][rr] = 0.5f; return; }
     pz[st][h][rr] = ld(r.z, vo, wZ.at(rr));
     if constexpr (GZ) pg[st][h][rr] = ld(r.gz, vo, wZ.at(rr));
-    if (rr == 3) wZ.next();
+    if constexpr (ROWP) pt[st][h][rr] = ld(rrow, vr, r.rthz + wR1.at(rr));
+    if (rr == 3) {
+      wZ.next();
+      if constexpr (ROWP) wR1.next();
+    }
   };
   // G2' operands, one block ahead: slot rr <- row rr of block `blk` (rv: this pass's Var view,
   // whose next-layer block holds the incoming adjoint of E)
@@ -406,23 +481,38 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
       pw[rr][S_B2J] = ld(o.B2J, vo, so);
       pw[rr][S_GB1] = ld(o.GB1K, vo, so);
     }
+    if constexpr (ROWP) {
+      const uint32_t rs = wR2.at(rr);
+      pw[rr][S_RB1K] = ld(rrow, vr, o.rb1k + rs);
+      pw[rr][S_RB1J] = ld(rrow, vr, o.rb1j + rs);
+      pw[rr][S_RB2J] = ld(rrow, vr, o.rb2j + rs);
+      pw[rr][S_RTHE] = ld(rrow, vr, o.rthe + rs);
+      if constexpr (kAE) {
+        pw[rr][S_RB3J] = ld(rrow, vr, o.rb3j + rs);
+        pw[rr][S_RSS2J] = ld(rrow, vr, o.rss2 + rs);
+      }
+    }
     if constexpr (COT) {
       pw[rr][S_GE] = ld(o.GE, vo, so);
       pw[rr][S_GL] = ld(o.GL, vo, so);
       pw[rr][S_GT] = ld(o.GT, vo, so);
     }
-    if (rr == 3) { wPT.next(); wX.next(); wA.next(); }
+    if (rr == 3) {
+      wPT.next(); wX.next(); wA.next();
+      if constexpr (ROWP) wR2.next();
+    }
   };
   auto reset2 = [&]() {
     wPT.reset();
     wX.reset();
+    wR2.reset();
     wA.cur = __builtin_amdgcn_readfirstlane(vas4 + aeo);
     asm volatile("" : "+s"(wA.cur));
   };
 
   // partial of (layer, slot): one fixed-order sum per wave, written by lane 0
   auto flush = [&](int layer, int slot, float v) {
-    if constexpr (kV1) return;  // V1 has no scalar parameters
+    if constexpr (!kSC) return;  // V1: no scalar parameters; V2 / V3: per-row partials
     const float s = wave_sum(v);
     if (lane == 0) a.part[((int64_t)layer * DLADMM_NSCALAR + slot) * a.ncg + cg] = s;
   };
@@ -442,24 +532,37 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
 
   // ---------------------------------------------------------------- per-row epilogues
   // BK2 of layer k, block b row r (dladmm_backward.hip phase 5): q = R = A^T gP_k, pz = Z_k
-  auto epi1_row = [&](const LP1& P1, rsrc_t rg, int b, int h, int r, const f32x4& q) {
+  auto epi1_row = [&](const LP1& P1, const R1& rzk, rsrc_t rg, int b, int h, int r,
+                      const f32x4& q) {
     if constexpr (REV_ABL & 4) { AZ[b][r] = q[r]; pin_agpr(AZ[b][r]); return; }
     const int st = set1(b / 2);
     const float zk = pz[st][h][r];
+    float cth = P1.c;
+    if constexpr (ROWP) {
+      const float th = pt[st][h][r];
+      cth = th >= 0.f ? 0.f : -2.0f * th;
+    }
     float gZt = (GZ ? AZ[b][r] + pg[st][h][r] : AZ[b][r]) + q[r];
     // + d/dZ_k of cz_k sum|Z_k|: cz_k sgn(Z_k) is exact, so the fma is phase 5's mul + add
     const float sg = (zk > 0.f ? 1.f : 0.f) - (zk < 0.f ? 1.f : 0.f);
     gZt = __builtin_fmaf(P1.cz, sg, gZt);
     // S'(U) = [U - th > 0] + [-U - th > 0] in {0, 1, 2}, from Z_k = S(U, th); gZt * S' as a
     // sum of selected gZt (exact), d/dth = [-U - th > 0] - [U - th > 0]
-    const float ga = zk > -P1.c ? gZt : 0.f, gb = zk < P1.c ? gZt : 0.f;
+    const float ga = zk > -cth ? gZt : 0.f, gb = zk < cth ? gZt : 0.f;
     const float gU = ga + gb;
-    psz += gb - ga;
-    asm volatile("" : "+v"(psz));
+    if constexpr (ROWP) {
+      pstore(rzk.pk, pso(DLADMM_P_THETA_Z) + wP1.at(r), 16 * b + 4 * g + r, a.n, gb - ga);
+    } else {
+      psz += gb - ga;
+      asm volatile("" : "+v"(psz));
+    }
     AZ[b][r] = gU;  // adjoint of Z_{k-1}
     pin_agpr(AZ[b][r]);
     if constexpr (!(REV_ABL & 16)) bstore_s(rg, vw, wG.at(r), gU);
-    if (r == 3) wG.next();
+    if (r == 3) {
+      wG.next();
+      if constexpr (ROWP) wP1.next();
+    }
   };
   // BK3 of layer k, then (MODE 0) BK1 of layer k - 1, block b row r (phase 6); q = gVar =
   // M_k^T gU_k.  MODE 1: BK3 of layer 0 alone (pv[r][S_P] = T_0).  MODE 2: the prologue, BK1 of
@@ -472,19 +575,28 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
     const float gVar = q[r];
     if constexpr ((REV_ABL & 2) && MODE != 2) { GP[b][r] = gVar; pin_agpr(GP[b][r]); return; }
     auto& pv = pvs_all[set2(b)];
+    const int row = 16 * b + 4 * g + r;  // this lane's row (ROWP partials)
     if constexpr (MODE == 1) {
       if constexpr (kV1) {
         // beta1_0's gradient: BK1(0)'s term (pv) + gVar T_0
         bstore_s(o.GB1K, vo, wB.at(r), pv[r][S_GB1] + gVar * pv[r][S_P]);
         bstore_s(none, vw, wV.at(r), 0.f);
         bstore_s(none, vw, wV.at(r), 0.f);
+      } else if constexpr (ROWP) {
+        // beta1_0's per-row partial: gVar T_0; the other slot stores keep the VM count
+        pstore(o.PK, pso(DLADMM_P_BETA1) + wP2.at(r), row, m, gVar * pv[r][S_P]);
+#pragma unroll
+        for (int i = 1; i < NRS; ++i) bstore_s(none, vw, wV.at(r), 0.f);
       } else {
         psb1 += gVar * pv[r][S_P];
         asm volatile("" : "+v"(psb1));
       }
       bstore_s(rv, vw, wV.at(r), 0.f);  // keeps the row's VM count (rv: no records)
       if constexpr (kAE) bstore_s(rv, vw, wV.at(r) + aeo, 0.f);
-      if (r == 3) { wV.next(); wB.next(); }
+      if (r == 3) {
+        wV.next(); wB.next();
+        if constexpr (ROWP) wP2.next();
+      }
       return;
     } else {
       // pv slot S of row r, or `dflt` for a slot this instantiation does not have
@@ -493,8 +605,16 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
         if constexpr (S < NS) return pv[r][S];
         else return dflt;
       };
-      using S_B1K_t = std::integral_constant<int, kV1 ? S_B1K : NS>;
-      using S_B1J_t = std::integral_constant<int, kV1 ? S_B1J : NS>;
+      using S_B1K_t = std::integral_constant<int, kV1 ? S_B1K : ROWP ? S_RB1K : NS>;
+      using S_B1J_t = std::integral_constant<int, kV1 ? S_B1J : ROWP ? S_RB1J : NS>;
+      using S_B2J_t = std::integral_constant<int, kV1 ? S_B2J : ROWP ? S_RB2J : NS>;
+      using S_B3J_t = std::integral_constant<int, (ROWP && kAE) ? S_RB3J : NS>;
+      using S_SS2_t = std::integral_constant<int, (ROWP && kAE) ? S_RSS2J : NS>;
+      using S_THE_t = std::integral_constant<int, ROWP ? S_RTHE : NS>;
+      const float b2p = pvs(S_B2J_t{}, P.b2);
+      const float b3p = pvs(S_B3J_t{}, P.b3);
+      const float ss2p = pvs(S_SS2_t{}, P.ss2);
+      const float thep = pvs(S_THE_t{}, P.the);
       using S_AE_t = std::integral_constant<int, kAE ? S_AE : NS>;
       using S_GE_t = std::integral_constant<int, COT ? S_GE : NS>;
       using S_GL_t = std::integral_constant<int, COT ? S_GL : NS>;
@@ -513,40 +633,41 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
       (void)gEp;
       float p3 = 0.f, p2 = 0.f, pe = 0.f, ps2 = 0.f, ps2b = 0.f;
       if constexpr (EMODE == EM_V1) {
-        const float b2 = pv[r][S_B2J];
+        const float b2 = b2p;
         const float u = (x - Pv) - b2 * lp;               // main_lena.py:87
-        const float e = shrink(u, P.the);
+        const float e = shrink(u, thep);
         t = (Pv + e) - x;                                 // T_k
         const float gTn = aT + b1 * aL;                   // L_{k-1} = L_{k-2} + b1 T_k (:89)
         p3 = aL * t;
         const float gEt = aE + gTn;
-        const float ga = (u - P.the) > 0.0f ? gEt : 0.f;
-        const float gb = (-u - P.the) > 0.0f ? gEt : 0.f;
+        const float ga = (u - thep) > 0.0f ? gEt : 0.f;
+        const float gb = (-u - thep) > 0.0f ? gEt : 0.f;
         const float gEh = ga + gb;
+        pe = gb - ga;                                     // V2's per-row theta_e
         gP = gTn - gEh;
         p2 = -gEh * lp;
         gLp = aL - b2 * gEh;
       } else if constexpr (EMODE == EM_VVAR) {
         const float ep = pv[r][S_E];
         const float r0 = (Pv + ep) - x;
-        const float vv = lp + P.b2 * r0;                  // main_syn_l1l1_scalar.py:114
-        const float eh = ep - P.ss2 * vv;                 // :115
-        const float e = shrink(eh, P.the);
+        const float vv = lp + b2p * r0;                   // main_syn_l1l1_scalar.py:114
+        const float eh = ep - ss2p * vv;                  // :115
+        const float e = shrink(eh, thep);
         t = (Pv + e) - x;                                 // T_k
-        const float gTn = aT + P.b3 * aL;
+        const float gTn = aT + b3p * aL;
         p3 = aL * t;
         const float gEt = aE + gTn;
         // shrink' = [eh - th > 0] + [-eh - th > 0]: gEt times it as a sum of selected gEt
-        const float ga = (eh - P.the) > 0.0f ? gEt : 0.f;
-        const float gb = (-eh - P.the) > 0.0f ? gEt : 0.f;
+        const float ga = (eh - thep) > 0.0f ? gEt : 0.f;
+        const float gb = (-eh - thep) > 0.0f ? gEt : 0.f;
         const float gEh = ga + gb;
         pe = gb - ga;
-        const float gVV = -P.ss2 * gEh;
+        const float gVV = -ss2p * gEh;
         ps2 = -gEh * vv;
         gLp = aL + gVV;
         p2 = gVV * r0;
-        gP = gTn + P.b2 * gVV;
-        gEp = gEh + P.b2 * gVV;
+        gP = gTn + b2p * gVV;
+        gEp = gEh + b2p * gVV;
       } else {
         const float e = P.ss2 * (x - Pv) - P.ss2b * lp;   // main_syn_lasso_scalar.py:102-103
         t = (Pv + e) - x;
@@ -572,6 +693,16 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
         bstore_s(MODE == 0 ? o.GB1K : none, vo, wB.at(r), pv[r][S_GB1] + gVar * t);
         bstore_s(o.GB1J, vo, wB.at(r), p3);
         bstore_s(o.GB2J, vo, wB.at(r), p2);
+      } else if constexpr (ROWP) {
+        // per-row partials: beta1 of layer k (BK3), then BK1(k-1)'s slots, as the per-layer
+        // kernels group them (BK1's beta3 slot carries V2's beta1 L term)
+        const uint32_t so2 = wP2.at(r);
+        if constexpr (MODE == 0) pstore(o.PK, pso(DLADMM_P_BETA1) + so2, row, m, gVar * t);
+        else bstore_s(none, vw, so2, 0.f);
+        pstore(o.PJ, pso(DLADMM_P_BETA3) + so2, row, m, p3);
+        pstore(o.PJ, pso(DLADMM_P_BETA2) + so2, row, m, p2);
+        pstore(o.PJ, pso(DLADMM_P_THETA_E) + so2, row, m, pe);
+        if constexpr (kAE) pstore(o.PJ, pso(DLADMM_P_SS2) + so2, row, m, ps2);
       } else {
         if constexpr (MODE == 0) {
           psb1 += gVar * t;  // beta1 of layer k: gVar * T_k
@@ -591,7 +722,10 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
       } else {
         asm volatile("" ::"v"(gEp), "v"(lp + b1 * tk));
       }
-      if (r == 3) { wV.next(); wB.next(); }
+      if (r == 3) {
+        wV.next(); wB.next();
+        if constexpr (ROWP) wP2.next();
+      }
     }
   };
 
@@ -633,6 +767,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
     reset2();
     wV.reset();
     wB.reset();
+    wP2.reset();
     constexpr int AHEAD = DEEP ? 2 : 1;   // blocks the operand loads run ahead
     static_for<4 * AHEAD>([&](auto R_) {
       constexpr int q = decltype(R_)::value;
@@ -664,6 +799,8 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
     const int gi = 2 * (K - 1 - k);
     wZ.reset();
     wG.reset();
+    wR1.reset();
+    wP1.reset();
     static_for<NB / 2>([&](auto P_) {
       constexpr int p = decltype(P_)::value;
       f32x4 ca = zero4, cb = zero4;
@@ -689,7 +826,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
                 }
               }
             } else {
-              epi1_row(P1, rg, 2 * p - 2 + h, h, r, h ? qb : qa);
+              epi1_row(P1, rzk, rg, 2 * p - 2 + h, h, r, h ? qb : qa);
               // this row's Z_k slot, for pair p (DEEP: p + 1)
               if constexpr (!DEEP) pre1(rzk, p, h, r);
               else if constexpr (p + 1 < NB / 2) pre1(rzk, p + 1, h, r);
@@ -721,11 +858,12 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   // of G1'(k)'s last pair and then flushes layer k's theta_z partial; pair p > 0 those of pair
   // p - 1 (LAST: BK3 of layer 0 alone).
   auto g2_pass = [&](auto LAST_, int k, const LP2& P, const R2& o, rsrc_t rv, const LP1& P1,
-                     rsrc_t rg) {
+                     const R1& rzk, rsrc_t rg) {
     constexpr bool LAST = decltype(LAST_)::value;
     const int gi = 2 * (K - 1 - k) + 1;
     wV.reset();
     wB.reset();
+    wP2.reset();
     reset2();
     static_for<MB / 2>([&](auto P_) {
       constexpr int p = decltype(P_)::value;
@@ -740,7 +878,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
           constexpr int h = i / 4, r = i % 4;
           if constexpr (rev_rows_at(kb, NB, i)) {
             if constexpr (p == 0) {
-              epi1_row(P1, rg, NB - 2 + h, h, r, h ? qb : qa);
+              epi1_row(P1, rzk, rg, NB - 2 + h, h, r, h ? qb : qa);
               if constexpr (i == 7) {
                 if constexpr (!kV1) flush(k, DLADMM_P_THETA_Z, psz);
                 psz = 0.f;
@@ -777,18 +915,20 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
 
   // ---------------------------------------------------------------- K layers, last to first
   LP1 P1 = lp1(K - 1);
-  g1_pass(std::true_type{}, K - 1, P1, rz(K - 1), rgu(K - 1), lp2(K, K - 1), res2_last(), none);
+  R1 Rk = rz(K - 1);
+  g1_pass(std::true_type{}, K - 1, P1, Rk, rgu(K - 1), lp2(K, K - 1), res2_last(), none);
   for (int k = K - 1; k >= 1; --k) {
     const LP2 P = lp2(k, k - 1);
     const R2 o = res2(k - 1);
     const rsrc_t rv = rvar(k - 1);
-    g2_pass(std::false_type{}, k, P, o, rv, P1, rgu(k));
+    g2_pass(std::false_type{}, k, P, o, rv, P1, Rk, rgu(k));
     P1 = lp1(k - 1);
-    g1_pass(std::false_type{}, k - 1, P1, rz(k - 1), rgu(k - 1), P, o, rv);
+    Rk = rz(k - 1);
+    g1_pass(std::false_type{}, k - 1, P1, Rk, rgu(k - 1), P, o, rv);
   }
   const LP2 P0 = lp2(0, -1);
   const R2 o0 = res2_last();
-  g2_pass(std::true_type{}, 0, P0, o0, none, P1, rgu(0));
+  g2_pass(std::true_type{}, 0, P0, o0, none, P1, Rk, rgu(0));
   // rows of layer 0's last G2' pair
   static_for<8>([&](auto I_) {
     constexpr int i = decltype(I_)::value;
@@ -801,19 +941,19 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int MP, int NP, int EM, bool GZ, bool COT>
+template <int MP, int NP, int EM, bool GZ, bool COT, bool ROWP>
 void launch_rev1(const RevArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((reverse_kernel<MP, NP, EM, GZ, COT>), dim3(grid), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((reverse_kernel<MP, NP, EM, GZ, COT, ROWP>), dim3(grid), dim3(256), 0, s, a);
 }
 
-template <int MP, int NP, int EM>
+// ROWP: per-row parameters (V2 with EM_V1, V3 with EM_VVAR)
+template <int MP, int NP, int EM, bool ROWP = false>
 hipError_t launch_rev(const RevArgs& a, int grid, hipStream_t s) {
-  if (a.has_gz && a.has_cot) launch_rev1<MP, NP, EM, true, true>(a, grid, s);
-  else if (a.has_gz) launch_rev1<MP, NP, EM, true, false>(a, grid, s);
-  else if (a.has_cot) launch_rev1<MP, NP, EM, false, true>(a, grid, s);
-  else launch_rev1<MP, NP, EM, false, false>(a, grid, s);
+  if (a.has_gz && a.has_cot) launch_rev1<MP, NP, EM, true, true, ROWP>(a, grid, s);
+  else if (a.has_gz) launch_rev1<MP, NP, EM, true, false, ROWP>(a, grid, s);
+  else if (a.has_cot) launch_rev1<MP, NP, EM, false, true, ROWP>(a, grid, s);
+  else launch_rev1<MP, NP, EM, false, false, ROWP>(a, grid, s);
   return hipGetLastError();
 }
-
 
 }  // namespace dladmm

@@ -234,14 +234,15 @@ size_t dladmm_bwd_workspace_bytes(const dladmm_bwd_desc* d);
 
 /* Which kernels the backward runs: 1 = one reverse-sweep kernel for every layer's adjoints,
    0 = per-layer kernels, <0 = DLADMM_E_* error.  The reverse sweep runs when ALL of these hold:
-     - variant V4, V5 or V6 (and the newS models built on them);
+     - any variant V1-V6 (and the newS models built on V4 / V5);
      - the forward ran on the fused fp32 path and saved P (fwd.P != NULL, keep_all);
-     - no gE / gL / gT cotangents; gZ is allowed when ld_g == fwd.ld_out and layers <= 128;
-     - fwd.ld_e0 == fwd.ld_l0 == fwd.ld_out;
+     - cotangents (gZ, gE, gL, gT; any subset, any depth) only with ld_g == fwd.ld_out;
+     - fwd.ld_e0 == fwd.ld_l0 == fwd.ld_out; V1: fwd.ld_beta == fwd.ld_out;
      - its 32-bit workspace offsets hold and its workspace, about
        (layers + 1) * MP * NP * 4 + layers * (Rn + 2 * MP) * Bpad * 4 bytes (MP, NP: the
-       instantiation's padded m, n; Rn = NP rounded up to 128; Bpad = batch rounded up to 16),
-       stays under a quarter of the device memory (DLADMM_REV_WS_MAX_MB overrides);
+       instantiation's padded m, n; Rn = NP rounded up to 128; Bpad = batch rounded up to 16;
+       V2 / V3 add 8 * layers * max(MP, NP) * (batch / 16, rounded up to 4) * 4 bytes of per-row
+       partials), stays under a quarter of the device memory (DLADMM_REV_WS_MAX_MB overrides);
      - DLADMM_BWD_REV is not "0".
    dladmm_bwd_workspace_bytes() reports the size of whichever path this returns. */
 int dladmm_bwd_path(const dladmm_bwd_desc* d);

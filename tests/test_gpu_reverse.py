@@ -258,3 +258,37 @@ def test_reverse_v5_tied_step(tied, dl, monkeypatch):
     for k in range(4):
         assert nrel(gs_r[k], gs_p[k]) <= 2e-6, (k, gs_r[k], gs_p[k])
     assert np.all(gs_r[:, 7] != 0.0)  # the ss1 slot (P_S1) is filled
+
+
+def check_equal_row(rev, per, K):
+    """V2 / V3: weight gradients bit for bit; the per-row parameter gradients are the same fp32
+    per-wave partials (row16_sum of the same elements) reduced in the same fixed fp64 order --
+    except BK1 of the last layer, whose per-layer kernel (phase 4, no GEMM) groups a row's terms
+    by 64 columns instead of 16: 2e-6 norm-relative, the bar of the scalar slots above."""
+    assert rev.path == 1 and per.path == 0
+    assert torch.equal(rev.gW, per.gW)
+    gr, gp = rev.g_row.cpu().numpy(), per.g_row.cpu().numpy()
+    assert gr.shape == gp.shape
+    for k in range(K):
+        e = nrel(gr[k], gp[k])
+        assert e <= (2e-6 if k == K - 1 else 1e-12), (k, e)
+
+
+@pytest.mark.parametrize("variant", ["v2", "v3"])
+@pytest.mark.parametrize("shape", [(20, 30, 70, 3), (64, 200, 333, 2), (250, 500, 200, 4),
+                                   (256, 512, 64, 1)])
+@pytest.mark.parametrize("loss", ["fused", "zel"])
+def test_reverse_per_row_params(variant, shape, loss, dl, monkeypatch):
+    """V2 (main_syn_l1l1_ltheta.py) and V3 (main_syn_l1l1_full.py) on the reverse sweep (round
+    4): per-row parameters as row-table operands, per-row gradient partials per (layer, slot,
+    row, 16-column wave) as the per-layer kernels form them."""
+    m, n, B, K = shape
+    which, fused = {"fused": ("", True), "zel": ("ZEL", False)}[loss]
+    rev, per = both_cot(dl, variant, m, n, B, K, 9870 + m, monkeypatch, which, fused)
+    check_equal_row(rev, per, K)
+
+
+@pytest.mark.parametrize("variant", ["v2", "v3"])
+def test_reverse_per_row_headline_shape(variant, dl, monkeypatch):
+    rev, per = both_cot(dl, variant, 256, 512, 4096, 15, 9880, monkeypatch, "", True)
+    check_equal_row(rev, per, 15)
