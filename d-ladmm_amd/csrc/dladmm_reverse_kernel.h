@@ -45,6 +45,9 @@
                    // G2' operand loads, 64 no Var / adjoint-of-E stores
 #endif
 
+#ifndef REV_LOAD_AUX
+#define REV_LOAD_AUX 0  // cache policy of the epilogue operand loads (experiment knob; 2 = nt)
+#endif
 #ifndef REV_SLOTS
 #define REV_SLOTS 4  // weight-ring slots (6 fit the LDS at 256 x 512 beside the AL tables)
 #endif
@@ -444,7 +447,8 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
     bstore_s(r, vpr, soff, row16_sum(v));
   };
   auto ld = [](rsrc_t r, uint32_t voff, uint32_t soff) -> float {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff,
+                                                                         REV_LOAD_AUX));
   };
   auto pre1 = [&](const R1& r, int pair, int h, int rr) {
     const int st = set1(pair);

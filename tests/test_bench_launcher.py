@@ -65,3 +65,36 @@ def test_self_launch_spawns_n_gloo_ranks():
     assert len(lines) == 1, p.stdout
     r = json.loads(lines[0])
     assert r["n_gpus"] == 3 and r["rank_sum"] == 3.0 and r["ranks"] == [0, 1, 2]
+
+
+def test_granted_cores_rules(monkeypatch, tmp_path):
+    """cpu_baseline's thread count: the cgroup quota when set, else OMP_NUM_THREADS, else the
+    affinity -- never more than the affinity."""
+    b = _bench()
+    import builtins
+    real_open = builtins.open
+
+    def fake_open(content):
+        def op(path, *a, **k):
+            if str(path) == "/sys/fs/cgroup/cpu.max":
+                if content is None:
+                    raise OSError("no cgroup")
+                p = tmp_path / "cpu.max"
+                p.write_text(content)
+                return real_open(p, *a, **k)
+            return real_open(path, *a, **k)
+        return op
+
+    aff = len(os.sched_getaffinity(0))
+    monkeypatch.setattr(builtins, "open", fake_open("200000 100000\n"))
+    monkeypatch.delenv("OMP_NUM_THREADS", raising=False)
+    c, how = b.granted_cores()
+    assert c == min(2, aff) and how["rule"] == "cgroup cpu.max quota"
+    monkeypatch.setattr(builtins, "open", fake_open("max 100000\n"))
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    c, how = b.granted_cores()
+    assert c == 1 and how["rule"].startswith("OMP_NUM_THREADS")
+    monkeypatch.setattr(builtins, "open", fake_open(None))
+    monkeypatch.delenv("OMP_NUM_THREADS", raising=False)
+    c, how = b.granted_cores()
+    assert c == aff and how["cgroup_cpu_max"] is None
