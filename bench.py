@@ -351,6 +351,9 @@ def main():
         c_el, c_kern, _, c_obj = timed(w2, "f32")
         cfg2 = dict(value=10000 * a.steps / c_el, ms_per_step=c_el / a.steps * 1e3, kern=c_kern,
                     obj=float(c_obj.cpu().numpy()[-1]))
+        if not a.no_split:   # the same batch on the split-f16 kernel (same fp32 tolerances)
+            s_el, s_kern, _, _ = timed(w2, "f32_split")
+            cfg2["split"] = (10000 * a.steps / s_el, s_el / a.steps * 1e3, s_kern, w2.path)
         del w2
     # BASELINE configs 4 (V6 LASSO m=512 n=2048 K=40, per-layer kernels) and 5 (bf16 operands,
     # m=1024 n=4096 K=15, 16,384 columns = its 131,072 over 8 GPUs) at N = 1
@@ -486,6 +489,14 @@ def main():
                         "(DESIGN.md section 12)",
                 "objective_last_layer": cfg2["obj"],
             }
+            if "split" in cfg2:
+                sv, sms, sk, spath = cfg2["split"]
+                res["cfg2"]["split_f16"] = {
+                    "value": sv, "ms_per_step": sms, "kernel_ms": sk * 1e3,
+                    "path": {4: "fused-split-f16"}.get(spath, spath),
+                    "roofline_frac_f16_over_3": f2 / sk / (PEAK_BF16_MFMA / 3),
+                    "note": "same workload, fp32 GEMMs as three exactly split f16 MFMA products "
+                            "(the split_f16 line above; fp32 parity tolerances)"}
         for name, c in cfg45.items():
             m_, n_, K_, B_ = c["shape"]
             fl = (4 * K_ + 2) * m_ * n_ * B_
