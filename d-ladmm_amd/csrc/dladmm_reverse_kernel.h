@@ -46,7 +46,8 @@
 #endif
 
 #ifndef REV_LOAD_AUX
-#define REV_LOAD_AUX 0  // cache policy of the epilogue operand loads (experiment knob; 2 = nt)
+#define REV_LOAD_AUX 2  // cache policy of the epilogue operand loads: nt (read once; 7.42 vs
+                        // 7.50 ms backward with the default policy, profiles/r04_rev_loadaux_ab.json)
 #endif
 #ifndef REV_SLOTS
 #define REV_SLOTS 4  // weight-ring slots (6 fit the LDS at 256 x 512 beside the AL tables)
