@@ -5,12 +5,15 @@
 #   3. PMC pass: WRITE_SIZE        -> gpurun_out/prof/pmc_write
 #   4. PMC pass: MFMA/VALU busy + GRBM_GUI_ACTIVE (clock) -> gpurun_out/prof/pmc_sq
 # Each pass has its own time limit; the script stops at the first failing pass.
+# The profiled bench runs the headline workload alone (--no-cfg3 --no-split: bench.py's default
+# line also launches the same fused kernel for configs 2 and 3, which would mix three grid sizes
+# into rocprofv3's per-kernel-name --stats average); BENCH_ARGS replaces that selection.
 set -u
 cd /tmp && export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-/root/repo}
 OUT=$R/gpurun_out/prof
 mkdir -p $OUT
-BENCH="$R/bench.py --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
+BENCH="$R/bench.py --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline ${BENCH_ARGS---no-cfg3 --no-split}"
 run() {
   local name=$1; shift
   echo "[profile] $name" | tee -a $OUT/steps.log
