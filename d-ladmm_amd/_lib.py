@@ -27,7 +27,8 @@ P_BETA1, P_BETA2, P_BETA3, P_SS2, P_SS2B, P_THETA_E, P_THETA_Z, P_S1 = range(8)
 # every symbol include/dladmm.h declares (checked by tests/test_capi.py)
 EXPORTED = ("dladmm_abi_version", "dladmm_fwd_workspace_bytes", "dladmm_fwd_path",
             "dladmm_fwd_f32", "dladmm_bwd_workspace_bytes", "dladmm_bwd_path", "dladmm_bwd_f32",
-            "dladmm_safeguard_f32", "dladmm_colobj_f32", "dladmm_error_string")
+            "dladmm_safeguard_f32", "dladmm_colobj_f32", "dladmm_lena_workspace_bytes",
+            "dladmm_lena_f32", "dladmm_error_string")
 # enum dladmm_mu_updater
 MU_NONE, MU_EMA, MU_GS, MU_RT = 0, 1, 2, 3
 
@@ -105,6 +106,21 @@ class ColObjDesc(ctypes.Structure):
     ]
 
 
+class LenaDesc(ctypes.Structure):
+    """Mirror of `struct dladmm_lena_desc` (include/dladmm.h)."""
+    _fields_ = [
+        ("abi_version", _i32), ("m", _i32), ("n", _i32), ("batch", _i32), ("layers", _i32),
+        ("mode", _i32), ("alpha", ctypes.c_float), ("inv_mb", ctypes.c_float),
+        ("inv_nb", ctypes.c_float), ("pad0", _i32),
+        ("X", _fp), ("ld_x", _i64), ("A", _fp), ("ld_a", _i64),
+        ("E", _fp), ("L", _fp), ("layer_stride", _i64), ("ld", _i64),
+        ("sums", _fp),
+        ("gE", _fp), ("gL", _fp), ("g_layer_stride", _i64), ("ld_g", _i64),
+        ("coef", _fp),
+        ("workspace", _fp), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
 _LIB = None
 
 
@@ -137,6 +153,10 @@ def lib():
     L.dladmm_safeguard_f32.argtypes = [ctypes.POINTER(SafeguardDesc), ctypes.c_void_p]
     L.dladmm_colobj_f32.restype = ctypes.c_int
     L.dladmm_colobj_f32.argtypes = [ctypes.POINTER(ColObjDesc), ctypes.c_void_p]
+    L.dladmm_lena_workspace_bytes.restype = ctypes.c_size_t
+    L.dladmm_lena_workspace_bytes.argtypes = [ctypes.POINTER(LenaDesc)]
+    L.dladmm_lena_f32.restype = ctypes.c_int
+    L.dladmm_lena_f32.argtypes = [ctypes.POINTER(LenaDesc), ctypes.c_void_p]
     L.dladmm_error_string.restype = ctypes.c_char_p
     L.dladmm_error_string.argtypes = [ctypes.c_int]
     if L.dladmm_abi_version() != ABI_VERSION:

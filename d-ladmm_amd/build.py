@@ -18,7 +18,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 UNITS = ("dladmm_capi.hip", "dladmm_fused.hip", "dladmm_fused_savep.hip", "dladmm_fused_x3.hip",
          "dladmm_layered.hip", "dladmm_backward.hip", "dladmm_lskm.hip", "dladmm_eval.hip",
-         "dladmm_tile_bf16.hip", "dladmm_reverse.hip",
+         "dladmm_tile_bf16.hip", "dladmm_reverse.hip", "dladmm_lena.hip",
          # reverse-sweep instantiations: one unit per E-step form and shape group (minutes each)
          "dladmm_reverse_vvar.hip", "dladmm_reverse_v1.hip", "dladmm_reverse_lasso.hip",
          "dladmm_reverse_vvar_small.hip", "dladmm_reverse_v1_small.hip",

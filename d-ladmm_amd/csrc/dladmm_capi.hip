@@ -1216,9 +1216,91 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
   return 0;
 }
 
+// ---- fused main_lena.py objective (dladmm_lena.hip)
+struct LenaPlan {
+  int shape, MP, NP, tiles, ldl;
+  size_t off_ap, off_atp, off_part, total;
+};
+
+inline int lena_plan(const dladmm_lena_desc* d, LenaPlan* p) {
+  *p = LenaPlan{};
+  if (!d) return DLADMM_E_NULL;
+  if (d->abi_version != DLADMM_ABI_VERSION) return DLADMM_E_ABI_VERSION;
+  if (d->m < 1 || d->n < 1 || d->batch < 1) return DLADMM_E_SHAPE;
+  if (d->layers < 1 || d->layers > 65535) return DLADMM_E_LAYERS;  // grid.y
+  if (d->mode != 0 && d->mode != 1) return DLADMM_E_UNSUPPORTED;
+  if (!d->X || !d->A || !d->E || !d->L) return DLADMM_E_NULL;
+  if (d->mode == 0 && !d->sums) return DLADMM_E_NULL;
+  if (d->mode == 1 && (!d->gE || !d->gL || !d->coef)) return DLADMM_E_NULL;
+  const int64_t B = d->batch;
+  if (d->ld < B || d->ld_x < B || d->ld_a < d->n) return DLADMM_E_SHAPE;
+  if (d->layers > 1 && d->layer_stride < (int64_t)d->m * d->ld) return DLADMM_E_SHAPE;
+  if (d->mode == 1) {
+    if (d->ld_g < B) return DLADMM_E_SHAPE;
+    if (d->layers > 1 && d->g_layer_stride < (int64_t)d->m * d->ld_g) return DLADMM_E_SHAPE;
+  }
+  const int64_t lim = (int64_t)1 << 31;  // 32-bit buffer offsets per layer
+  if ((int64_t)d->m * d->ld * 4 >= lim || (int64_t)d->m * d->ld_x * 4 >= lim ||
+      (d->mode == 1 && (int64_t)d->m * d->ld_g * 4 >= lim))
+    return DLADMM_E_UNSUPPORTED;
+  const int s = pick_shape(d->m, d->n);
+  if (s < 0) return DLADMM_E_UNSUPPORTED;
+  p->shape = s;
+  p->MP = kShapeMP[s];
+  p->NP = kShapeNP[s];
+  p->tiles = ceil_div(d->batch, kTileCols);
+  p->ldl = p->tiles * kTileCols;
+  const size_t fb = (size_t)p->MP * p->NP * sizeof(float);
+  p->off_ap = 0;
+  p->off_atp = align256(fb);
+  p->off_part = p->off_atp + align256(fb);
+  p->total = p->off_part +
+             (d->mode == 0 ? align256((size_t)4 * d->layers * p->ldl * sizeof(float)) : 0);
+  return 0;
+}
+
 }  // namespace dladmm
 
 extern "C" {
+
+size_t dladmm_lena_workspace_bytes(const dladmm_lena_desc* d) {
+  using namespace dladmm;
+  LenaPlan p;
+  return lena_plan(d, &p) ? 0 : p.total;
+}
+
+int dladmm_lena_f32(const dladmm_lena_desc* d, void* stream) {
+  using namespace dladmm;
+  LenaPlan p;
+  if (int e = lena_plan(d, &p)) return e;
+  if (!d->workspace || d->workspace_bytes < p.total) return DLADMM_E_WORKSPACE;
+  if (((uintptr_t)d->workspace) & 255) return DLADMM_E_ALIGN;
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)d->workspace;
+  float* Ap = (float*)(ws + p.off_ap);
+  float* Atp = (float*)(ws + p.off_atp);
+  const int MB = p.MP / 16, NB = p.NP / 16;
+  const float* asrc[1] = {d->A};
+  if (hipError_t e = pack(asrc, 1, d->m, d->n, d->ld_a, MB, NB, 2, Ap, s)) return (int)e;
+  if (hipError_t e = pack(asrc, 1, d->n, d->m, d->ld_a, NB, MB, 2, Atp, s, 1.0f, nullptr, 1))
+    return (int)e;
+  LenaArgs a{};
+  a.m = d->m; a.n = d->n; a.B = d->batch; a.K = d->layers; a.mode = d->mode; a.ldl = p.ldl;
+  a.alpha = d->alpha; a.inv_mb = d->inv_mb; a.inv_nb = d->inv_nb;
+  a.X = d->X; a.ldx = d->ld_x;
+  a.E = d->E; a.L = d->L; a.ls = d->layer_stride; a.ld = d->ld;
+  a.Ap = Ap; a.Atp = Atp;
+  a.part = (float*)(ws + p.off_part);
+  a.gE = d->gE; a.gL = d->gL; a.gls = d->g_layer_stride; a.ldg = d->ld_g;
+  a.coef = d->coef;
+  if (hipError_t e = launch_lena(p.shape, a, p.tiles, s)) return (int)e;
+  if (d->mode == 0) {
+    hipLaunchKernelGGL(loss_reduce_kernel, dim3((unsigned)(4 * d->layers)), dim3(1024), 0, s,
+                       (const float*)a.part, p.ldl, d->sums);
+    if (hipError_t e = hipGetLastError()) return (int)e;
+  }
+  return 0;
+}
 
 int dladmm_abi_version(void) { return DLADMM_ABI_VERSION; }
 

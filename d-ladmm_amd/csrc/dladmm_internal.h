@@ -209,6 +209,23 @@ struct RevArgs {
 static_assert(sizeof(RevArgs) <= 2048, "kernel argument size");
 bool reverse_supports(int variant);
 hipError_t launch_reverse_shape(int shape, int variant, const RevArgs& a, int grid, hipStream_t s);
+// fused main_lena.py objective (dladmm_lena.hip, dladmm_lena_f32): one workgroup per 64 columns
+// of one layer (grid tiles x K); mode 0 = per-column partial sums part[K][4][ldl], mode 1 = the
+// cotangents gE / gL
+struct LenaArgs {
+  int m, n, B, K, mode, ldl;
+  float alpha, inv_mb, inv_nb;
+  int pad0;
+  const float* X; int64_t ldx;
+  const float* E; const float* L; int64_t ls, ld;  // layer k at + k*ls, row stride ld
+  const float* Ap;   // packed A   [MB/2][NB][2] fragments (the forward's G2 order)
+  const float* Atp;  // packed A^T [NB/2][MB][2] fragments
+  float* part;
+  float* gE; float* gL; int64_t gls, ldg;
+  const float* coef;  // mode 1: [K]
+};
+hipError_t launch_lena(int shape, const LenaArgs& a, int grid, hipStream_t s);
+
 hipError_t launch_wgrad_reduce(const float* part, int nchunks, int n, int m, const float* scal,
                                int k, int accumulate, float* gW, int64_t ldgw, hipStream_t s,
                                const float* Wd = nullptr, int64_t ldwd = 0,

@@ -34,7 +34,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .ops import ForwardResult, dladmm_backward, dladmm_forward
+from .ops import ForwardResult, dladmm_backward, dladmm_forward, dladmm_lena
 
 
 def _dev(t: torch.Tensor) -> torch.Tensor:
@@ -187,7 +187,12 @@ class _DLADMMBase(nn.Module):
         """The reference training objective as one fused, differentiable op:
             total = sum_k coeffs[k] * (alpha * sum(|Z_k|,0).mean() + sum(|X - A Z_k|,0).mean())
         (main_syn_l1l1_scalar.py:283-296; kind='lasso': 0.5*sum((X - A Z_k)^2,0), lasso
-        :270-283).  coeffs default: all 1; the reference uses decay 0.6**epoch for k < K-1.
+        :270-283; kind='lena': main_lena.py:221-228,
+            l_k = alpha*mean|Z_k| + mean|E_k| + mean(dual_gap(A^T L_k, alpha))
+                  + mean(dual_gap(L_k, 1)) + mean(L_k * X),
+        dual_gap(x, c) = softplus(x - c) + softplus(-x - c) (:145-147), the means over all
+        elements; m <= 256, n <= 512).  coeffs default: all 1; the reference uses decay
+        0.6**epoch for k < K-1.
         Returns (total, per-layer losses [K]); call total.backward() as the reference does.
         Mathematically the same gradients as building the loss from forward()'s outputs with
         torch ops, without the K products A Z_k.
@@ -201,7 +206,7 @@ class _DLADMMBase(nn.Module):
         coeffs = [1.0] * K if coeffs is None else [float(c) for c in coeffs]
         if len(coeffs) != K:
             raise ValueError(f"dladmm: coeffs must have {K} entries")
-        if kind not in ("l1l1", "lasso"):
+        if kind not in ("l1l1", "lasso", "lena"):
             raise ValueError(f"dladmm: unknown loss kind {kind!r}")
         if cols is not None:
             cols = (int(cols[0]), int(cols[1]))
@@ -212,6 +217,11 @@ class _DLADMMBase(nn.Module):
                 raise ValueError(f"dladmm: cols {cols} do not match x {tuple(x.shape)} and the "
                                  f"model's batch of {self.Z0.shape[1]} columns")
         denom = float(batch if batch is not None else x.shape[1])
+        if kind == "lena":
+            if x.requires_grad:
+                raise RuntimeError("dladmm: gradients w.r.t. the input X are not supported")
+            return _DLADMMLenaLossFunction.apply(self, x, coeffs, float(alpha), denom, cols,
+                                                 *self.parameters())
         if self._needs_grad():
             if x.requires_grad:
                 raise RuntimeError("dladmm: gradients w.r.t. the input X are not supported")
@@ -416,6 +426,63 @@ class _DLADMMLossFunction(torch.autograd.Function):
         grads = mod._param_grads(res, K, reach, ctx.cols)
         names = [n for n, _ in mod.named_parameters()]
         return (None,) * 7 + tuple(grads.get(n) for n in names)
+
+
+class _DLADMMLenaLossFunction(torch.autograd.Function):
+    """main_lena.py's training objective (:221-228; dual_gap :145-147) as one differentiable op:
+        total = sum_k coeffs[k] * (alpha mean|Z_k| + mean|E_k| + mean dual_gap(A^T L_k, alpha)
+                                   + mean dual_gap(L_k, 1) + mean(L_k X)).
+    Forward: the fused K-layer kernel (its sum|Z_k| partials) + dladmm_lena_f32 mode 0 (the
+    other four sums; A^T L_k is formed and reduced in registers, never stored).  Backward:
+    dladmm_lena_f32 mode 1 writes the E_k / L_k cotangents (the product A S_k of the dual_gap
+    term included) and dladmm_bwd_f32 takes them, with alpha mean|Z_k| as its fused |Z| term --
+    the reverse sweep where the shape has it.  The reference instead forms the K products
+    A^T L_k and a dozen elementwise passes over them with torch ops, and autograd as many more.
+    Outputs: total (0-dim) and the per-layer losses [K] (non-differentiable)."""
+
+    @staticmethod
+    def forward(ctx, mod, x, coeffs, alpha, denom, cols, *params):
+        dev = mod.A.device
+        tables = mod._tables(dev, cols)
+        W = [w.detach() for w in mod._weights()]
+        Z0, E0, L0 = mod._init_state(cols)
+        r = dladmm_forward(mod.VARIANT, x, mod.A, W, Z0, E0, L0, keep_all=True, want_T=True,
+                           loss_kind=_lib.LOSS_L1L1, want_P=True, **tables)
+        m, n = mod.A.shape
+        sums = dladmm_lena(x, mod.A, r.E, r.L, alpha, denom)  # fp64 (K, 4)
+        per_layer = (alpha * r.loss_sums[:, 0] / n + sums[:, 1] / n +
+                     (sums[:, 0] + sums[:, 2] + sums[:, 3]) / m) / denom
+        c = _coef_tensor(coeffs, dev)
+        total = (c * per_layer).sum().to(torch.float32)
+        ctx.mod, ctx.tables, ctx.W, ctx.cols = mod, tables, W, cols
+        ctx.alpha, ctx.denom = alpha, denom
+        ctx.c = c.to(torch.float32)
+        ctx.save_for_backward(x, r.Z, r.E, r.L, r.T, r.P)
+        per_layer = per_layer.to(torch.float32)
+        ctx.mark_non_differentiable(per_layer)
+        return total, per_layer
+
+    @staticmethod
+    def backward(ctx, g_total, g_layers):
+        x, Z, E, L, T, P = ctx.saved_tensors
+        mod = ctx.mod
+        K = mod.layers
+        m, n = mod.A.shape
+        ck = (ctx.c * g_total).contiguous()                     # device-side, no host sync
+        gE, gL = dladmm_lena(x, mod.A, E, L, ctx.alpha, ctx.denom, coef=ck)
+        # alpha mean|Z_k| as the backward's fused |Z| term; no fit term
+        coef = torch.stack([ck * (ctx.alpha / (n * ctx.denom)), torch.zeros_like(ck)],
+                           1).contiguous()
+        Z0, E0, L0 = mod._init_state(ctx.cols)
+        res = dladmm_backward(mod.VARIANT, x, mod.A, ctx.W, Z0, E0, L0,
+                              ForwardResult(Z, E, L, T, None, P=P),
+                              gE=[gE[k] for k in range(K)], gL=[gL[k] for k in range(K)],
+                              loss_kind=_lib.LOSS_L1L1, loss_coef=coef,
+                              tied=mod._shared_weight(), **ctx.tables)
+        reach = {"z": [True] * K, "e": [True] * K, "l": [True] * K}
+        grads = mod._param_grads(res, K, reach, ctx.cols)
+        names = [n_ for n_, _ in mod.named_parameters()]
+        return (None,) * 6 + tuple(grads.get(n_) for n_ in names)
 
 
 def _reachable(K: int, g, has_t: bool) -> dict:

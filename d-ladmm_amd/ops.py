@@ -308,6 +308,58 @@ def dladmm_backward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[
     return BackwardResult(gWo, g_scalar, g_row, g1, g2, path)
 
 
+def dladmm_lena(X: torch.Tensor, A: torch.Tensor, E: torch.Tensor, L: torch.Tensor, alpha: float,
+                denom: float, coef: Optional[torch.Tensor] = None):
+    """The fused main_lena.py objective terms over a forward's saved E_k, L_k ((K, m, B) each;
+    main_lena.py:221-228 with dual_gap :145-147) through `dladmm_lena_f32` (include/dladmm.h,
+    csrc/dladmm_lena.hip).  coef None (mode 0): returns the fp64 (K, 4) sums
+    [sum|E_k|, sum dual_gap(A^T L_k, alpha), sum dual_gap(L_k, 1), sum L_k X].  coef = device
+    fp32 (K,) (mode 1): returns the cotangents (gE, gL), each (K, m, B), of
+    sum_k coef[k] * (mean|E_k| + mean dual_gap(A^T L_k, alpha) + mean dual_gap(L_k, 1)
+    + mean(L_k X)), the means over m*denom (n*denom for A^T L_k) elements."""
+    Lb = _lib.lib()
+    K, m, B = L.shape
+    n = A.shape[1]
+    dev = X.device
+    for t in (E, L):
+        if tuple(t.shape) != (K, m, B) or t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("dladmm: E and L must be contiguous fp32 (K, m, B) tensors")
+    X = X.contiguous()
+    A = A.contiguous()
+    d = _lib.LenaDesc()
+    d.abi_version = _lib.ABI_VERSION
+    d.m, d.n, d.batch, d.layers = m, n, B, K
+    d.alpha = float(alpha)
+    d.inv_mb, d.inv_nb = 1.0 / (m * float(denom)), 1.0 / (n * float(denom))
+    d.X, d.ld_x = X.data_ptr(), X.stride(0)
+    d.A, d.ld_a = A.data_ptr(), A.stride(0)
+    d.E, d.L, d.layer_stride, d.ld = E.data_ptr(), L.data_ptr(), m * B, B
+    out = None
+    if coef is None:
+        d.mode = 0
+        out = torch.empty((K, 4), device=dev, dtype=torch.float64)
+        d.sums = out.data_ptr()
+    else:
+        if tuple(coef.shape) != (K,) or coef.dtype != torch.float32 or coef.device != dev:
+            raise ValueError("dladmm: coef must be an fp32 (K,) device tensor")
+        coef = coef.contiguous()
+        d.mode = 1
+        gE = torch.empty((K, m, B), device=dev, dtype=torch.float32)
+        gL = torch.empty((K, m, B), device=dev, dtype=torch.float32)
+        d.gE, d.gL, d.g_layer_stride, d.ld_g = gE.data_ptr(), gL.data_ptr(), m * B, B
+        d.coef = coef.data_ptr()
+        out = (gE, gL)
+    wsb = Lb.dladmm_lena_workspace_bytes(ctypes.byref(d))
+    if wsb == 0:
+        raise ValueError(f"dladmm: the fused main_lena objective supports m <= 256, n <= 512 "
+                         f"(got m={m}, n={n}, K={K}, B={B})")
+    ws = _workspace(dev, wsb)
+    d.workspace, d.workspace_bytes = ws.data_ptr(), wsb
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _lib.check(Lb.dladmm_lena_f32(ctypes.byref(d), ctypes.c_void_p(stream)))
+    return out
+
+
 _WS: "OrderedDict" = None
 _WS_PER_DEVICE = 4   # streams whose workspace stays cached per device (least recently used out)
 

@@ -313,6 +313,44 @@ typedef struct dladmm_colobj_desc {
 
 int dladmm_colobj_f32(const dladmm_colobj_desc* d, void* stream);
 
+/*
+ * Fused main_lena.py training objective over a forward's saved layers (SURVEY.md section 8 rows
+ * a11 / f1; main_lena.py:221-228, dual_gap :145-147), for any variant:
+ *   l_k = alpha/(n N) sum|Z_k| + 1/(m N) sum|E_k| + 1/(n N) sum dual_gap(A^T L_k, alpha)
+ *         + 1/(m N) sum dual_gap(L_k, 1) + 1/(m N) sum L_k * X,
+ *   dual_gap(x, c) = softplus(x - c) + softplus(-x - c)   (torch softplus: beta 1, threshold 20),
+ * N = the batch of the mean (a data-parallel shard passes the global batch).  The sum|Z_k| term is
+ * the forward's own loss_sums[k*2+0] (loss_kind DLADMM_LOSS_L1L1); this call forms the other four
+ * without storing A^T L_k:
+ *   mode 0: sums[k*4 + t] (fp64, fixed order): t = 0 sum|E_k|, 1 sum dual_gap(A^T L_k, alpha)
+ *           (rows < n), 2 sum dual_gap(L_k, 1), 3 sum L_k * X;
+ *   mode 1: the cotangents of coef[k] * those terms with their means, i.e. for inv_mb = 1/(m N),
+ *           inv_nb = 1/(n N):  gE_k = coef[k] inv_mb sgn(E_k),
+ *           gL_k = coef[k] inv_nb A S_k + coef[k] inv_mb (softplus'(L_k - 1) - softplus'(-L_k - 1)
+ *           + X),  S_k = softplus'(A^T L_k - alpha) - softplus'(-A^T L_k - alpha)
+ *           -- what a dladmm_bwd_f32 call then takes as its gE / gL cotangents.
+ * E_k and L_k (m x batch) sit at E + k*layer_stride (row stride ld), likewise the outputs (gE, gL
+ * at + k*g_layer_stride, row stride ld_g).  coef: device [layers] (mode 1).  Shapes: m <= 256 and
+ * n <= 512 (the fused forward's register-resident shapes); otherwise DLADMM_E_UNSUPPORTED.
+ */
+typedef struct dladmm_lena_desc {
+  int32_t abi_version;
+  int32_t m, n, batch, layers;
+  int32_t mode;
+  float alpha, inv_mb, inv_nb;
+  int32_t pad0;
+  const float* X; int64_t ld_x;
+  const float* A; int64_t ld_a;
+  const float* E; const float* L; int64_t layer_stride; int64_t ld;
+  double* sums;                                   /* mode 0: [layers][4] */
+  float* gE; float* gL; int64_t g_layer_stride; int64_t ld_g;   /* mode 1 */
+  const float* coef;                              /* mode 1: device [layers] */
+  void* workspace; size_t workspace_bytes;
+} dladmm_lena_desc;
+
+size_t dladmm_lena_workspace_bytes(const dladmm_lena_desc* d);
+int dladmm_lena_f32(const dladmm_lena_desc* d, void* stream);
+
 /* Text for a return code of this library (DLADMM_E_* or hipError_t). */
 const char* dladmm_error_string(int code);
 

@@ -1,0 +1,166 @@
+"""The fused main_lena.py training objective (net.training_loss(kind="lena"): the fused K-layer
+forward + dladmm_lena_f32 + dladmm_bwd_f32 with E / L cotangents) against the same objective built
+with torch ops, main_lena.py:221-228 with dual_gap of :145-147:
+
+  * in fp64 on the CPU over the reference-op restatement (oracle/dladmm_torch_cpu.py, pinned to
+    the reference classes by tests/test_oracle_torch.py) with torch autograd -- the reference;
+  * in fp32 on the GPU over this package's differentiable forward (the reference training loop
+    unchanged: torch ops on the returned Z_k, E_k, L_k).
+
+Bar: loss values within 1e-5 (norm-relative, per layer) of fp64; every parameter gradient within
+max(GTOL, 3 x the torch-op GPU path's own distance to fp64) -- the GTOL of tests/test_gpu_backward.py
+(GEMM summation order and near-threshold shrink masks move fp32 gradients by more than rounding).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import problems as P
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "oracle"))
+import dladmm_torch_cpu as TC  # noqa: E402
+
+GTOL = 1e-4
+ALPHA = 0.45  # main_lena.py's alpha
+
+
+def nrel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    nb = np.linalg.norm(b)
+    return float(np.linalg.norm(a - b) / nb) if nb > 0 else float(np.linalg.norm(a))
+
+
+def dual_gap(x, a):  # main_lena.py:145-147
+    return torch.nn.functional.softplus(x - a) + torch.nn.functional.softplus(-x - a)
+
+
+def lena_losses(Z, E, L, X, A, alpha, K):
+    """main_lena.py:221-228, one entry per layer."""
+    return [alpha * torch.mean(torch.abs(Z[k])) + torch.mean(torch.abs(E[k])) +
+            torch.mean(dual_gap(torch.mm(A.t(), L[k]), alpha)) +
+            torch.mean(dual_gap(L[k], 1)) + torch.mean(L[k] * X) for k in range(K)]
+
+
+def build(dl, defn, K):
+    d = dict(defn, K=K)
+    inp, sd = P.build_problem(d)
+    m, n = inp["A"].shape
+    B = inp["X"].shape[1]
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+    net = dl.VARIANTS[d["variant"]](m=m, n=0, d=n, batch_size=B, A=t(inp["A"]),
+                                    Z0=t(inp["Z0"]), E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K)
+    net.load_state_dict({k: t(v) for k, v in sd.items()}, strict=True)
+    return net.cuda(), inp, sd
+
+
+def fp64_reference(variant, inp, sd, K, coeffs):
+    d64 = lambda a: torch.from_numpy(np.asarray(a, np.float64))  # noqa: E731
+    params = {k: d64(v).requires_grad_(True) for k, v in sd.items()}
+    X, A = d64(inp["X"]), d64(inp["A"])
+    fwd = getattr(TC.forward, "__wrapped__", TC.forward)  # the restatement without no_grad
+    with torch.enable_grad():
+        out = fwd(variant, X, A, d64(inp["Z0"]), d64(inp["E0"]), d64(inp["L0"]), params, K)
+        per = lena_losses(out[0], out[1], out[2], X, A, ALPHA, K)
+        tot = sum(c * l for c, l in zip(coeffs, per))
+        tot.backward()
+    return float(tot), [float(v) for v in per], {k: p.grad.numpy() for k, p in params.items()}
+
+
+CASES = [
+    ("v1_small_pert", 3),     # shape (32, 32), B = 8
+    ("v1_lena_cfg1", 5),      # BASELINE config 1: main_lena.py's shape (64 x 256), B = 20
+    ("v1_med_w04", 3),        # config-2 shape (256 x 512), B = 12
+    ("v4_med_pert", 3),       # the objective on another variant (any variant takes it)
+    ("v2_ragged", 3),         # m = 30, n = 70, B = 5
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,K", CASES, ids=[c[0] for c in CASES])
+def test_lena_loss_and_grads_vs_fp64(dl, name, K):
+    defn = P.FIXTURES[name]
+    coeffs = [0.6 if k < K - 1 else 1.0 for k in range(K)]
+    net, inp, sd = build(dl, defn, K)
+    net.requires_grad_(True)
+    X = torch.from_numpy(inp["X"]).cuda()
+    A = torch.from_numpy(inp["A"]).cuda()
+    # fused
+    tot_f, per_f = net.training_loss(X, ALPHA, coeffs, kind="lena")
+    tot_f.backward()
+    g_f = {k: p.grad.detach().cpu().numpy() for k, p in net.named_parameters()}
+    # torch ops over the differentiable forward (the reference loop unchanged)
+    net.zero_grad(set_to_none=True)
+    out = net(X)
+    per_t = lena_losses(out[0], out[1], out[2], X, A, ALPHA, K)
+    tot_t = sum(c * l for c, l in zip(coeffs, per_t))
+    tot_t.backward()
+    g_t = {k: p.grad.detach().cpu().numpy() for k, p in net.named_parameters()}
+    # fp64 reference
+    tot64, per64, g64 = fp64_reference(defn["variant"], inp, sd, K, coeffs)
+
+    assert abs(float(tot_f) - tot64) <= 1e-5 * abs(tot64), (float(tot_f), tot64)
+    assert nrel(per_f.detach().cpu().numpy(), per64) <= 1e-5
+    worst = []
+    for k, g in g64.items():
+        if not np.any(g):
+            continue
+        ef, et = nrel(g_f[k], g), nrel(g_t[k], g)
+        bar = max(GTOL, 3 * et)
+        worst.append((ef / bar, k, ef, et))
+        assert ef <= bar, (k, ef, et)
+    worst.sort(reverse=True)
+    print(f"{name}: loss {float(tot_f):.8g} vs fp64 {tot64:.8g}; worst grad {worst[0]}")
+
+
+@pytest.mark.gpu
+def test_lena_path_matches_torch_op_path_at_batch(dl):
+    """A larger ragged batch at main_lena.py's shape: fused vs torch-op loss on the GPU."""
+    defn = dict(P.FIXTURES["v1_lena_cfg1"], B=1000, seed=2201, perturb=0.1, wscale=0.4)
+    K = 5
+    coeffs = [1.0] * K
+    net, inp, _ = build(dl, defn, K)
+    net.requires_grad_(True)
+    X = torch.from_numpy(inp["X"]).cuda()
+    A = torch.from_numpy(inp["A"]).cuda()
+    tot_f, per_f = net.training_loss(X, ALPHA, coeffs, kind="lena")
+    tot_f.backward()
+    g_f = {k: p.grad.detach().double() for k, p in net.named_parameters()}
+    net.zero_grad(set_to_none=True)
+    out = net(X)
+    per_t = lena_losses(out[0], out[1], out[2], X, A, ALPHA, K)
+    sum(c * l for c, l in zip(coeffs, per_t)).backward()
+    for k, p in net.named_parameters():
+        g = p.grad.detach().double()
+        e = float((g_f[k] - g).norm() / g.norm().clamp_min(1e-30))
+        assert e <= GTOL, (k, e)
+    pt = torch.stack([v.detach() for v in per_t]).double()
+    assert float((per_f.double() - pt).norm() / pt.norm()) <= 1e-5
+
+
+def test_lena_descriptor_validation(dl):
+    """Host-only: the workspace query rejects what the kernel does not cover (no device work)."""
+    import ctypes
+    from importlib import import_module
+    _lib = import_module("d-ladmm_amd._lib")
+    L = _lib.lib()
+    d = _lib.LenaDesc()
+    d.abi_version = _lib.ABI_VERSION
+    d.m, d.n, d.batch, d.layers, d.mode = 64, 256, 100, 3, 0
+    d.X = d.A = d.E = d.L = d.sums = 16  # non-null placeholders: never dereferenced here
+    d.ld_x = d.ld = 100
+    d.ld_a = 256
+    d.layer_stride = 64 * 100
+    assert L.dladmm_lena_workspace_bytes(ctypes.byref(d)) > 0
+    d.n = 600   # past the register-resident shapes
+    assert L.dladmm_lena_workspace_bytes(ctypes.byref(d)) == 0
+    d.n = 256
+    d.mode = 1  # cotangent outputs missing
+    assert L.dladmm_lena_workspace_bytes(ctypes.byref(d)) == 0
+    d.mode = 0
+    d.ld = 50   # row stride below the batch
+    assert L.dladmm_lena_workspace_bytes(ctypes.byref(d)) == 0

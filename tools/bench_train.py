@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--lena-loss", action="store_true",
                     help="V1 with main_lena.py:221-228's loss (torch ops over the returned Z_k, "
                          "E_k and L_k: cotangents of Z, E and L reach the backward), alpha 0.45")
+    ap.add_argument("--lena-fused", action="store_true",
+                    help="main_lena.py:221-228's loss as net.training_loss(kind='lena') (fused: "
+                         "dladmm_lena_f32 + the reverse sweep with E / L cotangents), alpha 0.45")
     ap.add_argument("--fused-loss", action="store_true",
                     help="net.training_loss (objective fused into the kernels) instead of the "
                          "reference's torch-op loss over the returned Z_k")
@@ -56,9 +59,11 @@ def main():
     net = dl.VARIANTS[a.variant](m=m, n=0, d=n, batch_size=B, A=A, Z0=Z0, E0=E0, L0=L0,
                                  layers=K)
     kind = "lasso" if a.variant == "v6" else "l1l1"
+    if a.lena_fused:
+        a.alpha = 0.45
     if a.lena_loss and a.variant != "v1":
         raise SystemExit("--lena-loss is main_lena.py's (V1)")
-    if not a.fused_loss and not a.lena_loss and a.variant != "v4":
+    if not a.fused_loss and not a.lena_loss and not a.lena_fused and a.variant != "v4":
         raise SystemExit("the torch-op loss leg is V4's (main_syn_l1l1_scalar.py)")
     At = A.t()
 
@@ -72,7 +77,12 @@ def main():
         if timed:
             ev[0].record()
         coeffs = [0.6 if k < K - 1 else 1.0 for k in range(K)]
-        if a.fused_loss:
+        if a.lena_fused:
+            tot, _ = net.training_loss(X, a.alpha, [1.0] * K, "lena")
+            if timed:
+                ev[1].record()
+                ev[2].record()
+        elif a.fused_loss:
             tot, _ = net.training_loss(X, a.alpha, coeffs, kind)
             if timed:
                 ev[1].record()
@@ -123,9 +133,10 @@ def main():
     flop_r = 10 * K * m * n * B      # reference-equivalent (recomputing backward)
     res = {
         "metric": f"training steps/s ({a.variant.upper()} forward + "
-                  f"{'main_lena' if a.lena_loss else kind} loss + backward + Adam)",
+                  f"{'main_lena' if a.lena_loss or a.lena_fused else kind} loss + backward + Adam)",
         "variant": a.variant,
-        "loss_path": ("fused (net.training_loss)" if a.fused_loss else
+        "loss_path": ("main_lena.py:221-228 fused (net.training_loss kind='lena')"
+                      if a.lena_fused else "fused (net.training_loss)" if a.fused_loss else
                       "main_lena.py:221-228 torch ops on Z_k, E_k, L_k" if a.lena_loss else
                       "torch ops on Z_k"),
         "batch": B, "m": m, "n": n, "layers": K,
