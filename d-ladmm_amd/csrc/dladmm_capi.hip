@@ -1,6 +1,7 @@
 // dladmm_capi.hip -- the C ABI of include/dladmm.h: descriptor validation, planning, weight
 // packing, the loss reduction, and dispatch to the fused (dladmm_fused.hip) or per-layer
 // (dladmm_layered.hip) kernels.
+#include <math.h>
 #include <stdlib.h>
 
 #include <vector>
@@ -1287,6 +1288,13 @@ int dladmm_lena_f32(const dladmm_lena_desc* d, void* stream) {
   LenaArgs a{};
   a.m = d->m; a.n = d->n; a.B = d->batch; a.K = d->layers; a.mode = d->mode; a.ldl = p.ldl;
   a.alpha = d->alpha; a.inv_mb = d->inv_mb; a.inv_nb = d->inv_nb;
+  for (int i = 0; i < 2; ++i) {  // dual_gap constants (dladmm_lena.hip)
+    const double c = i == 0 ? (double)d->alpha : 1.0;
+    a.gc[4 * i + 0] = (float)c;
+    a.gc[4 * i + 1] = (float)(1.0 + exp(-2.0 * c));
+    a.gc[4 * i + 2] = (float)exp(-c);
+    a.gc[4 * i + 3] = (float)(exp(c) + exp(-c));
+  }
   a.X = d->X; a.ldx = d->ld_x;
   a.E = d->E; a.L = d->L; a.ls = d->layer_stride; a.ld = d->ld;
   a.Ap = Ap; a.Atp = Atp;

@@ -209,13 +209,13 @@ struct RevArgs {
 static_assert(sizeof(RevArgs) <= 2048, "kernel argument size");
 bool reverse_supports(int variant);
 hipError_t launch_reverse_shape(int shape, int variant, const RevArgs& a, int grid, hipStream_t s);
-// fused main_lena.py objective (dladmm_lena.hip, dladmm_lena_f32): one workgroup per 64 columns
-// of one layer (grid tiles x K); mode 0 = per-column partial sums part[K][4][ldl], mode 1 = the
-// cotangents gE / gL
+// fused main_lena.py objective (dladmm_lena.hip, dladmm_lena_f32): one workgroup per 64 columns,
+// every layer; mode 0 = per-column partial sums part[K][4][ldl], mode 1 = the cotangents gE / gL
 struct LenaArgs {
   int m, n, B, K, mode, ldl;
   float alpha, inv_mb, inv_nb;
   int pad0;
+  float gc[8];  // dual_gap constants (a, 1 + e^-2a, e^-a, e^a + e^-a) for a = alpha, then a = 1
   const float* X; int64_t ldx;
   const float* E; const float* L; int64_t ls, ld;  // layer k at + k*ls, row stride ld
   const float* Ap;   // packed A   [MB/2][NB][2] fragments (the forward's G2 order)

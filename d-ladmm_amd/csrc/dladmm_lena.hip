@@ -6,10 +6,10 @@
 //   dual_gap(x, c) = softplus(x - c) + softplus(-x - c).
 // The reference builds it from the returned E_k, L_k with torch ops: K products A^T L_k (n x B
 // each, 128 MB per layer at B = 65,536) and a dozen elementwise passes over them forward, as many
-// backward plus the products A (d/dY).  Here one launch covers every layer (grid = tiles x K) and
-// A^T L_k never leaves the registers:
-//  * one workgroup = 4 waves = 64 batch columns of one layer; wave w owns 16.  L_k's tile sits in
-//    registers in the C/D layout of v_mfma_f32_16x16x4_f32 (lane l: column l & 15, rows
+// backward plus the products A (d/dY).  Here one launch covers every layer and A^T L_k never
+// leaves the registers:
+//  * one workgroup = 4 waves = 64 batch columns for all K layers; wave w owns 16.  L_k's tile
+//    sits in registers (L_{k+1}'s blocks load as L_k's last reads of them pass) in the C/D layout of v_mfma_f32_16x16x4_f32 (lane l: column l & 15, rows
 //    16 b + 4 (l >> 4) + r), i.e. as the B operand of
 //      G1: Y = A^T L_k     (rows n, contraction m)  -- A^T packed in paired fragment order
 //    whose epilogue either sums dual_gap(Y, a) (mode 0) or keeps S = softplus'(Y - a) -
@@ -20,25 +20,73 @@
 //    scheme, dladmm_fused_kernel.h), two output blocks per MFMA pass;
 //  * mode 0's per-column partial sums go to part[k][t][col], reduced in fp64 in a fixed order by
 //    loss_reduce_kernel (dladmm_capi.hip).
-// softplus / its derivative follow torch's (beta 1, threshold 20): x > 20 ? x : log1p(exp(x)),
-// x > 20 ? 1 : e / (e + 1), e = exp(x).
+// dual_gap and its derivative in closed form (below), to torch's softplus (beta 1, threshold 20)
+// within fp32 precision.
 #include "dladmm_common.h"
 #include "dladmm_internal.h"
 
 namespace dladmm {
 
-// Hardware exp2 / log2 (v_exp_f32, v_log_f32: ~1 ulp): softplus(x) = log(1 + e^x) for x <= 20
-// is within ~1e-7 absolute of torch's log1p form (below e^x < 2^-24 the 1 + e^x rounds to 1 and
-// the value to 0 instead of e^x); its derivative e / (e + 1) keeps full relative accuracy.  The
-// OCML expf / log1pf sequences cost the unrolled G1 epilogue its registers (scratch spills).
+// dual_gap(y, a) = softplus(y - a) + softplus(-y - a) = ln((1 + e^(y-a)) (1 + e^(-y-a)))
+//                 = ln(c1 + c2 (e^y + e^-y)),  c1 = 1 + e^-2a, c2 = e^-a,
+// and its derivative softplus'(y - a) - softplus'(-y - a) = (e^y - e^-y) / (e^y + e^-y + c3),
+// c3 = e^a + e^-a: two transcendentals less per element than the four softplus terms, no
+// cancellation in the log (its argument is >= 1).  Past |y| = 30 they are |y| - a and sgn(y)
+// (what torch's softplus threshold of 20 gives to fp32 precision).  Hardware v_exp_f32 /
+// v_log_f32 / v_rcp_f32 (~1 ulp each): within ~1e-7 of the torch values, relative to the
+// terms' scale; branch-free (selects), so no lane diverges around the transcendental work.
+struct Gap { float a, c1, c2, c3; };
 __device__ __forceinline__ float exp_h(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
-__device__ __forceinline__ float softplus_t(float x) {
-  return x > 20.0f ? x : 0.693147180559945309f * __builtin_amdgcn_logf(1.0f + exp_h(x));
+__device__ __forceinline__ float dual_gap(float y, const Gap& G) {
+  const float e = exp_h(y), ei = __builtin_amdgcn_rcpf(e);
+  float v = 0.693147180559945309f * __builtin_amdgcn_logf(G.c1 + G.c2 * (e + ei));
+  asm("" : "+v"(v));  // computed on every lane: the select below must not become a branch
+  const float ay = fabsf(y);
+  return ay > 30.0f ? ay - G.a : v;
 }
-__device__ __forceinline__ float softplus_d(float x) {
-  const float e = exp_h(x);
-  return x > 20.0f ? 1.0f : e / (e + 1.0f);
+__device__ __forceinline__ float dual_gap_d(float y, const Gap& G) {
+  const float e = exp_h(y), ei = __builtin_amdgcn_rcpf(e);
+  float v = (e - ei) * __builtin_amdgcn_rcpf((e + ei) + G.c3);
+  asm("" : "+v"(v));
+  return fabsf(y) > 30.0f ? copysignf(1.0f, y) : v;
 }
+
+template <int MB, int NB, int CF, int MODE>
+struct LenaWin {
+  static constexpr int SPC = CF / 2;
+  static constexpr int DMAOPS = CF % 16 == 0 ? 4 * (CF / 16) : 1;  // VM ops of one chunk DMA
+  static constexpr int NP1 = NB / 2;                                // G1 pairs
+  static constexpr int T1 = NP1 * MB;
+  static constexpr int pair_of_block(int b) { return NP1 > 1 ? (b * (NP1 - 1)) / MB : 0; }
+  static constexpr int blocks_at(int p) {
+    int c = 0;
+    for (int b = 0; b < MB; ++b) c += pair_of_block(b) == p ? 1 : 0;
+    return c;
+  }
+  static constexpr int ops(int t) {
+    int c = 0;
+    if constexpr (MODE == 0) {
+      const int p = t / MB, j = t % MB;
+      if (j == 0 && NP1 > 1) c += 8 * blocks_at(p);
+      if (p == NP1 - 1) c += 4;
+      if (t == T1 - 1) c += 4;
+    } else {
+      if (t >= T1) {
+        const int u = t - T1, j = u % NB;
+        if (j == 0) c += 16;
+        if (j == NB - 1) c += 24;
+      }
+    }
+    return c;
+  }
+  template <int S>
+  static constexpr int at() {
+    int n = DMAOPS;
+    for (int t = S - 2 * SPC; t < S; ++t)
+      if (t >= 0) n += ops(t);
+    return n < 63 ? n : 63;
+  }
+};
 
 template <int MP, int NP, int MODE>
 __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
@@ -46,23 +94,27 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
   constexpr int GF = MB * NB;                  // fragments per product
   constexpr int CF = GF < 16 ? GF : 16;        // fragments per ring chunk
   constexpr int NCH = GF / CF;                 // chunks per product
+  constexpr int CPL = MODE == 1 ? 2 * NCH : NCH;  // chunks per layer
   constexpr int SLOTS = 4;
+  using Win = LenaWin<MB, NB, CF, MODE>;
+  constexpr int NP1 = NB / 2, T1 = Win::T1;
   static_assert(MB % 2 == 0 && NB % 2 == 0 && GF % CF == 0 && CF % 2 == 0, "shape");
   __shared__ f32x4 ring[SLOTS * CF * 64];
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
-  const int k = blockIdx.y;
+  const int K = a.K;
   const int64_t col = (int64_t)blockIdx.x * kTileCols + w * 16 + (lane & 15);
   const bool cv = col < a.B;
   const int m = a.m, n = a.n;
 
-  // ---- ring: product gi = 0 (A^T, G1), 1 (A, G2); past the end: A again (harmless filler)
+  // ---- ring: per layer A^T (G1) [, A (G2)], layer after layer; past the end: harmless filler
   auto chunk_src = [&](int ch) -> const float* {
-    uint64_t sb = (uint64_t)(ch < NCH ? a.Atp : a.Ap);
+    const int q = ch % CPL;
+    uint64_t sb = (uint64_t)(q < NCH ? a.Atp : a.Ap);
     asm volatile("" : "+s"(sb));
-    return (const float*)sb + (ch % NCH) * CF * kFrag;
+    return (const float*)sb + (q % NCH) * CF * kFrag;
   };
   auto issue = [&](const float* base, int slot) {
     f32x4* dst = ring + slot * (CF * 64);
@@ -71,11 +123,10 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
       for (int i = 0; i < CF / 16; ++i)
         glds16x4(base + (16 * i + 4 * w) * kFrag, lane * 16, dst + (16 * i + 4 * w) * 64);
     } else {
-#pragma unroll
-      for (int i = 0; i < (CF + 3) / 4; ++i) {
-        const int f = i * 4 + w;
-        if (CF % 4 == 0 || f < CF) glds16(base + f * kFrag, lane * 16, dst + f * 64);
-      }
+      // CF < 16 (the 32 x 32 shape): fragment w per wave; waves past CF issue a harmless
+      // duplicate so every wave's VM count is the same
+      const int f = w < CF ? w : 0;
+      glds16(base + f * kFrag, lane * 16, dst + f * 64);
     }
   };
   int cur = 0;
@@ -83,49 +134,30 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
 #pragma unroll
   for (int c = 0; c < SLOTS - 1; ++c) issue(chunk_src(c), c);
 
-  // ---- L_k's tile (rows past m and columns past B read 0)
+  // ---- views (rows past m and columns past B read 0 / are dropped)
   const int64_t ld = a.ld;
   const uint32_t vo = cv ? (uint32_t)((col + (int64_t)(4 * g) * ld) * 4) : kOOB;
   const uint32_t vx = cv ? (uint32_t)((col + (int64_t)(4 * g) * a.ldx) * 4) : kOOB;
   const uint32_t mbytes = (uint32_t)((int64_t)m * ld * 4);
-  const rsrc_t rl = mkrsrc(a.L + (int64_t)k * a.ls, mbytes);
-  const rsrc_t re = mkrsrc(a.E + (int64_t)k * a.ls, mbytes);
   const rsrc_t rx = mkrsrc(a.X, (uint32_t)((int64_t)m * a.ldx * 4));
+  auto lview = [&](int k) { return mkrsrc(k < K ? a.L + (int64_t)k * a.ls : nullptr, k < K ? mbytes : 0u); };
+  auto row_off = [&](int b, int r, int64_t stride) { return (uint32_t)((int64_t)(16 * b + r) * stride * 4); };
   float Lr[MB][4];
+  {
+    const rsrc_t rl = lview(0);
 #pragma unroll
-  for (int b = 0; b < MB; ++b)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      Lr[b][r] = bload(rl, vo + (uint32_t)((int64_t)(16 * b + r) * ld * 4));
-      pin_agpr(Lr[b][r]);
-    }
-
-  // mode 0: the elementwise terms over L_k's rows -- |E_k|, dual_gap(L_k, 1), L_k * X -- one
-  // block at a time (the scheduling barrier keeps the unrolled blocks' loads from piling up)
-  float se = 0.f, sdl = 0.f, slx = 0.f;
-  if constexpr (MODE == 0) {
-#pragma unroll
-    for (int b = 0; b < MB; ++b) {
+    for (int b = 0; b < MB; ++b)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const bool ok = cv && (16 * b + 4 * g + r) < m;
-        const float l = Lr[b][r];
-        const float e = bload(re, vo + (uint32_t)((int64_t)(16 * b + r) * ld * 4));
-        const float x = bload(rx, vx + (uint32_t)((int64_t)(16 * b + r) * a.ldx * 4));
-        se += fabsf(e);
-        sdl += ok ? softplus_t(l - 1.0f) + softplus_t(-l - 1.0f) : 0.f;
-        slx += l * x;
+        Lr[b][r] = bload(rl, vo + row_off(b, r, ld));
+        pin_agpr(Lr[b][r]);
       }
-      __builtin_amdgcn_sched_barrier(0);
-    }
   }
-  ring_barrier();  // the primed chunks landed; every load above is complete
+  ring_barrier();  // the primed chunks landed; L_0 is in
   f32x4 fr[4];
   fr[0] = frag(0, 0);
   fr[1] = frag(0, 1);
-  // step s of the stream (compile time): fragments 2s, 2s+1; the next step's two are read ahead
-  // (at a chunk's last step: ring barrier, the next chunk's first fragments, and the DMA of the
-  // chunk SLOTS - 1 ahead into the slot every wave has finished)
+  int chb = 0;  // stream chunk of the current layer's first chunk
   auto step_head = [&](auto S_) {
     constexpr int s = decltype(S_)::value;
     constexpr int fi = 2 * s, fc = fi % CF, ch = fi / CF;
@@ -133,8 +165,8 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
       fr[(fi + 2) % 4] = frag(cur, fc + 2);
       fr[(fi + 3) % 4] = frag(cur, fc + 3);
     } else {
-      ring_barrier();
-      issue(chunk_src(ch + SLOTS - 1), (cur + SLOTS - 1) % SLOTS);
+      ring_barrier_cnt<Win::template at<s>()>();
+      issue(chunk_src(chb + ch + SLOTS - 1), (cur + SLOTS - 1) % SLOTS);
       const int nx = (cur + 1) % SLOTS;
       fr[(fi + 2) % 4] = frag(nx, 0);
       fr[(fi + 3) % 4] = frag(nx, 1);
@@ -147,115 +179,200 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
     if constexpr (fc + 2 >= CF) cur = (cur + 1) % SLOTS;
   };
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  const float al = a.alpha;
+  // constants of dual_gap(., alpha) and dual_gap(., 1), formed on the host (lena_gap_consts)
+  const Gap Gac{a.gc[0], a.gc[1], a.gc[2], a.gc[3]}, G1c{a.gc[4], a.gc[5], a.gc[6], a.gc[7]};
+  // mode 0: per-column sums of the layer; part[k][t] through a buffer view (lanes g > 0 and
+  // padded columns write nothing / their zero sums: every lane issues the store)
+  const rsrc_t rpart = mkrsrc(a.part, (uint32_t)((int64_t)4 * K * a.ldl * 4));
+  const uint32_t vp = g == 0 ? (uint32_t)(col * 4) : kOOB;
 
-  // ---- G1: Y = A^T L_k, blocks (2p, 2p+1) of the n rows over jb = 0..MB-1
+  // valid rows of this lane: 16 b + r < lim (no rows for a padded column)
+  const int limm = cv ? m - 4 * g : -1, limn = cv ? n - 4 * g : -1;
   float S[MODE == 1 ? NB : 1][4];
-  float sdy = 0.f;  // mode 0: this lane's sum of dual_gap(Y, alpha) over valid rows
-  static_for<NB / 2>([&](auto P_) {
-    constexpr int p = decltype(P_)::value;
-    f32x4 ca = zero4, cb = zero4;
-    static_for<MB>([&](auto J_) {
-      constexpr int jb = decltype(J_)::value;
-      constexpr int s = p * MB + jb;
-      step_head(std::integral_constant<int, s>{});
-      const f32x4 wa = fr[(2 * s) % 4], wb = fr[(2 * s + 1) % 4];
-      ca = mfma4(wa.x, Lr[jb][0], ca);
-      cb = mfma4(wb.x, Lr[jb][0], cb);
-      ca = mfma4(wa.y, Lr[jb][1], ca);
-      cb = mfma4(wb.y, Lr[jb][1], cb);
-      ca = mfma4(wa.z, Lr[jb][2], ca);
-      cb = mfma4(wb.z, Lr[jb][2], cb);
-      ca = mfma4(wa.w, Lr[jb][3], ca);
-      cb = mfma4(wb.w, Lr[jb][3], cb);
-      step_tail(std::integral_constant<int, s>{});
-    });
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
+  for (int k = 0; k < K; ++k) {
+    // the ring slot at a layer start is the same every layer (chunks per layer: a multiple of
+    // the slots); opaque, so the compiler cannot precompute the unrolled body's LDS addresses
+    // and keep them all live across the layer loop
+    cur = __builtin_amdgcn_readfirstlane(cur);
+    asm volatile("" : "+s"(cur));
+    const rsrc_t rln = lview(k + 1);
+    const rsrc_t re = mkrsrc(a.E + (int64_t)k * a.ls, mbytes);
+    float se = 0.f, sdl = 0.f, slx = 0.f, sdy = 0.f;
+    // mode 0: |E_k|, dual_gap(L_k, 1), L_k X over block b's rows (E / X rows in ev / xv)
+    // Row masks: row 16 b + 4 g + r is valid iff 16 b + r < lim (lim folds in the lane's 4 g
+    // and its column); lim goes through an opaque copy where it is used, so the compiler can
+    // neither precompute every (b, r) mask at the top (hundreds of live lane masks: spills) nor
+    // branch around the transcendental work of masked-off lanes.
+    auto masked_add = [](float& acc, float v, int rr, int lim0) {
+      int lim = lim0;
+      asm volatile("" : "+v"(lim), "+v"(v));
+      acc += rr < lim ? v : 0.f;
+    };
+    auto elem_sums = [&](int b, const float (&ev)[4], const float (&xv)[4]) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float y = h ? cb[r] : ca[r];
-        if constexpr (MODE == 0) {
-          const bool ok = cv && (16 * (2 * p + h) + 4 * g + r) < n;
-          const float dg = softplus_t(y - al) + softplus_t(-y - al);
-          sdy += ok ? dg : 0.f;
-        } else {
-          // rows past n: y = 0 exactly (zero-padded A^T), so S = 0 there
-          S[2 * p + h][r] = softplus_d(y - al) - softplus_d(-y - al);
-          pin_agpr(S[2 * p + h][r]);
-        }
+        const float l = Lr[b][r];
+        se += fabsf(ev[r]);
+        masked_add(sdl, dual_gap(l, G1c), 16 * b + r, limm);
+        slx += l * xv[r];
       }
-  });
-
-  if constexpr (MODE == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's filler DMA has landed
-    const float v[4] = {col_sum(se), col_sum(sdy), col_sum(sdl), col_sum(slx)};
-    if (g == 0) {  // padded columns write their zero sums (the reduction reads every column)
+    };
+    if constexpr (MODE == 0 && NP1 == 1) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) a.part[((int64_t)k * 4 + t) * a.ldl + col] = v[t];
-    }
-    return;
-  } else {
-    // ---- G2: G = A S, blocks (2p, 2p+1) of the m rows over kb = 0..NB-1; epilogue gL, gE
-    const float c = a.coef[k];
-    const float cn = c * a.inv_nb, cm = c * a.inv_mb;
-    const uint32_t vg = cv ? (uint32_t)((col + (int64_t)(4 * g) * a.ldg) * 4) : kOOB;
-    const uint32_t gbytes = (uint32_t)((int64_t)m * a.ldg * 4);
-    const rsrc_t rgl = mkrsrc(a.gL + (int64_t)k * a.gls, gbytes);
-    const rsrc_t rge = mkrsrc(a.gE + (int64_t)k * a.gls, gbytes);
-    static_for<MB / 2>([&](auto P_) {
-      constexpr int p = decltype(P_)::value;
-      // this pair's X and E rows, in flight during its MFMAs
-      float xv[2][4], ev[2][4];
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
+      for (int b = 0; b < MB; ++b) {
+        float ev[4], xv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = 16 * (2 * p + h) + r;
-          xv[h][r] = bload(rx, vx + (uint32_t)((int64_t)row * a.ldx * 4));
-          ev[h][r] = bload(re, vo + (uint32_t)((int64_t)row * ld * 4));
+          ev[r] = bload(re, vo + row_off(b, r, ld));
+          xv[r] = bload(rx, vx + row_off(b, r, a.ldx));
         }
+        elem_sums(b, ev, xv);
+      }
+    }
+    // ---- G1: Y = A^T L_k, blocks (2p, 2p+1) of the n rows over jb = 0..MB-1
+    static_for<NP1>([&](auto P_) {
+      constexpr int p = decltype(P_)::value;
+      constexpr int NBP = MODE == 0 && NP1 > 1 ? Win::blocks_at(p) : 0;
+      float ev[NBP > 0 ? NBP : 1][4], xv[NBP > 0 ? NBP : 1][4];
       f32x4 ca = zero4, cb = zero4;
-      static_for<NB>([&](auto K_) {
-        constexpr int kb = decltype(K_)::value;
-        constexpr int s = (NB / 2) * MB + p * NB + kb;  // G2 follows G1 in the stream
+      static_for<MB>([&](auto J_) {
+        constexpr int jb = decltype(J_)::value;
+        constexpr int s = p * MB + jb;
         step_head(std::integral_constant<int, s>{});
+        if constexpr (jb == 0 && NBP > 0) {  // E / X rows of this pair's blocks
+          int q = 0;
+#pragma unroll
+          for (int b = 0; b < MB; ++b) {
+            if (Win::pair_of_block(b) != p) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              ev[q][r] = bload(re, vo + row_off(b, r, ld));
+              xv[q][r] = bload(rx, vx + row_off(b, r, a.ldx));
+            }
+            ++q;
+          }
+        }
         const f32x4 wa = fr[(2 * s) % 4], wb = fr[(2 * s + 1) % 4];
-        ca = mfma4(wa.x, S[kb][0], ca);
-        cb = mfma4(wb.x, S[kb][0], cb);
-        ca = mfma4(wa.y, S[kb][1], ca);
-        cb = mfma4(wb.y, S[kb][1], cb);
-        ca = mfma4(wa.z, S[kb][2], ca);
-        cb = mfma4(wb.z, S[kb][2], cb);
-        ca = mfma4(wa.w, S[kb][3], ca);
-        cb = mfma4(wb.w, S[kb][3], cb);
+        ca = mfma4(wa.x, Lr[jb][0], ca);
+        cb = mfma4(wb.x, Lr[jb][0], cb);
+        ca = mfma4(wa.y, Lr[jb][1], ca);
+        cb = mfma4(wb.y, Lr[jb][1], cb);
+        ca = mfma4(wa.z, Lr[jb][2], ca);
+        cb = mfma4(wb.z, Lr[jb][2], cb);
+        ca = mfma4(wa.w, Lr[jb][3], ca);
+        cb = mfma4(wb.w, Lr[jb][3], cb);
+        if constexpr (MODE == 0 && p == NP1 - 1) {
+          // L_{k+1}'s block jb: this was the last read of L_k's block jb
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            Lr[jb][r] = bload(rln, vo + row_off(jb, r, ld));
+            pin_agpr(Lr[jb][r]);
+          }
+        }
         step_tail(std::integral_constant<int, s>{});
       });
+      if constexpr (NBP > 0) {
+        int q = 0;
+#pragma unroll
+        for (int b = 0; b < MB; ++b) {
+          if (Win::pair_of_block(b) != p) continue;
+          elem_sums(b, ev[q], xv[q]);
+          ++q;
+        }
+      }
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int b = 2 * p + h;
-          const uint32_t so = (uint32_t)((int64_t)(16 * b + r) * a.ldg * 4);
-          const float l = Lr[b][r];
-          const float dl = softplus_d(l - 1.0f) - softplus_d(-l - 1.0f);
-          const float gl = cn * (h ? cb[r] : ca[r]) + cm * (dl + xv[h][r]);
-          const float e = ev[h][r];
-          const float sg = (e > 0.f ? 1.f : 0.f) - (e < 0.f ? 1.f : 0.f);
-          bstore_s(rgl, vg, so, gl);
-          bstore_s(rge, vg, so, cm * sg);
+          const float y = h ? cb[r] : ca[r];
+          if constexpr (MODE == 0) {
+            masked_add(sdy, dual_gap(y, Gac), 16 * (2 * p + h) + r, limn);
+          } else {
+            // rows past n: y = 0 exactly (zero-padded A^T), so S = 0 there
+            S[2 * p + h][r] = dual_gap_d(y, Gac);
+            pin_agpr(S[2 * p + h][r]);
+          }
         }
     });
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's last DMA has landed
+
+    if constexpr (MODE == 0) {
+      const float v[4] = {col_sum(se), col_sum(sdy), col_sum(sdl), col_sum(slx)};
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        bstore_s(rpart, vp, (uint32_t)(((int64_t)k * 4 + t) * a.ldl * 4), v[t]);
+    } else {
+      // ---- G2: G = A S, blocks (2p, 2p+1) of the m rows over kb = 0..NB-1; epilogue gL, gE
+      const float c = a.coef[k];
+      const float cn = c * a.inv_nb, cm = c * a.inv_mb;
+      const uint32_t vg = cv ? (uint32_t)((col + (int64_t)(4 * g) * a.ldg) * 4) : kOOB;
+      const uint32_t gbytes = (uint32_t)((int64_t)m * a.ldg * 4);
+      const rsrc_t rgl = mkrsrc(a.gL + (int64_t)k * a.gls, gbytes);
+      const rsrc_t rge = mkrsrc(a.gE + (int64_t)k * a.gls, gbytes);
+      static_for<MB / 2>([&](auto P_) {
+        constexpr int p = decltype(P_)::value;
+        float xv[2][4], ev[2][4];
+        f32x4 ca = zero4, cb = zero4;
+        static_for<NB>([&](auto K_) {
+          constexpr int kb = decltype(K_)::value;
+          constexpr int s = T1 + p * NB + kb;  // G2 follows G1 in the stream
+          step_head(std::integral_constant<int, s>{});
+          if constexpr (kb == 0) {  // this pair's X and E rows, in flight during its MFMAs
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                xv[h][r] = bload(rx, vx + row_off(2 * p + h, r, a.ldx));
+                ev[h][r] = bload(re, vo + row_off(2 * p + h, r, ld));
+              }
+          }
+          const f32x4 wa = fr[(2 * s) % 4], wb = fr[(2 * s + 1) % 4];
+          ca = mfma4(wa.x, S[kb][0], ca);
+          cb = mfma4(wb.x, S[kb][0], cb);
+          ca = mfma4(wa.y, S[kb][1], ca);
+          cb = mfma4(wb.y, S[kb][1], cb);
+          ca = mfma4(wa.z, S[kb][2], ca);
+          cb = mfma4(wb.z, S[kb][2], cb);
+          ca = mfma4(wa.w, S[kb][3], ca);
+          cb = mfma4(wb.w, S[kb][3], cb);
+          if constexpr (kb == NB - 1) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int b = 2 * p + h;
+                const uint32_t so = row_off(b, r, a.ldg);
+                const float l = Lr[b][r];
+                const float dl = dual_gap_d(l, G1c);
+                const float gl = cn * (h ? cb[r] : ca[r]) + cm * (dl + xv[h][r]);
+                const float e = ev[h][r];
+                const float sg = (e > 0.f ? 1.f : 0.f) - (e < 0.f ? 1.f : 0.f);
+                bstore_s(rgl, vg, so, gl);
+                bstore_s(rge, vg, so, cm * sg);
+              }
+            // L_{k+1}'s blocks 2p, 2p+1 (their last read of L_k was just above)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                Lr[2 * p + h][r] = bload(rln, vo + row_off(2 * p + h, r, ld));
+                pin_agpr(Lr[2 * p + h][r]);
+              }
+          }
+          step_tail(std::integral_constant<int, s>{});
+        });
+      });
+    }
+    chb += CPL;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's last DMA has landed
 }
 
 template <int MP, int NP>
 hipError_t launch_lena_s(const LenaArgs& a, int grid, hipStream_t s) {
   if (a.mode == 0)
-    hipLaunchKernelGGL((lena_kernel<MP, NP, 0>), dim3(grid, a.K), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((lena_kernel<MP, NP, 0>), dim3(grid), dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((lena_kernel<MP, NP, 1>), dim3(grid, a.K), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((lena_kernel<MP, NP, 1>), dim3(grid), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
