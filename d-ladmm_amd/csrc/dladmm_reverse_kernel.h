@@ -191,7 +191,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   // per-row parameter gradient slots a G2' row stores (BK3's beta1 of layer k; BK1's of layer
   // k - 1): V2 beta3 (= beta1's L term), beta2, theta_e; V3 also ss2
   constexpr int NRS = ROWP ? (kAE ? 5 : 4) : 0;
-  constexpr int LD2 = 4 + (kAE ? 2 : 0) + (kV1 ? 4 : 0) + NR + (COT ? 3 : 0);
+  constexpr int LD2 = 3 + (kAE ? 2 : 0) + (kV1 ? 4 : 0) + NR + (COT ? 3 : 0);
   constexpr int ST2 = 1 + (kAE ? 1 : 0) + (kV1 ? 3 : 0) + NRS;
   constexpr int LD1 = 1 + (GZ ? 1 : 0) + (ROWP ? 1 : 0);
   // DEEP: operands two pairs (G1') / one pair (G2') ahead instead of one pair / one block --
@@ -397,8 +397,10 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   auto res2_last = [&]() -> R2 {
     R2 o;
     o.P = mkrsrc(a.T, mbytes);
-    o.E = o.L = o.T = none;
-    o.B1K = o.B1J = o.B2J = o.GB1J = o.GB2J = o.GE = o.GL = o.GT = none;
+    o.L = urs(a.L0, mbytes);  // Var_0 = L0 + beta1_0 T_0 (E0 / L0: the outputs' row stride)
+    o.E = o.T = none;
+    o.B1J = o.B2J = o.GB1J = o.GB2J = o.GE = o.GL = o.GT = none;
+    o.B1K = kV1 ? tview(RT_B1, 0) : none;
     o.GB1K = kV1 ? tview(RT_GB1, 0) : none;
     if constexpr (ROWP) {
       o.PK = rpart(0);
@@ -474,7 +476,6 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
     const uint32_t so = wPT.at(rr);
     pw[rr][S_P] = ld(o.P, vo, so);
     pw[rr][S_L] = ld(o.L, vo, so);
-    pw[rr][S_T] = ld(o.T, vo, so);
     pw[rr][S_X] = ld(rx, vx, wX.at(rr));
     if constexpr (kAE) {
       pw[rr][S_E] = ld(o.E, vo, so);
@@ -581,6 +582,14 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
     if constexpr ((REV_ABL & 2) && MODE != 2) { GP[b][r] = gVar; pin_agpr(GP[b][r]); return; }
     auto& pv = pvs_all[set2(b)];
     const int row = 16 * b + 4 * g + r;  // this lane's row (ROWP partials)
+    // pv slot S of row r, or `dflt` for a slot this instantiation does not have
+    auto pvs = [&](auto S_, float dflt) -> float {
+      constexpr int S = decltype(S_)::value;
+      if constexpr (S < NS) return pv[r][S];
+      else return dflt;
+    };
+    using S_B1K_t = std::integral_constant<int, kV1 ? S_B1K : ROWP ? S_RB1K : NS>;
+    const float b1k = pvs(S_B1K_t{}, P.b1k);
     if constexpr (MODE == 1) {
       if constexpr (kV1) {
         // beta1_0's gradient: BK1(0)'s term (pv) + gVar T_0
@@ -596,21 +605,15 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
         psb1 += gVar * pv[r][S_P];
         asm volatile("" : "+v"(psb1));
       }
-      bstore_s(rv, vw, wV.at(r), 0.f);  // keeps the row's VM count (rv: no records)
-      if constexpr (kAE) bstore_s(rv, vw, wV.at(r) + aeo, 0.f);
+      // Var_0 = L0 + beta1_0 T_0, the forward's prologue expression (pv: T_0 in the P slot, L0)
+      bstore_s(rv, vw, wV.at(r), pv[r][S_L] + b1k * pv[r][S_P]);
+      if constexpr (kAE) bstore_s(none, vw, wV.at(r) + aeo, 0.f);  // keeps the row's VM count
       if (r == 3) {
         wV.next(); wB.next();
         if constexpr (ROWP) wP2.next();
       }
       return;
     } else {
-      // pv slot S of row r, or `dflt` for a slot this instantiation does not have
-      auto pvs = [&](auto S_, float dflt) -> float {
-        constexpr int S = decltype(S_)::value;
-        if constexpr (S < NS) return pv[r][S];
-        else return dflt;
-      };
-      using S_B1K_t = std::integral_constant<int, kV1 ? S_B1K : ROWP ? S_RB1K : NS>;
       using S_B1J_t = std::integral_constant<int, kV1 ? S_B1J : ROWP ? S_RB1J : NS>;
       using S_B2J_t = std::integral_constant<int, kV1 ? S_B2J : ROWP ? S_RB2J : NS>;
       using S_B3J_t = std::integral_constant<int, (ROWP && kAE) ? S_RB3J : NS>;
@@ -625,14 +628,13 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
       using S_GL_t = std::integral_constant<int, COT ? S_GL : NS>;
       using S_GT_t = std::integral_constant<int, COT ? S_GT : NS>;
       const float aLin = pv[r][S_AL] + gVar;  // complete adjoint of L_{k-1} (upstream aside)
-      const float b1k = pvs(S_B1K_t{}, P.b1k);
       const float aTin = b1k * gVar;          // adjoint of T_k (main_syn_l1l1_scalar.py:117)
       const float aL = COT ? aLin + pvs(S_GL_t{}, 0.f) : aLin;
       const float aT = COT ? aTin + pvs(S_GT_t{}, 0.f) : aTin;
       // incoming adjoint of E_{k-1}: zero in the prologue (the buffer is not yet written)
       const float aE0 = MODE == 0 ? pvs(S_AE_t{}, 0.f) : 0.f;
       const float aE = COT ? aE0 + pvs(S_GE_t{}, 0.f) : aE0;
-      const float Pv = pv[r][S_P], lp = pv[r][S_L], tk = pv[r][S_T], x = pv[r][S_X];
+      const float Pv = pv[r][S_P], lp = pv[r][S_L], x = pv[r][S_X];
       const float b1 = pvs(S_B1J_t{}, P.b1);
       float gP, gEp = 0.f, gLp, t;
       (void)gEp;
@@ -640,7 +642,8 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
       if constexpr (EMODE == EM_V1) {
         const float b2 = b2p;
         const float u = (x - Pv) - b2 * lp;               // main_lena.py:87
-        const float e = shrink(u, thep);
+        // E_{k-1} as the forward formed it (scalar theta: the clamp form; common.h)
+        const float e = ROWP ? shrink(u, thep) : shrink_u(u, shrink_params(thep));
         t = (Pv + e) - x;                                 // T_k
         const float gTn = aT + b1 * aL;                   // L_{k-1} = L_{k-2} + b1 T_k (:89)
         p3 = aL * t;
@@ -657,7 +660,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
         const float r0 = (Pv + ep) - x;
         const float vv = lp + b2p * r0;                   // main_syn_l1l1_scalar.py:114
         const float eh = ep - ss2p * vv;                  // :115
-        const float e = shrink(eh, thep);
+        const float e = ROWP ? shrink(eh, thep) : shrink_u(eh, shrink_params(thep));
         t = (Pv + e) - x;                                 // T_k
         const float gTn = aT + b3p * aL;
         p3 = aL * t;
@@ -721,11 +724,18 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
       GP[b][r] = gP;
       pin_agpr(GP[b][r]);
       als[al_at(b, r)] = gLp;
+      // Var of layer k (BK3's): L_{k-1} + beta1_k T_k from the values just recomputed, the
+      // forward's own expression (l = L_{k-2} + c T_k, then + beta1_k T_k; c = the L-update
+      // coefficient), so T_{k-1} is never loaded.  The prologue's (layer K) is dropped: its
+      // store runs past rv's last layer block.
+      const float lcoef = EMODE == EM_V1 ? b1 : (EMODE == EM_VVAR ? b3p : P.b3);
+      const float lk = lp + lcoef * t;
+      const float vark = lk + b1k * t;
       if constexpr (!(REV_ABL & 64)) {
-        bstore_s(rv, vw, wV.at(r), lp + b1 * tk);  // Var_{k-1} = L_{k-2} + b1 T_{k-1}
+        bstore_s(rv, vw, vas4 + wV.at(r), vark);
         if constexpr (kAE) bstore_s(rv, vw, wV.at(r) + aeo, gEp);  // adjoint of E_{k-2}
       } else {
-        asm volatile("" ::"v"(gEp), "v"(lp + b1 * tk));
+        asm volatile("" ::"v"(gEp), "v"(vark));
       }
       if (r == 3) {
         wV.next(); wB.next();
@@ -933,13 +943,14 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
   }
   const LP2 P0 = lp2(0, -1);
   const R2 o0 = res2_last();
-  g2_pass(std::true_type{}, 0, P0, o0, none, P1, Rk, rgu(0));
+  const rsrc_t rv0 = rvar(0);  // the last pass stores Var_0
+  g2_pass(std::true_type{}, 0, P0, o0, rv0, P1, Rk, rgu(0));
   // rows of layer 0's last G2' pair
   static_for<8>([&](auto I_) {
     constexpr int i = decltype(I_)::value;
     constexpr int h = i / 4, r = i % 4;
-    epi2_row(std::integral_constant<int, 1>{}, P0, o0, none, MB - 2 + h, r, h ? qb : qa);
-    if constexpr (h == 0 && !DEEP) pre2(o0, none, MB - 1, r);
+    epi2_row(std::integral_constant<int, 1>{}, P0, o0, rv0, MB - 2 + h, r, h ? qb : qa);
+    if constexpr (h == 0 && !DEEP) pre2(o0, rv0, MB - 1, r);
   });
   flush(0, DLADMM_P_BETA1, psb1);
   // drain: the ring's last LDS-DMA must land before the workgroup's LDS is released
