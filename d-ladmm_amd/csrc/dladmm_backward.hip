@@ -492,6 +492,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tiles_m = a.MBp16 / 8;  // 128-column tiles (of V rows)
   const int tile = blockIdx.x;
+  const int64_t zl = blockIdx.z;   // layer of a batched launch
   const int ti = tile / tiles_m, tj = tile % tiles_m;
   const int64_t b0 = (int64_t)blockIdx.y * a.chunk;
   int64_t b1 = b0 + a.chunk;
@@ -507,8 +508,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
 
   // this wave's DMA share: waves 0, 1 the G row blocks 4w .. 4w+3, waves 2, 3 the V row blocks
   // 4(w-2) .. +3 of the tile; lane offset of row 16 f + r, column 4 g (bytes, < 2^31: host)
-  const float* src = w < 2 ? a.G + (int64_t)(ti * 128 + 64 * w) * a.ld
-                           : a.V + (int64_t)(tj * 128 + 64 * (w - 2)) * a.ld;
+  const float* src = w < 2 ? a.G + zl * a.gls + (int64_t)(ti * 128 + 64 * w) * a.ld
+                           : a.V + zl * a.vls + (int64_t)(tj * 128 + 64 * (w - 2)) * a.ld;
   src += b0;
   const uint32_t vl = (uint32_t)(((int64_t)r * a.ld + 4 * g) * 4);
   const uint32_t rs16 = (uint32_t)(16 * a.ld * 4);
@@ -546,7 +547,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA in flight when the LDS is released
   // C/D layout: lane holds column (l & 15) = V row j, rows 4g + r' = G rows
   const int i0 = ti * 128 + (w >> 1) * 64, j0 = tj * 128 + (w & 1) * 64;
-  float* out = a.part + (int64_t)blockIdx.y * a.n * a.m;
+  float* out = a.part + zl * a.pls + (int64_t)blockIdx.y * a.n * a.m;
 #pragma unroll
   for (int x = 0; x < 4; ++x)
 #pragma unroll
@@ -590,6 +591,61 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* part, in
     }
     if (threadIdx.x == 0) dotp[blockIdx.x] = red[0];
   }
+}
+
+// The same reduction for the nl layers of a batched weight-gradient launch (WredArgs): per
+// element, each layer's chunk sum in the chunk order of wgrad_reduce_kernel; tied: added into
+// one gW in descending layer order, as the per-layer launches did
+__global__ __launch_bounds__(256) void wgrad_reduce_layers_kernel(const WredArgs a) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int i = (int)(e / a.m), j = (int)(e % a.m);  // used for e < nm only
+  __shared__ double red[256];
+  auto layer_sum = [&](int y) -> float {
+    float s = 0.0f;
+    const float* pp = a.part + (int64_t)y * a.pls;
+    for (int c = 0; c < a.nchunks; ++c) s += pp[(int64_t)c * a.nm + e];
+    return s;
+  };
+  auto dot_flush = [&](int k, double dv) {  // uniform: fixed-order block sum
+    red[threadIdx.x] = dv;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) a.dotp[(int64_t)k * a.nbd + blockIdx.x] = red[0];
+    __syncthreads();
+  };
+  if (!a.tied) {
+    const int y = blockIdx.y, k = a.klo + y;
+    double dv = 0.0;
+    if (e < a.nm) {
+      const float s = layer_sum(y);
+      const float scale = -(a.scal ? a.scal[k * DLADMM_NSCALAR + DLADMM_P_S1] : 1.0f);
+      a.gW[(int64_t)k * a.gls + (int64_t)i * a.ldgw + j] = scale * s;
+      if (a.Wd) dv = (double)a.Wd[(int64_t)i * a.ldwd + j] * (double)s;
+    }
+    if (a.Wd) dot_flush(k, dv);
+    return;
+  }
+  for (int y = a.nl - 1; y >= 0; --y) {
+    const int k = a.klo + y;
+    double dv = 0.0;
+    if (e < a.nm) {
+      const float s = layer_sum(y);
+      const float scale = -(a.scal ? a.scal[k * DLADMM_NSCALAR + DLADMM_P_S1] : 1.0f);
+      float* dst = a.gW + (int64_t)i * a.ldgw + j;
+      *dst = *dst + scale * s;
+      if (a.Wd) dv = (double)a.Wd[(int64_t)i * a.ldwd + j] * (double)s;
+    }
+    if (a.Wd) dot_flush(k, dv);
+  }
+}
+
+hipError_t launch_wgrad_reduce_layers(const WredArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(wgrad_reduce_layers_kernel, dim3((unsigned)((a.nm + 255) / 256),
+                                                      a.tied ? 1 : a.nl), dim3(256), 0, s, a);
+  return hipGetLastError();
 }
 
 // g_s1 = -sum_b dotp[b] (fixed order) -> the layer's ss1 slot of the scalar gradients
@@ -645,8 +701,8 @@ hipError_t launch_bwd(int phase, int variant, const BwdArgs& a, dim3 grid, int s
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_wgrad(const WgradArgs& a, int tiles, hipStream_t s) {
-  hipLaunchKernelGGL(wgrad_kernel, dim3(tiles, a.nchunks), dim3(256), 0, s, a);
+hipError_t launch_wgrad(const WgradArgs& a, int tiles, hipStream_t s, int layers) {
+  hipLaunchKernelGGL(wgrad_kernel, dim3(tiles, a.nchunks, layers), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -734,6 +734,7 @@ struct BwdPlan {
   int64_t Bpad, Rn, Rm;           // padded batch; padded rows of the gU / Var buffers
   int nslots, ncg;
   int wtiles, nchunks; int64_t chunk;
+  int wgl;  // reverse path: layers per batched weight-gradient launch
   bool saved_p;                   // BK1 reads the forward's A Z_k (fwd_desc.P)
   size_t off_a1, off_at, off_m, off_mt, off_az, off_ae, off_al, off_at_, off_gp, off_var,
       off_part, off_part2, off_wpart, off_s1dot, total;
@@ -884,7 +885,13 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
     // adjoint of E_{k-1} (V4) that the next-lower layer's BK1 reads
     p->off_rvar = o; o += align256(colb * (p->Rm2 + kShapeMP[p->fwd.shape]) * K);
     p->off_rpart = o; o += align256(sizeof(float) * DLADMM_NSCALAR * K * p->rncg);
-    p->off_wpart = o; o += align256(sizeof(float) * (size_t)p->nchunks * n * m);
+    // the weight gradients of up to wgl layers per launch (one grid over their tiles and
+    // chunks; partials <= 256 MiB): no per-layer launch gaps and tails
+    const size_t lpart = sizeof(float) * (size_t)p->nchunks * n * m;
+    p->wgl = (int)((size_t)256 * 1024 * 1024 / lpart);
+    if (p->wgl < 1) p->wgl = 1;
+    if (p->wgl > (int)K) p->wgl = (int)K;
+    p->off_wpart = o; o += align256(lpart * p->wgl);
     p->off_s1dot = o; o += align256(sizeof(double) * (size_t)s1_dot_blocks(n, m) * K);
     p->off_rptab = o; o += align256(sizeof(void*) * (size_t)(RT_NTAB * K + 1));
     // V2 / V3: per-row partials [K][8][max(MP, NP)][waves] (the kernel's padded rows)
@@ -999,18 +1006,27 @@ inline int run_reverse(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hip
   const int nbd = s1_dot_blocks(n, m);
   if (tied)
     if (hipError_t e = zero_2d_async(d->gW, d->ld_gw, m, n, s)) return (int)e;
-  for (int k = K - 1; k >= 0; --k) {
+  // batches of wgl layers, highest first (the tied sum keeps the per-layer order K-1 .. 0)
+  // V5 with distinct per-layer weights (not what the module passes): one layer per batch, so
+  // each layer's <W_k, G_k> reads its own W_k
+  bool wsame = true;
+  for (int k = 1; k < K; ++k) wsame = wsame && f.W[k] == f.W[0];
+  const int wgl = v5 && !wsame ? 1 : p.wgl;
+  for (int khi = K - 1; khi >= 0; khi -= wgl) {
+    const int nl = khi + 1 < wgl ? khi + 1 : wgl, klo = khi - nl + 1;
     WgradArgs wa{};
-    wa.G = GU + k * gus; wa.V = VAR + k * vas; wa.ld = ldw; wa.n = n; wa.m = m;
+    wa.G = GU + klo * gus; wa.V = VAR + klo * vas; wa.ld = ldw; wa.n = n; wa.m = m;
     wa.NBp16 = (int)(p.Rn2 / 16); wa.MBp16 = (int)(p.Rm2 / 16);
     wa.Bpad = p.Bpad; wa.chunk = p.chunk; wa.nchunks = p.nchunks; wa.part = wpart;
-    if (hipError_t e = launch_wgrad(wa, p.wtiles, s)) return (int)e;
-    if (hipError_t e = launch_wgrad_reduce(wpart, p.nchunks, n, m, f.scalar_params, k,
-                                           tied ? 1 : 0,
-                                           tied ? d->gW : d->gW + (int64_t)k * n * d->ld_gw,
-                                           d->ld_gw, s, v5 ? f.W[k] : nullptr, f.ld_w,
-                                           v5 ? s1dot + (int64_t)k * nbd : nullptr))
-      return (int)e;
+    wa.gls = gus; wa.vls = vas; wa.pls = (int64_t)p.nchunks * n * m;
+    if (hipError_t e = launch_wgrad(wa, p.wtiles, s, nl)) return (int)e;
+    WredArgs ra{};
+    ra.part = wpart; ra.pls = wa.pls; ra.nchunks = p.nchunks; ra.nm = (int64_t)n * m;
+    ra.scal = f.scalar_params; ra.klo = klo; ra.nl = nl; ra.tied = tied ? 1 : 0;
+    ra.gW = d->gW; ra.gls = (int64_t)n * d->ld_gw; ra.ldgw = d->ld_gw; ra.m = m;
+    ra.Wd = v5 ? f.W[klo] : nullptr; ra.ldwd = f.ld_w;  // V5: the batch's (shared) weight
+    ra.dotp = v5 ? s1dot : nullptr; ra.nbd = nbd;
+    if (hipError_t e = launch_wgrad_reduce_layers(ra, s)) return (int)e;
   }
   // parameter slots of every layer: fixed-order fp64 sums of the per-wave partials (V1: its
   // per-sample beta gradients were written elementwise by the sweep)

@@ -160,6 +160,7 @@ struct WgradArgs {
   int64_t Bpad, chunk;                         // padded batch; columns per split-K chunk
   int nchunks;
   float* part;                                 // [nchunks][n][m]
+  int64_t gls, vls, pls;                       // layer strides (grid.z = layer of a batch)
 };
 
 hipError_t launch_bwd(int phase, int variant, const BwdArgs& a, dim3 grid, int sb,
@@ -170,7 +171,18 @@ static_assert(sizeof(FusedArgs) <= 2048, "kernel argument size");
 static_assert(sizeof(LayerArgs) <= 2048, "kernel argument size");
 static_assert(sizeof(BwdArgs) <= 2048, "kernel argument size");
 static_assert(sizeof(WgradArgs) <= 2048, "kernel argument size");
-hipError_t launch_wgrad(const WgradArgs& a, int tiles, hipStream_t s);
+hipError_t launch_wgrad(const WgradArgs& a, int tiles, hipStream_t s, int layers = 1);
+// fixed-order chunk sums of `nl` consecutive layers' split-K partials (part + y*pls, layers
+// klo + y): gW_k = -s1_k * sum (each its own output, layer stride gls), or (tied) all of them
+// added into one gW in the order k = klo + nl - 1 .. klo -- the per-layer reduce's order
+struct WredArgs {
+  const float* part; int64_t pls; int nchunks; int64_t nm;
+  const float* scal; int klo, nl, tied;
+  float* gW; int64_t gls, ldgw; int m;
+  const float* Wd; int64_t ldwd;  // V5: <W, G_k> per layer -> dotp + k*nbd
+  double* dotp; int nbd;
+};
+hipError_t launch_wgrad_reduce_layers(const WredArgs& a, hipStream_t s);
 
 // ---- backward as one reverse sweep (dladmm_reverse.hip): V1 / V4 / V5 / V6 after a saved-
 // product fused forward, register-resident shapes (kShapeMP / kShapeNP), optional upstream
