@@ -342,7 +342,11 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     const float u = (PKIND == PK_S1) ? Zr[b][r] + P.s1 * q[r] : Zr[b][r] + q[r];
     float z;
     if constexpr (PKIND == PK_ROW) {
-      z = shrink(u, rowp(k, DLADMM_P_THETA_Z, b, r));
+      // per-row theta in the clamp form as for the scalar kinds (common.h): for theta < 0 it
+      // gives Z = 2U exactly where both relus are open, so the backward's masks read off the
+      // saved Z_k (|Z| < 2|theta|) are exact -- the literal form can round U within an ulp of
+      // -|theta| to Z = -2|theta| and drop a term there
+      z = shrink_u(u, shrink_params(rowp(k, DLADMM_P_THETA_Z, b, r)));
     } else {
       z = shrink_u(u, P.thz);
     }

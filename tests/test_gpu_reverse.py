@@ -292,3 +292,54 @@ def test_reverse_per_row_params(variant, shape, loss, dl, monkeypatch):
 def test_reverse_per_row_headline_shape(variant, dl, monkeypatch):
     rev, per = both_cot(dl, variant, 256, 512, 4096, 15, 9880, monkeypatch, "", True)
     check_equal_row(rev, per, 15)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["v2", "v3"])
+def test_per_row_negative_theta_masks_at_the_boundary(variant, dl):
+    """Per-row theta_z < 0 with U = Z_{k-1} - W Var placed exactly at -|theta| and one ulp either
+    side (W_0 = 0, so U = Z0 exactly): the reverse sweep reads S'(U) off the saved Z_k, which the
+    forward forms in the clamp form (Z = 2U exactly where both relus are open).  Against fp64
+    autograd of the reference-op restatement (literal two-relu shrink, torch's relu'(0) = 0):
+    theta_z's per-row gradient is a sum of +-cotangents, so a dropped or extra mask term shows
+    as an O(1) relative error."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "oracle"))
+    import dladmm_torch_cpu as TC
+    m, n, B, K = 32, 64, 64, 1
+    inp = P.make_inputs(m, n, B, 9910)
+    sd = P.make_state_dict(variant, m, n, B, K, inp["A"], 9910, perturb=0.1)
+    c = np.linspace(0.05, 0.3, n).astype(np.float32)           # |theta| per row
+    sd["active_para.0"] = (-c).reshape(n, 1)
+    sd["fc.0.weight"] = np.zeros_like(sd["fc.0.weight"])        # U = Z0 exactly
+    Z0 = np.empty((n, B), np.float32)
+    picks = []
+    for i in range(n):
+        ci = np.float32(c[i])
+        picks.append([-ci, np.nextafter(-ci, np.float32(-1)), np.nextafter(-ci, np.float32(1)),
+                      ci, np.nextafter(ci, np.float32(1)), np.nextafter(ci, np.float32(-1)),
+                      np.float32(0.0), -2 * ci])
+    for b in range(B):
+        Z0[:, b] = [picks[i][b % 8] for i in range(n)]
+    inp = dict(inp, Z0=Z0)
+    G = np.random.default_rng(9911).standard_normal((n, B)).astype(np.float32)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+    net = dl.VARIANTS[variant](m=m, n=0, d=n, batch_size=B, A=t(inp["A"]), Z0=t(Z0),
+                               E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K)
+    net.load_state_dict({k: t(v) for k, v in sd.items()}, strict=True)
+    net = net.cuda().requires_grad_(True)
+    out = net(t(inp["X"]).cuda())
+    (out[0][0] * t(G).cuda()).sum().backward()
+    g_gpu = net.active_para[0].grad.detach().cpu().double().numpy().ravel()
+    d64 = lambda a: torch.from_numpy(np.asarray(a, np.float64))  # noqa: E731
+    params = {k: d64(v).requires_grad_(True) for k, v in sd.items()}
+    fwd = getattr(TC.forward, "__wrapped__", TC.forward)
+    with torch.enable_grad():
+        o64 = fwd(variant, d64(inp["X"]), d64(inp["A"]), d64(Z0), d64(inp["E0"]),
+                  d64(inp["L0"]), params, K)
+        (o64[0][0] * d64(G)).sum().backward()
+    g64 = params["active_para.0"].grad.numpy().ravel()
+    assert np.allclose(g_gpu, g64, rtol=1e-5, atol=1e-5 * np.abs(g64).max()), \
+        np.abs(g_gpu - g64).max()
