@@ -25,6 +25,12 @@
 #include "dladmm_common.h"
 #include "dladmm_internal.h"
 
+#ifndef LENA_ABL
+#define LENA_ABL 0  // timing experiments only (WRONG results): 1 no G1 epilogue transcendentals,
+                    // 2 no mode-0 elementwise sums (E / X loads), 8 no G1 MFMAs, 16 mode-0
+                    // E loads without the sums' math, 32 the math without the E loads
+#endif
+
 namespace dladmm {
 
 // dual_gap(y, a) = softplus(y - a) + softplus(-y - a) = ln((1 + e^(y-a)) (1 + e^(-y-a)))
@@ -51,7 +57,22 @@ __device__ __forceinline__ float dual_gap_d(float y, const Gap& G) {
   return fabsf(y) > 30.0f ? copysignf(1.0f, y) : v;
 }
 
-template <int MB, int NB, int CF, int MODE>
+// Static VM-operation counts of one layer body, for the counted ring barriers (the scheme of the
+// forward's WinCount).  Steps: mode 0 = G1 only (T1 steps per layer), mode 1 = G1 then G2.  Ops
+// issued in the body of local step t (after its head, i.e. after any barrier / DMA of t):
+//   mode 0: at the start of G1 pair p the E loads of the L blocks assigned to p (blocks go to
+//           pairs 0 .. NB/2 - 2, their sums formed one step before the pair's last; NB/2 = 1:
+//           at the layer start); in the last pair, after each step's MFMAs, L_{k+1}'s block jb
+//           (4 loads); after the layer's last step the 4 sum stores;
+//   mode 1: at the start of G2 pair p the E loads of its two blocks (8); after its last step
+//           the gL / gE stores (16) and L_{k+1}'s two blocks (8).
+// A barrier at step s (last step of a chunk of SPC steps) awaits the chunk DMA issued SLOTS - 2
+// barriers back: newer are the DMAs of the barriers in between and every op of the steps since
+// (VM operations complete in issue order for vmcnt, so a load must have landed by the barrier
+// that awaits the first chunk DMA issued after it: a deeper ring gives the E loads, which miss
+// to HBM, more steps);
+// ops of the previous layer are not counted (fewer counted only waits longer).  X sits in LDS.
+template <int MB, int NB, int CF, int MODE, int SLOTS>
 struct LenaWin {
   static constexpr int SPC = CF / 2;
   static constexpr int DMAOPS = CF % 16 == 0 ? 4 * (CF / 16) : 1;  // VM ops of one chunk DMA
@@ -67,13 +88,13 @@ struct LenaWin {
     int c = 0;
     if constexpr (MODE == 0) {
       const int p = t / MB, j = t % MB;
-      if (j == 0 && NP1 > 1) c += 8 * blocks_at(p);
+      if (j == 0 && NP1 > 1 && !(LENA_ABL & 2)) c += 4 * blocks_at(p);
       if (p == NP1 - 1) c += 4;
       if (t == T1 - 1) c += 4;
     } else {
       if (t >= T1) {
         const int u = t - T1, j = u % NB;
-        if (j == 0) c += 16;
+        if (j == 0) c += 8;
         if (j == NB - 1) c += 24;
       }
     }
@@ -81,8 +102,8 @@ struct LenaWin {
   }
   template <int S>
   static constexpr int at() {
-    int n = DMAOPS;
-    for (int t = S - 2 * SPC; t < S; ++t)
+    int n = DMAOPS * (SLOTS - 3);
+    for (int t = S - (SLOTS - 2) * SPC; t < S; ++t)
       if (t >= 0) n += ops(t);
     return n < 63 ? n : 63;
   }
@@ -95,11 +116,13 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
   constexpr int CF = GF < 16 ? GF : 16;        // fragments per ring chunk
   constexpr int NCH = GF / CF;                 // chunks per product
   constexpr int CPL = MODE == 1 ? 2 * NCH : NCH;  // chunks per layer
-  constexpr int SLOTS = 4;
-  using Win = LenaWin<MB, NB, CF, MODE>;
+  // ring slots: 6 where they fit beside the X tile (160 KiB at 256 x 512), else 4
+  constexpr int SLOTS = (6 * CF + kWaves * MB) * 64 * 16 <= 160 * 1024 ? 6 : 4;
+  using Win = LenaWin<MB, NB, CF, MODE, SLOTS>;
   constexpr int NP1 = NB / 2, T1 = Win::T1;
   static_assert(MB % 2 == 0 && NB % 2 == 0 && GF % CF == 0 && CF % 2 == 0, "shape");
   __shared__ f32x4 ring[SLOTS * CF * 64];
+  __shared__ f32x4 xs[kWaves * MB * 64];  // xs[w][b][lane] = X rows 16 b + 4 g .. +3 (read by w)
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -153,7 +176,14 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
         pin_agpr(Lr[b][r]);
       }
   }
-  ring_barrier();  // the primed chunks landed; L_0 is in
+#pragma unroll
+  for (int b = 0; b < MB; ++b) {
+    f32x4 xv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) xv[r] = bload(rx, vx + row_off(b, r, a.ldx));
+    xs[(w * MB + b) * 64 + lane] = xv;  // this wave's own columns: no barrier needed
+  }
+  ring_barrier();  // the primed chunks landed; L_0 and X are in
   f32x4 fr[4];
   fr[0] = frag(0, 0);
   fr[1] = frag(0, 1);
@@ -190,9 +220,8 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
   const int limm = cv ? m - 4 * g : -1, limn = cv ? n - 4 * g : -1;
   float S[MODE == 1 ? NB : 1][4];
   for (int k = 0; k < K; ++k) {
-    // the ring slot at a layer start is the same every layer (chunks per layer: a multiple of
-    // the slots); opaque, so the compiler cannot precompute the unrolled body's LDS addresses
-    // and keep them all live across the layer loop
+    // opaque ring slot at the layer start, so the compiler cannot precompute the unrolled
+    // body's LDS addresses and keep them all live across the layer loop
     cur = __builtin_amdgcn_readfirstlane(cur);
     asm volatile("" : "+s"(cur));
     const rsrc_t rln = lview(k + 1);
@@ -208,7 +237,12 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
       asm volatile("" : "+v"(lim), "+v"(v));
       acc += rr < lim ? v : 0.f;
     };
-    auto elem_sums = [&](int b, const float (&ev)[4], const float (&xv)[4]) {
+    auto elem_sums = [&](int b, const float (&ev)[4]) {
+      const f32x4 xv = xs[(w * MB + b) * 64 + lane];
+      if constexpr (LENA_ABL & 16) {  // loads kept, no math
+        se += ev[0] + ev[1] + ev[2] + ev[3] + xv[0];
+        return;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float l = Lr[b][r];
@@ -220,39 +254,52 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
     if constexpr (MODE == 0 && NP1 == 1) {
 #pragma unroll
       for (int b = 0; b < MB; ++b) {
-        float ev[4], xv[4];
+        float ev[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          ev[r] = bload(re, vo + row_off(b, r, ld));
-          xv[r] = bload(rx, vx + row_off(b, r, a.ldx));
-        }
-        elem_sums(b, ev, xv);
+        for (int r = 0; r < 4; ++r) ev[r] = bload(re, vo + row_off(b, r, ld));
+        elem_sums(b, ev);
       }
     }
     // ---- G1: Y = A^T L_k, blocks (2p, 2p+1) of the n rows over jb = 0..MB-1
     static_for<NP1>([&](auto P_) {
       constexpr int p = decltype(P_)::value;
-      constexpr int NBP = MODE == 0 && NP1 > 1 ? Win::blocks_at(p) : 0;
-      float ev[NBP > 0 ? NBP : 1][4], xv[NBP > 0 ? NBP : 1][4];
+      constexpr int NBP = MODE == 0 && NP1 > 1 && !(LENA_ABL & 2) ? Win::blocks_at(p) : 0;
+      float ev[NBP > 0 ? NBP : 1][4];
       f32x4 ca = zero4, cb = zero4;
       static_for<MB>([&](auto J_) {
         constexpr int jb = decltype(J_)::value;
         constexpr int s = p * MB + jb;
         step_head(std::integral_constant<int, s>{});
-        if constexpr (jb == 0 && NBP > 0) {  // E / X rows of this pair's blocks
+        if constexpr (jb == 0 && NBP > 0) {  // E rows of this pair's blocks
           int q = 0;
 #pragma unroll
           for (int b = 0; b < MB; ++b) {
             if (Win::pair_of_block(b) != p) continue;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              ev[q][r] = bload(re, vo + row_off(b, r, ld));
-              xv[q][r] = bload(rx, vx + row_off(b, r, a.ldx));
-            }
+            for (int r = 0; r < 4; ++r)
+              ev[q][r] = (LENA_ABL & 32) ? 0.5f : bload(re, vo + row_off(b, r, ld));
+            ++q;
+          }
+        }
+        // the sums of this pair's blocks one step before the pair's last step: their E rows are
+        // then waited for before that step's ring barrier issues the next DMA (the compiler's
+        // own wait for a loaded value counts every VM operation after it, the LDS-DMA included)
+        if constexpr (jb == MB - 2 && NBP > 0) {
+          int q = 0;
+#pragma unroll
+          for (int b = 0; b < MB; ++b) {
+            if (Win::pair_of_block(b) != p) continue;
+            elem_sums(b, ev[q]);
             ++q;
           }
         }
         const f32x4 wa = fr[(2 * s) % 4], wb = fr[(2 * s + 1) % 4];
+        if constexpr (LENA_ABL & 8) {  // no MFMAs: the ring, barriers and epilogues alone
+          ca += wa * Lr[jb][0];
+          cb += wb * Lr[jb][1];
+          step_tail(std::integral_constant<int, s>{});
+          return;
+        }
         ca = mfma4(wa.x, Lr[jb][0], ca);
         cb = mfma4(wb.x, Lr[jb][0], cb);
         ca = mfma4(wa.y, Lr[jb][1], ca);
@@ -271,25 +318,18 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
         }
         step_tail(std::integral_constant<int, s>{});
       });
-      if constexpr (NBP > 0) {
-        int q = 0;
-#pragma unroll
-        for (int b = 0; b < MB; ++b) {
-          if (Win::pair_of_block(b) != p) continue;
-          elem_sums(b, ev[q], xv[q]);
-          ++q;
-        }
-      }
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float y = h ? cb[r] : ca[r];
           if constexpr (MODE == 0) {
-            masked_add(sdy, dual_gap(y, Gac), 16 * (2 * p + h) + r, limn);
+            if constexpr (LENA_ABL & 1) sdy += y;
+            else masked_add(sdy, dual_gap(y, Gac), 16 * (2 * p + h) + r, limn);
           } else {
             // rows past n: y = 0 exactly (zero-padded A^T), so S = 0 there
-            S[2 * p + h][r] = dual_gap_d(y, Gac);
+            if constexpr (LENA_ABL & 1) S[2 * p + h][r] = y;
+            else S[2 * p + h][r] = dual_gap_d(y, Gac);
             pin_agpr(S[2 * p + h][r]);
           }
         }
@@ -310,20 +350,32 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
       const rsrc_t rge = mkrsrc(a.gE + (int64_t)k * a.gls, gbytes);
       static_for<MB / 2>([&](auto P_) {
         constexpr int p = decltype(P_)::value;
-        float xv[2][4], ev[2][4];
+        float ev[2][4], base[2][4], gsg[2][4];
         f32x4 ca = zero4, cb = zero4;
         static_for<NB>([&](auto K_) {
           constexpr int kb = decltype(K_)::value;
           constexpr int s = T1 + p * NB + kb;  // G2 follows G1 in the stream
           step_head(std::integral_constant<int, s>{});
-          if constexpr (kb == 0) {  // this pair's X and E rows, in flight during its MFMAs
+          if constexpr (kb == 0) {  // this pair's E rows, in flight during its MFMAs
 #pragma unroll
             for (int h = 0; h < 2; ++h)
 #pragma unroll
+              for (int r = 0; r < 4; ++r) ev[h][r] = bload(re, vo + row_off(2 * p + h, r, ld));
+          }
+          if constexpr (kb == NB - 2) {
+            // the parts of the epilogue that need no product, one step before the pair's last
+            // (E waited for before the last step's barrier issues the next DMA; see G1)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const f32x4 xv = xs[(w * MB + 2 * p + h) * 64 + lane];
+#pragma unroll
               for (int r = 0; r < 4; ++r) {
-                xv[h][r] = bload(rx, vx + row_off(2 * p + h, r, a.ldx));
-                ev[h][r] = bload(re, vo + row_off(2 * p + h, r, ld));
+                const float l = Lr[2 * p + h][r];
+                base[h][r] = cm * (dual_gap_d(l, G1c) + xv[r]);
+                const float e = ev[h][r];
+                gsg[h][r] = cm * ((e > 0.f ? 1.f : 0.f) - (e < 0.f ? 1.f : 0.f));
               }
+            }
           }
           const f32x4 wa = fr[(2 * s) % 4], wb = fr[(2 * s + 1) % 4];
           ca = mfma4(wa.x, S[kb][0], ca);
@@ -339,15 +391,9 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
             for (int h = 0; h < 2; ++h)
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                const int b = 2 * p + h;
-                const uint32_t so = row_off(b, r, a.ldg);
-                const float l = Lr[b][r];
-                const float dl = dual_gap_d(l, G1c);
-                const float gl = cn * (h ? cb[r] : ca[r]) + cm * (dl + xv[h][r]);
-                const float e = ev[h][r];
-                const float sg = (e > 0.f ? 1.f : 0.f) - (e < 0.f ? 1.f : 0.f);
-                bstore_s(rgl, vg, so, gl);
-                bstore_s(rge, vg, so, cm * sg);
+                const uint32_t so = row_off(2 * p + h, r, a.ldg);
+                bstore_s(rgl, vg, so, cn * (h ? cb[r] : ca[r]) + base[h][r]);
+                bstore_s(rge, vg, so, gsg[h][r]);
               }
             // L_{k+1}'s blocks 2p, 2p+1 (their last read of L_k was just above)
 #pragma unroll
