@@ -52,6 +52,9 @@
 #ifndef REV_SLOTS
 #define REV_SLOTS 4  // weight-ring slots (6 fit the LDS at 256 x 512 beside the AL tables)
 #endif
+#ifndef REV_CF
+#define REV_CF 16    // fragments per ring chunk (a ring barrier every REV_CF / 2 MFMA steps)
+#endif
 #ifndef REV_DEEP
 #define REV_DEEP 0   // 1: operands two pairs / one pair ahead (needs REV_SLOTS 6); measured no
                      // faster (7.58 vs 7.53 ms backward, profiles/r04_rev_deep_ab.json)
@@ -64,7 +67,7 @@ struct Rev {
   static constexpr int MB = MP / 16;
   static constexpr int NB = NP / 16;
   static constexpr int GF = MB * NB;                       // fragments per product
-  static constexpr int CF = GF < 16 ? GF : 16;             // fragments per ring chunk
+  static constexpr int CF = GF < REV_CF ? GF : REV_CF;     // fragments per ring chunk
   static constexpr int NCH = GF / CF;                      // chunks per product
   static constexpr int SLOTS = REV_SLOTS;                  // ring slots (SLOTS - 1 in flight)
   static constexpr int RING_F4 = SLOTS * CF * 64;
