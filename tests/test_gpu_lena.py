@@ -68,7 +68,8 @@ def fp64_reference(variant, inp, sd, K, coeffs):
         per = lena_losses(out[0], out[1], out[2], X, A, ALPHA, K)
         tot = sum(c * l for c, l in zip(coeffs, per))
         tot.backward()
-    return float(tot), [float(v) for v in per], {k: p.grad.numpy() for k, p in params.items()}
+    return float(tot.detach()), [float(v.detach()) for v in per], \
+        {k: p.grad.numpy() for k, p in params.items()}
 
 
 CASES = [
@@ -164,3 +165,78 @@ def test_lena_descriptor_validation(dl):
     d.mode = 0
     d.ld = 50   # row stride below the batch
     assert L.dladmm_lena_workspace_bytes(ctypes.byref(d)) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["v1", "v4"])
+def test_lena_column_shards_sum_to_full_batch(variant, dl):
+    """Data-parallel shards of the fused main_lena objective (training_loss(kind="lena",
+    cols=..., batch=B)): the summed losses and gradients equal the whole batch's."""
+    base = "v1_lena_cfg1" if variant == "v1" else "v4_med_pert"
+    defn = dict(P.FIXTURES[base], B=96, seed=4411, perturb=0.1, wscale=0.4)
+    K, B = 3, 96
+    net, inp, sd = build(dl, defn, K)
+    net.requires_grad_(True)
+    X = torch.from_numpy(inp["X"]).cuda()
+    coeffs = [0.6, 0.6, 1.0]
+    tf, pf = net.training_loss(X, ALPHA, coeffs, kind="lena")
+    tf.backward()
+    shard, _, _ = build(dl, defn, K)
+    shard.requires_grad_(True)
+    tot, per = 0.0, 0.0
+    for c0, c1 in (dl.dist.shard_columns(B, 0, 2), dl.dist.shard_columns(B, 1, 2)):
+        t, pl = shard.training_loss(X[:, c0:c1], ALPHA, coeffs, kind="lena", batch=B,
+                                    cols=(c0, c1))
+        t.backward()
+        tot, per = tot + float(t), per + pl.double().cpu().numpy()
+    np.testing.assert_allclose(tot, float(tf), rtol=1e-5)
+    np.testing.assert_allclose(per, pf.double().cpu().numpy(), rtol=1e-5)
+    ps = dict(shard.named_parameters())
+    for key, p in net.named_parameters():
+        e = nrel(ps[key].grad.cpu().numpy(), p.grad.cpu().numpy())
+        assert e <= 1e-5, (key, e)
+
+
+@pytest.mark.gpu
+def test_lena_graph_training_step(dl):
+    """V1 forward + fused main_lena objective + backward captured as one HIP graph and replayed on
+    new data: the objective and every gradient equal an eager step's bit for bit."""
+    defn = dict(P.FIXTURES["v1_lena_cfg1"], B=640, seed=4412, perturb=0.1, wscale=0.4)
+    K = 4
+    net, inp, _ = build(dl, defn, K)
+    net.requires_grad_(True)
+    X2 = P.make_inputs(defn["m"], defn["n"], defn["B"], 4413)["X"]
+
+    def step(xx):
+        total, _ = net.training_loss(xx, ALPHA, [1.0] * K, kind="lena")
+        total.backward()
+        return total
+
+    def eager(data):
+        net.zero_grad(set_to_none=True)
+        tot = step(torch.from_numpy(data).cuda()).detach()
+        torch.cuda.synchronize()
+        return tot, {k: p.grad.clone() for k, p in net.named_parameters()}
+
+    refs = [eager(X2), eager(inp["X"])]
+    x = torch.from_numpy(inp["X"]).cuda()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            net.zero_grad(set_to_none=False)
+            step(x)
+    torch.cuda.current_stream().wait_stream(s)
+    net.zero_grad(set_to_none=False)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        static_total = step(x)
+    for data, (ref_total, ref) in zip((X2, inp["X"]), refs):
+        x.copy_(torch.from_numpy(data).cuda())
+        for p in net.parameters():
+            p.grad.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(static_total.detach(), ref_total)
+        for k, p in net.named_parameters():
+            assert torch.equal(p.grad, ref[k]), f"grad {k} of the replayed step differs"
