@@ -17,6 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 UNITS = ("dladmm_capi.hip", "dladmm_fused.hip", "dladmm_fused_savep.hip", "dladmm_fused_x3.hip",
+         "dladmm_fused_x3_savep.hip",
          "dladmm_layered.hip", "dladmm_backward.hip", "dladmm_lskm.hip", "dladmm_eval.hip",
          "dladmm_tile_bf16.hip", "dladmm_reverse.hip", "dladmm_lena.hip",
          # reverse-sweep instantiations: one unit per E-step form and shape group (minutes each)
@@ -34,7 +35,7 @@ FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", f"--offload-arch={AR
 # MFMAs (packed v_pk_* f32 ops issue slower there; MI355X_MICROARCH.md, price of one filler
 # beside MFMAs)
 UNIT_FLAGS = {u: ["-fno-slp-vectorize"] for u in UNITS
-              if u == "dladmm_fused_x3.hip" or u.startswith("dladmm_reverse")}
+              if u.startswith("dladmm_fused_x3") or u.startswith("dladmm_reverse")}
 
 
 def deps(path, seen=None):

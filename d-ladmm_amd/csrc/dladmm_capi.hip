@@ -612,7 +612,12 @@ inline int run_fused_x3(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipSt
   if (d->ev_kernel_start) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_start, s)) return (int)e;
   }
-  if (hipError_t e = launch_fused_x3_shape(p.shape, d->variant, a, p.tiles, s)) return (int)e;
+  // training forwards also store P_k = A Z_k for the backward (fwd_desc.P, keep_all only)
+  const bool savep = d->P != nullptr && d->keep_all;
+  a.Po = savep ? d->P : nullptr;
+  if (hipError_t e = (savep ? launch_fused_x3_shape_savep : launch_fused_x3_shape)(
+          p.shape, d->variant, a, p.tiles, s))
+    return (int)e;
   if (d->ev_kernel_stop) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_stop, s)) return (int)e;
   }
@@ -812,8 +817,8 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   *p = BwdPlan{};
   const dladmm_fwd_desc& f = d->fwd;
   if (int e = make_plan(&f, &p->fwd)) return e;
-  // the forward stored A Z_k only on the fused fp32 path (fwd_desc.P)
-  p->saved_p = f.P != nullptr && f.keep_all && p->fwd.path == 1;
+  // the forward stored A Z_k only on the fused paths, fp32 and split-f16 (fwd_desc.P)
+  p->saved_p = f.P != nullptr && f.keep_all && (p->fwd.path == 1 || p->fwd.path == 4);
   const int m = f.m, n = f.n;
   const int64_t B = f.batch;
   p->MB = ceil_div(m, 16);

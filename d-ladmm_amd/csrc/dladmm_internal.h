@@ -52,6 +52,9 @@ hipError_t launch_fused_shape_savep(int shape, int variant, const FusedArgs& a, 
 bool x3_supports(int variant);
 hipError_t launch_fused_x3_shape(int shape, int variant, const FusedArgs& a, int grid,
                                  hipStream_t s);
+// the same kernels that also store P_k = A Z_k (a.Po) for the backward (dladmm_fused_x3_savep.hip)
+hipError_t launch_fused_x3_shape_savep(int shape, int variant, const FusedArgs& a, int grid,
+                                       hipStream_t s);
 
 }  // namespace dladmm
 

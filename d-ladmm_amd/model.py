@@ -126,8 +126,9 @@ class _DLADMMBase(nn.Module):
     # "f32_split" (the same fp32 GEMMs on the f16 matrix cores: operands split exactly into
     # scaled hi + lo f16 halves, hi*hi + hi*lo + lo*hi accumulated in fp32 -- the error of an fp32
     # GEMM, ~3x the throughput; V4-V6 fused shapes, others run f32) or "bf16" (BASELINE config 5:
-    # bf16 MFMA operands, fp32 accumulation and fp32 elementwise state).  The backward always
-    # differentiates the f32 forward, so training runs "f32".
+    # bf16 MFMA operands, fp32 accumulation and fp32 elementwise state).  Training runs "f32" or
+    # "f32_split": the split-f16 forward saves the product A Z_k its updates consumed, and the
+    # (fp32) backward differentiates that forward; "bf16" is inference-only.
     precision = "f32"
 
     def run(self, x: torch.Tensor, keep_all: bool = True, loss_kind: int = 0,
@@ -149,9 +150,9 @@ class _DLADMMBase(nn.Module):
             if x.requires_grad:
                 raise RuntimeError("dladmm: gradients w.r.t. the input X are not supported (the "
                                    "reference trains the parameters only)")
-            if self.precision != "f32":
+            if self.precision not in ("f32", "f32_split"):
                 raise RuntimeError(f"dladmm: precision {self.precision!r} is inference-only "
-                                   "(the backward differentiates the f32 forward)")
+                                   "(training runs f32 or f32_split)")
             outs = _DLADMMFunction.apply(self, x, nl, *self.parameters())
             return (list(outs[:nl]), list(outs[nl:2 * nl]), list(outs[2 * nl:3 * nl]),
                     list(outs[3 * nl:]))
@@ -319,6 +320,15 @@ def _slice_tables(tables: dict, nl: int) -> dict:
     return {k: (v[:nl] if v is not None else None) for k, v in tables.items()}
 
 
+def _train_precision(mod) -> str:
+    """Forward precision of a differentiable call: the module's "f32_split" (which saves its own
+    A Z_k for the backward), else "f32"."""
+    if mod.precision not in ("f32", "f32_split"):
+        raise RuntimeError(f"dladmm: precision {mod.precision!r} is inference-only "
+                           "(training runs f32 or f32_split)")
+    return mod.precision
+
+
 class _DLADMMFunction(torch.autograd.Function):
     """The K-layer forward as one differentiable op: forward = dladmm_fwd_f32 with every layer
     (and T) saved, backward = dladmm_bwd_f32 (the HIP reverse sweep).
@@ -334,7 +344,7 @@ class _DLADMMFunction(torch.autograd.Function):
         tables = _slice_tables(mod._tables(dev), nl)
         W = [w.detach() for w in mod._weights()[:nl]]
         r = dladmm_forward(mod.VARIANT, x, mod.A, W, mod.Z0, mod.E0, mod.L0, keep_all=True,
-                           want_T=True, want_P=True, **tables)
+                           want_T=True, want_P=True, precision=_train_precision(mod), **tables)
         ctx.mod = mod
         ctx.nl = nl
         ctx.tables = tables
@@ -397,7 +407,7 @@ class _DLADMMLossFunction(torch.autograd.Function):
         Z0, E0, L0 = mod._init_state(cols)
         lk = {"l1l1": _lib.LOSS_L1L1, "lasso": _lib.LOSS_LASSO}[kind]
         r = dladmm_forward(mod.VARIANT, x, mod.A, W, Z0, E0, L0, keep_all=True, want_T=True,
-                           loss_kind=lk, want_P=True, **tables)
+                           loss_kind=lk, want_P=True, precision=_train_precision(mod), **tables)
         per_layer = (alpha * r.loss_sums[:, 0] + r.loss_sums[:, 1]) / denom  # fp64 [K]
         c = _coef_tensor(coeffs, dev)
         total = (c * per_layer).sum().to(torch.float32)
@@ -447,7 +457,8 @@ class _DLADMMLenaLossFunction(torch.autograd.Function):
         W = [w.detach() for w in mod._weights()]
         Z0, E0, L0 = mod._init_state(cols)
         r = dladmm_forward(mod.VARIANT, x, mod.A, W, Z0, E0, L0, keep_all=True, want_T=True,
-                           loss_kind=_lib.LOSS_L1L1, want_P=True, **tables)
+                           loss_kind=_lib.LOSS_L1L1, want_P=True, precision=_train_precision(mod),
+                           **tables)
         m, n = mod.A.shape
         sums = dladmm_lena(x, mod.A, r.E, r.L, alpha, denom)  # fp64 (K, 4)
         per_layer = (alpha * r.loss_sums[:, 0] / n + sums[:, 1] / n +

@@ -177,7 +177,7 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
         raise ValueError(f"dladmm: precision must be one of {sorted(_PRECISIONS)}, "
                          f"got {precision!r}")
     d.precision = _PRECISIONS[precision]
-    if want_P and keep_all and out.P is None and L.dladmm_fwd_path(ctypes.byref(d)) == 1:
+    if want_P and keep_all and out.P is None and L.dladmm_fwd_path(ctypes.byref(d)) in (1, 4):
         out.P = torch.empty((K, m, B), device=dev, dtype=torch.float32)
         d.P = out.P.data_ptr()
     if want_col_loss:

@@ -194,5 +194,52 @@ def test_split_falls_back_where_unsupported(dl, oracle):
             out = net(X)
         _compare(out, ref, tag=f"split fallback {variant}")
     net.requires_grad_(True)
+    out = net(X)          # f32_split trains (here on the fp32 fallback kernels)
+    assert out[0][0].requires_grad
+    net.precision = "bf16"
     with pytest.raises(RuntimeError, match="inference-only"):
         net(X)
+
+
+@pytest.mark.parametrize("variant", ["v4", "v5", "v6"])
+def test_split_training_saves_product_and_matches_fp32(variant, dl):
+    """Training on the split-f16 forward: it stores P_k = A Z_k (the product its E / L / T updates
+    consumed), so the backward runs the reverse sweep on it; the gradients of the fused objective
+    equal the fp32 path's within the backward tests' GTOL (tests/test_gpu_backward.py), both runs
+    on the same parameters and data, and the saved P equals A Z_k to fp32 GEMM accuracy."""
+    from importlib import import_module
+    ops = import_module("d-ladmm_amd.ops")
+    from test_gpu_backward import make_train_net
+    m, n, B, K = 256, 512, 200, 4
+    inp = P.make_inputs(m, n, B, 7711)
+    sd = P.make_state_dict(variant, m, n, B, K, inp["A"], 7711, perturb=0.1)
+    X = torch.from_numpy(inp["X"]).cuda()
+    kind = "lasso" if variant == "v6" else "l1l1"
+    coeffs = [0.6] * (K - 1) + [1.0]
+    grads, tots = {}, {}
+    for prec in ("f32", "f32_split"):
+        net = make_train_net(dl, variant, inp, sd, K)
+        net.precision = prec
+        tot, _ = net.training_loss(X, 1e-3, coeffs, kind)
+        tot.backward()
+        tots[prec] = float(tot.detach())
+        grads[prec] = {k: p.grad.detach().double().cpu().numpy() for k, p in net.named_parameters()
+                       if p.grad is not None}
+    assert abs(tots["f32_split"] - tots["f32"]) <= 1e-5 * abs(tots["f32"])
+    assert grads["f32"].keys() == grads["f32_split"].keys()
+    for k, g in grads["f32"].items():
+        assert nrel(grads["f32_split"][k], g) <= 1e-4, k
+    # the saved product and the plan
+    net = make_train_net(dl, variant, inp, sd, K)
+    net.precision = "f32_split"
+    W = [w.detach() for w in net._weights()]
+    r = ops.dladmm_forward(net.VARIANT, X, net.A, W, net.Z0, net.E0, net.L0, keep_all=True,
+                           want_T=True, want_P=True, precision="f32_split",
+                           **net._tables(net.A.device))
+    assert r.path == 4 and r.P is not None
+    Pref = torch.stack([net.A.double() @ r.Z[k].double() for k in range(K)])
+    assert float((r.P.double() - Pref).norm() / Pref.norm()) < 1e-6
+    res = ops.dladmm_backward(net.VARIANT, X, net.A, W, net.Z0, net.E0, net.L0, r,
+                              gZ=[torch.ones_like(r.Z[k]) for k in range(K)],
+                              tied=net._shared_weight(), **net._tables(net.A.device))
+    assert res.path == 1

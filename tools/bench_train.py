@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--lena-loss", action="store_true",
                     help="V1 with main_lena.py:221-228's loss (torch ops over the returned Z_k, "
                          "E_k and L_k: cotangents of Z, E and L reach the backward), alpha 0.45")
+    ap.add_argument("--precision", default="f32", choices=["f32", "f32_split"],
+                    help="forward GEMM precision (f32_split: the split-f16 fused forward, which "
+                         "saves its A Z_k for the fp32 backward)")
     ap.add_argument("--lena-fused", action="store_true",
                     help="main_lena.py:221-228's loss as net.training_loss(kind='lena') (fused: "
                          "dladmm_lena_f32 + the reverse sweep with E / L cotangents), alpha 0.45")
@@ -58,6 +61,7 @@ def main():
     A, X, Z0, E0, L0 = bench.synth(m, n, B, 0, dev)
     net = dl.VARIANTS[a.variant](m=m, n=0, d=n, batch_size=B, A=A, Z0=Z0, E0=E0, L0=L0,
                                  layers=K)
+    net.precision = a.precision
     kind = "lasso" if a.variant == "v6" else "l1l1"
     if a.lena_fused:
         a.alpha = 0.45
@@ -134,7 +138,7 @@ def main():
     res = {
         "metric": f"training steps/s ({a.variant.upper()} forward + "
                   f"{'main_lena' if a.lena_loss or a.lena_fused else kind} loss + backward + Adam)",
-        "variant": a.variant,
+        "variant": a.variant, "precision": a.precision,
         "loss_path": ("main_lena.py:221-228 fused (net.training_loss kind='lena')"
                       if a.lena_fused else "fused (net.training_loss)" if a.fused_loss else
                       "main_lena.py:221-228 torch ops on Z_k, E_k, L_k" if a.lena_loss else
