@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--precision", default="f32", choices=["f32", "f32_split"],
                     help="forward GEMM precision (f32_split: the split-f16 fused forward, which "
                          "saves its A Z_k for the fp32 backward)")
+    ap.add_argument("--adam-fused", action="store_true",
+                    help="torch.optim.Adam(fused=True) instead of the reference's default Adam")
     ap.add_argument("--lena-fused", action="store_true",
                     help="main_lena.py:221-228's loss as net.training_loss(kind='lena') (fused: "
                          "dladmm_lena_f32 + the reverse sweep with E / L cotangents), alpha 0.45")
@@ -73,7 +75,7 @@ def main():
 
     def dual_gap(x, al):  # main_lena.py:145-147
         return torch.nn.functional.softplus(x - al) + torch.nn.functional.softplus(-x - al)
-    opt = torch.optim.Adam(net.parameters(), lr=0.005)
+    opt = torch.optim.Adam(net.parameters(), lr=0.005, **({"fused": True} if a.adam_fused else {}))
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
 
     def step(timed):
@@ -138,7 +140,7 @@ def main():
     res = {
         "metric": f"training steps/s ({a.variant.upper()} forward + "
                   f"{'main_lena' if a.lena_loss or a.lena_fused else kind} loss + backward + Adam)",
-        "variant": a.variant, "precision": a.precision,
+        "variant": a.variant, "precision": a.precision, "adam_fused": a.adam_fused,
         "loss_path": ("main_lena.py:221-228 fused (net.training_loss kind='lena')"
                       if a.lena_fused else "fused (net.training_loss)" if a.fused_loss else
                       "main_lena.py:221-228 torch ops on Z_k, E_k, L_k" if a.lena_loss else
