@@ -28,7 +28,7 @@ P_BETA1, P_BETA2, P_BETA3, P_SS2, P_SS2B, P_THETA_E, P_THETA_Z, P_S1 = range(8)
 EXPORTED = ("dladmm_abi_version", "dladmm_fwd_workspace_bytes", "dladmm_fwd_path",
             "dladmm_fwd_f32", "dladmm_bwd_workspace_bytes", "dladmm_bwd_path", "dladmm_bwd_f32",
             "dladmm_safeguard_f32", "dladmm_colobj_f32", "dladmm_lena_workspace_bytes",
-            "dladmm_lena_f32", "dladmm_error_string")
+            "dladmm_lena_f32", "dladmm_scale_f32", "dladmm_error_string")
 # enum dladmm_mu_updater
 MU_NONE, MU_EMA, MU_GS, MU_RT = 0, 1, 2, 3
 
@@ -157,6 +157,8 @@ def lib():
     L.dladmm_lena_workspace_bytes.argtypes = [ctypes.POINTER(LenaDesc)]
     L.dladmm_lena_f32.restype = ctypes.c_int
     L.dladmm_lena_f32.argtypes = [ctypes.POINTER(LenaDesc), ctypes.c_void_p]
+    L.dladmm_scale_f32.restype = ctypes.c_int
+    L.dladmm_scale_f32.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
     L.dladmm_error_string.restype = ctypes.c_char_p
     L.dladmm_error_string.argtypes = [ctypes.c_int]
     if L.dladmm_abi_version() != ABI_VERSION:

@@ -1238,6 +1238,15 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
   return 0;
 }
 
+// x *= *s, unless *s == 1 (read on the device: no host synchronisation; the common
+// total.backward() scale 1 costs one launch)
+__global__ __launch_bounds__(256) void scale_if_kernel(float* x, int64_t n, const float* s) {
+  const float v = *s;
+  if (v == 1.0f) return;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    x[i] *= v;
+}
+
 // ---- fused main_lena.py objective (dladmm_lena.hip)
 struct LenaPlan {
   int shape, MP, NP, tiles, ldl;
@@ -1250,20 +1259,20 @@ inline int lena_plan(const dladmm_lena_desc* d, LenaPlan* p) {
   if (d->abi_version != DLADMM_ABI_VERSION) return DLADMM_E_ABI_VERSION;
   if (d->m < 1 || d->n < 1 || d->batch < 1) return DLADMM_E_SHAPE;
   if (d->layers < 1 || d->layers > 65535) return DLADMM_E_LAYERS;  // grid.y
-  if (d->mode != 0 && d->mode != 1) return DLADMM_E_UNSUPPORTED;
+  if (d->mode < 0 || d->mode > 2) return DLADMM_E_UNSUPPORTED;
   if (!d->X || !d->A || !d->E || !d->L) return DLADMM_E_NULL;
-  if (d->mode == 0 && !d->sums) return DLADMM_E_NULL;
-  if (d->mode == 1 && (!d->gE || !d->gL || !d->coef)) return DLADMM_E_NULL;
+  if (d->mode != 1 && !d->sums) return DLADMM_E_NULL;
+  if (d->mode != 0 && (!d->gE || !d->gL || !d->coef)) return DLADMM_E_NULL;
   const int64_t B = d->batch;
   if (d->ld < B || d->ld_x < B || d->ld_a < d->n) return DLADMM_E_SHAPE;
   if (d->layers > 1 && d->layer_stride < (int64_t)d->m * d->ld) return DLADMM_E_SHAPE;
-  if (d->mode == 1) {
+  if (d->mode != 0) {
     if (d->ld_g < B) return DLADMM_E_SHAPE;
     if (d->layers > 1 && d->g_layer_stride < (int64_t)d->m * d->ld_g) return DLADMM_E_SHAPE;
   }
   const int64_t lim = (int64_t)1 << 31;  // 32-bit buffer offsets per layer
   if ((int64_t)d->m * d->ld * 4 >= lim || (int64_t)d->m * d->ld_x * 4 >= lim ||
-      (d->mode == 1 && (int64_t)d->m * d->ld_g * 4 >= lim))
+      (d->mode != 0 && (int64_t)d->m * d->ld_g * 4 >= lim))
     return DLADMM_E_UNSUPPORTED;
   const int s = pick_shape(d->m, d->n);
   if (s < 0) return DLADMM_E_UNSUPPORTED;
@@ -1277,7 +1286,7 @@ inline int lena_plan(const dladmm_lena_desc* d, LenaPlan* p) {
   p->off_atp = align256(fb);
   p->off_part = p->off_atp + align256(fb);
   p->total = p->off_part +
-             (d->mode == 0 ? align256((size_t)4 * d->layers * p->ldl * sizeof(float)) : 0);
+             (d->mode != 1 ? align256((size_t)4 * d->layers * p->ldl * sizeof(float)) : 0);
   return 0;
 }
 
@@ -1323,12 +1332,24 @@ int dladmm_lena_f32(const dladmm_lena_desc* d, void* stream) {
   a.gE = d->gE; a.gL = d->gL; a.gls = d->g_layer_stride; a.ldg = d->ld_g;
   a.coef = d->coef;
   if (hipError_t e = launch_lena(p.shape, a, p.tiles, s)) return (int)e;
-  if (d->mode == 0) {
+  if (d->mode != 1) {
     hipLaunchKernelGGL(loss_reduce_kernel, dim3((unsigned)(4 * d->layers)), dim3(1024), 0, s,
                        (const float*)a.part, p.ldl, d->sums);
     if (hipError_t e = hipGetLastError()) return (int)e;
   }
   return 0;
+}
+
+int dladmm_scale_f32(float* x, int64_t n, const float* s, void* stream) {
+  using namespace dladmm;
+  if (n < 0) return DLADMM_E_SHAPE;
+  if (n == 0) return 0;
+  if (!x || !s) return DLADMM_E_NULL;
+  int64_t blocks = (n + 255) / 256;
+  blocks = blocks > 4096 ? 4096 : blocks;
+  hipLaunchKernelGGL(scale_if_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     x, n, s);
+  return (int)hipGetLastError();
 }
 
 int dladmm_abi_version(void) { return DLADMM_ABI_VERSION; }

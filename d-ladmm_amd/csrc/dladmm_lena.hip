@@ -50,6 +50,16 @@ __device__ __forceinline__ float dual_gap(float y, const Gap& G) {
   const float ay = fabsf(y);
   return ay > 30.0f ? ay - G.a : v;
 }
+// both at once (mode 2): the two share e^y and e^-y
+__device__ __forceinline__ void dual_gap_vd(float y, const Gap& G, float& val, float& der) {
+  const float e = exp_h(y), ei = __builtin_amdgcn_rcpf(e);
+  float v = 0.693147180559945309f * __builtin_amdgcn_logf(G.c1 + G.c2 * (e + ei));
+  float d = (e - ei) * __builtin_amdgcn_rcpf((e + ei) + G.c3);
+  asm("" : "+v"(v), "+v"(d));
+  const float ay = fabsf(y);
+  val = ay > 30.0f ? ay - G.a : v;
+  der = ay > 30.0f ? copysignf(1.0f, y) : d;
+}
 __device__ __forceinline__ float dual_gap_d(float y, const Gap& G) {
   const float e = exp_h(y), ei = __builtin_amdgcn_rcpf(e);
   float v = (e - ei) * __builtin_amdgcn_rcpf((e + ei) + G.c3);
@@ -115,7 +125,10 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
   constexpr int GF = MB * NB;                  // fragments per product
   constexpr int CF = GF < 16 ? GF : 16;        // fragments per ring chunk
   constexpr int NCH = GF / CF;                 // chunks per product
-  constexpr int CPL = MODE == 1 ? 2 * NCH : NCH;  // chunks per layer
+  // MODE 0: the sums; 1: the cotangents; 2: both (a training forward: the backward then only
+  // scales the cotangents by its upstream gradient)
+  constexpr bool GRAD = MODE >= 1, SUMS = MODE != 1;
+  constexpr int CPL = GRAD ? 2 * NCH : NCH;  // chunks per layer
   // ring slots: 6 where they fit beside the X tile (160 KiB at 256 x 512), else 4
   constexpr int SLOTS = (6 * CF + kWaves * MB) * 64 * 16 <= 160 * 1024 ? 6 : 4;
   using Win = LenaWin<MB, NB, CF, MODE, SLOTS>;
@@ -218,7 +231,7 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
 
   // valid rows of this lane: 16 b + r < lim (no rows for a padded column)
   const int limm = cv ? m - 4 * g : -1, limn = cv ? n - 4 * g : -1;
-  float S[MODE == 1 ? NB : 1][4];
+  float S[GRAD ? NB : 1][4];
   for (int k = 0; k < K; ++k) {
     // opaque ring slot at the layer start, so the compiler cannot precompute the unrolled
     // body's LDS addresses and keep them all live across the layer loop
@@ -326,6 +339,12 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
           if constexpr (MODE == 0) {
             if constexpr (LENA_ABL & 1) sdy += y;
             else masked_add(sdy, dual_gap(y, Gac), 16 * (2 * p + h) + r, limn);
+          } else if constexpr (MODE == 2) {
+            float dv, dd;
+            dual_gap_vd(y, Gac, dv, dd);
+            masked_add(sdy, dv, 16 * (2 * p + h) + r, limn);
+            S[2 * p + h][r] = dd;  // rows past n: y = 0 exactly, so S = 0 there
+            pin_agpr(S[2 * p + h][r]);
           } else {
             // rows past n: y = 0 exactly (zero-padded A^T), so S = 0 there
             if constexpr (LENA_ABL & 1) S[2 * p + h][r] = y;
@@ -371,8 +390,18 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const float l = Lr[2 * p + h][r];
-                base[h][r] = cm * (dual_gap_d(l, G1c) + xv[r]);
                 const float e = ev[h][r];
+                float dl;
+                if constexpr (MODE == 2) {  // the elementwise sums of the objective too
+                  float gv;
+                  dual_gap_vd(l, G1c, gv, dl);
+                  se += fabsf(e);
+                  masked_add(sdl, gv, 16 * (2 * p + h) + r, limm);
+                  slx += l * xv[r];
+                } else {
+                  dl = dual_gap_d(l, G1c);
+                }
+                base[h][r] = cm * (dl + xv[r]);
                 gsg[h][r] = cm * ((e > 0.f ? 1.f : 0.f) - (e < 0.f ? 1.f : 0.f));
               }
             }
@@ -407,6 +436,12 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
           step_tail(std::integral_constant<int, s>{});
         });
       });
+      if constexpr (MODE == 2) {
+        const float v[4] = {col_sum(se), col_sum(sdy), col_sum(sdl), col_sum(slx)};
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          bstore_s(rpart, vp, (uint32_t)(((int64_t)k * 4 + t) * a.ldl * 4), v[t]);
+      }
     }
     chb += CPL;
   }
@@ -417,8 +452,10 @@ template <int MP, int NP>
 hipError_t launch_lena_s(const LenaArgs& a, int grid, hipStream_t s) {
   if (a.mode == 0)
     hipLaunchKernelGGL((lena_kernel<MP, NP, 0>), dim3(grid), dim3(256), 0, s, a);
-  else
+  else if (a.mode == 1)
     hipLaunchKernelGGL((lena_kernel<MP, NP, 1>), dim3(grid), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((lena_kernel<MP, NP, 2>), dim3(grid), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -34,7 +34,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .ops import ForwardResult, dladmm_backward, dladmm_forward, dladmm_lena
+from .ops import ForwardResult, dladmm_backward, dladmm_forward, dladmm_lena, dladmm_scale_
 
 
 def _dev(t: torch.Tensor) -> torch.Tensor:
@@ -442,11 +442,13 @@ class _DLADMMLenaLossFunction(torch.autograd.Function):
     """main_lena.py's training objective (:221-228; dual_gap :145-147) as one differentiable op:
         total = sum_k coeffs[k] * (alpha mean|Z_k| + mean|E_k| + mean dual_gap(A^T L_k, alpha)
                                    + mean dual_gap(L_k, 1) + mean(L_k X)).
-    Forward: the fused K-layer kernel (its sum|Z_k| partials) + dladmm_lena_f32 mode 0 (the
-    other four sums; A^T L_k is formed and reduced in registers, never stored).  Backward:
-    dladmm_lena_f32 mode 1 writes the E_k / L_k cotangents (the product A S_k of the dual_gap
-    term included) and dladmm_bwd_f32 takes them, with alpha mean|Z_k| as its fused |Z| term --
-    the reverse sweep where the shape has it.  The reference instead forms the K products
+    Forward: the fused K-layer kernel (its sum|Z_k| partials) + dladmm_lena_f32 -- mode 0 (the
+    other four sums; A^T L_k is formed and reduced in registers, never stored) when no gradient
+    is wanted, else mode 2: the same sums and, in the same pass, the E_k / L_k cotangents of
+    sum_k c_k l_k (the product A S_k of the dual_gap term included).  Backward: those cotangents
+    times the upstream gradient (dladmm_scale_f32: no pass at all for total.backward()'s 1) into
+    dladmm_bwd_f32, with alpha mean|Z_k| as its fused |Z| term -- the reverse sweep where the
+    shape has it.  The reference instead forms the K products
     A^T L_k and a dozen elementwise passes over them with torch ops, and autograd as many more.
     Outputs: total (0-dim) and the per-layer losses [K] (non-differentiable)."""
 
@@ -460,14 +462,23 @@ class _DLADMMLenaLossFunction(torch.autograd.Function):
                            loss_kind=_lib.LOSS_L1L1, want_P=True, precision=_train_precision(mod),
                            **tables)
         m, n = mod.A.shape
-        sums = dladmm_lena(x, mod.A, r.E, r.L, alpha, denom)  # fp64 (K, 4)
+        c = _coef_tensor(coeffs, dev)
+        c32 = c.to(torch.float32)
+        ctx.grad = any(ctx.needs_input_grad[6:])
+        if ctx.grad:
+            # a training forward: the sums and the cotangents of sum_k c_k l_k in one pass
+            # (mode 2); the backward scales the cotangents by its upstream gradient
+            sums, gE, gL = dladmm_lena(x, mod.A, r.E, r.L, alpha, denom, coef=c32)
+        else:
+            sums = dladmm_lena(x, mod.A, r.E, r.L, alpha, denom)  # fp64 (K, 4)
+            gE = gL = None
         per_layer = (alpha * r.loss_sums[:, 0] / n + sums[:, 1] / n +
                      (sums[:, 0] + sums[:, 2] + sums[:, 3]) / m) / denom
-        c = _coef_tensor(coeffs, dev)
         total = (c * per_layer).sum().to(torch.float32)
         ctx.mod, ctx.tables, ctx.W, ctx.cols = mod, tables, W, cols
         ctx.alpha, ctx.denom = alpha, denom
-        ctx.c = c.to(torch.float32)
+        ctx.c = c32
+        ctx.gEL = (gE, gL)
         ctx.save_for_backward(x, r.Z, r.E, r.L, r.T, r.P)
         per_layer = per_layer.to(torch.float32)
         ctx.mark_non_differentiable(per_layer)
@@ -480,7 +491,11 @@ class _DLADMMLenaLossFunction(torch.autograd.Function):
         K = mod.layers
         m, n = mod.A.shape
         ck = (ctx.c * g_total).contiguous()                     # device-side, no host sync
-        gE, gL = dladmm_lena(x, mod.A, E, L, ctx.alpha, ctx.denom, coef=ck)
+        gE, gL = ctx.gEL
+        ctx.gEL = None
+        g1 = g_total.to(torch.float32).reshape(1).contiguous()
+        dladmm_scale_(gE, g1)   # a launch that returns at once for total.backward()'s 1
+        dladmm_scale_(gL, g1)
         # alpha mean|Z_k| as the backward's fused |Z| term; no fit term
         coef = torch.stack([ck * (ctx.alpha / (n * ctx.denom)), torch.zeros_like(ck)],
                            1).contiguous()

@@ -308,15 +308,29 @@ def dladmm_backward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[
     return BackwardResult(gWo, g_scalar, g_row, g1, g2, path)
 
 
+def dladmm_scale_(x: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    """x *= s in place (s: a one-element fp32 device tensor) through dladmm_scale_f32, which skips
+    the pass on the device when s == 1 -- no host synchronisation."""
+    if x.dtype != torch.float32 or not x.is_contiguous() or s.dtype != torch.float32 or \
+            s.numel() != 1 or s.device != x.device:
+        raise ValueError("dladmm: scale needs a contiguous fp32 tensor and an fp32 device scalar")
+    s = s.contiguous()
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    _lib.check(_lib.lib().dladmm_scale_f32(ctypes.c_void_p(x.data_ptr()), x.numel(),
+                                           ctypes.c_void_p(s.data_ptr()), ctypes.c_void_p(stream)))
+    return x
+
+
 def dladmm_lena(X: torch.Tensor, A: torch.Tensor, E: torch.Tensor, L: torch.Tensor, alpha: float,
-                denom: float, coef: Optional[torch.Tensor] = None):
+                denom: float, coef: Optional[torch.Tensor] = None, sums: bool = True):
     """The fused main_lena.py objective terms over a forward's saved E_k, L_k ((K, m, B) each;
     main_lena.py:221-228 with dual_gap :145-147) through `dladmm_lena_f32` (include/dladmm.h,
     csrc/dladmm_lena.hip).  coef None (mode 0): returns the fp64 (K, 4) sums
     [sum|E_k|, sum dual_gap(A^T L_k, alpha), sum dual_gap(L_k, 1), sum L_k X].  coef = device
     fp32 (K,) (mode 1): returns the cotangents (gE, gL), each (K, m, B), of
     sum_k coef[k] * (mean|E_k| + mean dual_gap(A^T L_k, alpha) + mean dual_gap(L_k, 1)
-    + mean(L_k X)), the means over m*denom (n*denom for A^T L_k) elements."""
+    + mean(L_k X)), the means over m*denom (n*denom for A^T L_k) elements; with coef and sums
+    (mode 2, one pass) returns (sums, gE, gL)."""
     Lb = _lib.lib()
     K, m, B = L.shape
     n = A.shape[1]
@@ -334,21 +348,20 @@ def dladmm_lena(X: torch.Tensor, A: torch.Tensor, E: torch.Tensor, L: torch.Tens
     d.X, d.ld_x = X.data_ptr(), X.stride(0)
     d.A, d.ld_a = A.data_ptr(), A.stride(0)
     d.E, d.L, d.layer_stride, d.ld = E.data_ptr(), L.data_ptr(), m * B, B
-    out = None
-    if coef is None:
-        d.mode = 0
-        out = torch.empty((K, 4), device=dev, dtype=torch.float64)
-        d.sums = out.data_ptr()
-    else:
+    sm = gE = gL = None
+    if coef is None or sums:
+        sm = torch.empty((K, 4), device=dev, dtype=torch.float64)
+        d.sums = sm.data_ptr()
+    if coef is not None:
         if tuple(coef.shape) != (K,) or coef.dtype != torch.float32 or coef.device != dev:
             raise ValueError("dladmm: coef must be an fp32 (K,) device tensor")
         coef = coef.contiguous()
-        d.mode = 1
         gE = torch.empty((K, m, B), device=dev, dtype=torch.float32)
         gL = torch.empty((K, m, B), device=dev, dtype=torch.float32)
         d.gE, d.gL, d.g_layer_stride, d.ld_g = gE.data_ptr(), gL.data_ptr(), m * B, B
         d.coef = coef.data_ptr()
-        out = (gE, gL)
+    d.mode = 0 if coef is None else (2 if sums else 1)
+    out = sm if coef is None else ((sm, gE, gL) if sums else (gE, gL))
     wsb = Lb.dladmm_lena_workspace_bytes(ctypes.byref(d))
     if wsb == 0:
         raise ValueError(f"dladmm: the fused main_lena objective supports m <= 256, n <= 512 "

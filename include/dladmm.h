@@ -328,7 +328,9 @@ int dladmm_colobj_f32(const dladmm_colobj_desc* d, void* stream);
  *           inv_nb = 1/(n N):  gE_k = coef[k] inv_mb sgn(E_k),
  *           gL_k = coef[k] inv_nb A S_k + coef[k] inv_mb (softplus'(L_k - 1) - softplus'(-L_k - 1)
  *           + X),  S_k = softplus'(A^T L_k - alpha) - softplus'(-A^T L_k - alpha)
- *           -- what a dladmm_bwd_f32 call then takes as its gE / gL cotangents.
+ *           -- what a dladmm_bwd_f32 call then takes as its gE / gL cotangents;
+ *   mode 2: both (a training forward: one pass over the layers; the backward scales the
+ *           cotangents by its upstream gradient with dladmm_scale_f32).
  * E_k and L_k (m x batch) sit at E + k*layer_stride (row stride ld), likewise the outputs (gE, gL
  * at + k*g_layer_stride, row stride ld_g).  coef: device [layers] (mode 1).  Shapes: m <= 256 and
  * n <= 512 (the fused forward's register-resident shapes); otherwise DLADMM_E_UNSUPPORTED.
@@ -342,14 +344,17 @@ typedef struct dladmm_lena_desc {
   const float* X; int64_t ld_x;
   const float* A; int64_t ld_a;
   const float* E; const float* L; int64_t layer_stride; int64_t ld;
-  double* sums;                                   /* mode 0: [layers][4] */
-  float* gE; float* gL; int64_t g_layer_stride; int64_t ld_g;   /* mode 1 */
-  const float* coef;                              /* mode 1: device [layers] */
+  double* sums;                                   /* modes 0, 2: [layers][4] */
+  float* gE; float* gL; int64_t g_layer_stride; int64_t ld_g;   /* modes 1, 2 */
+  const float* coef;                              /* modes 1, 2: device [layers] */
   void* workspace; size_t workspace_bytes;
 } dladmm_lena_desc;
 
 size_t dladmm_lena_workspace_bytes(const dladmm_lena_desc* d);
 int dladmm_lena_f32(const dladmm_lena_desc* d, void* stream);
+
+/* x[0 .. n) *= *s on `stream`, unless *s == 1 (s: a device scalar, read on the device). */
+int dladmm_scale_f32(float* x, int64_t n, const float* s, void* stream);
 
 /* Text for a return code of this library (DLADMM_E_* or hipError_t). */
 const char* dladmm_error_string(int code);

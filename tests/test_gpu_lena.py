@@ -240,3 +240,32 @@ def test_lena_graph_training_step(dl):
         assert torch.equal(static_total.detach(), ref_total)
         for k, p in net.named_parameters():
             assert torch.equal(p.grad, ref[k]), f"grad {k} of the replayed step differs"
+
+
+@pytest.mark.gpu
+def test_lena_upstream_scale_and_eval(dl):
+    """The training forward forms the cotangents of sum_k c_k l_k in the same pass as the sums
+    (mode 2); the backward multiplies them by the upstream gradient on the device: (2.5 * total)
+    .backward() gives 2.5x the gradients, and a no-grad evaluation (mode 0) returns the same
+    loss values."""
+    defn = dict(P.FIXTURES["v1_lena_cfg1"], B=200, seed=4421, perturb=0.1, wscale=0.4)
+    K = 3
+    net, inp, _ = build(dl, defn, K)
+    net.requires_grad_(True)
+    X = torch.from_numpy(inp["X"]).cuda()
+    tot, per = net.training_loss(X, ALPHA, [0.6, 0.6, 1.0], kind="lena")
+    tot.backward()
+    g1 = {k: p.grad.clone() for k, p in net.named_parameters()}
+    for scale in (2.0, 2.5):   # 2: every scaled value exact, so the gradients are exactly 2x
+        net.zero_grad(set_to_none=True)
+        tot2, _ = net.training_loss(X, ALPHA, [0.6, 0.6, 1.0], kind="lena")
+        (scale * tot2).backward()
+        for k, p in net.named_parameters():
+            if scale == 2.0:
+                assert torch.equal(p.grad, 2.0 * g1[k]), k
+            else:
+                g, r = p.grad.double(), scale * g1[k].double()
+                assert float((g - r).norm()) <= 1e-6 * float(r.norm()), k   # some grads are all zero
+    with torch.no_grad():
+        tot3, per3 = net.training_loss(X, ALPHA, [0.6, 0.6, 1.0], kind="lena")
+    assert torch.equal(tot3, tot.detach()) and torch.equal(per3, per.detach())

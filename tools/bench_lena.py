@@ -1,4 +1,4 @@
-"""Time dladmm_lena_f32 alone (mode 0: the loss sums; mode 1: the E / L cotangents) at the
+"""Time dladmm_lena_f32 alone (mode 0: the loss sums; mode 1: the E / L cotangents; mode 2: both) at the
 main_lena training shape: V1 m=256 n=512 K=15 B=65,536, synthetic E_k / L_k.  One JSON line.
 DLADMM_LIB selects a library (tools/ablate.py --unit dladmm_lena.hip variants)."""
 import argparse
@@ -27,12 +27,12 @@ L = torch.randn(K, m, B, device=dev, generator=g)
 coef = torch.ones(K, device=dev)
 res = {"shape": [m, n, K, B]}
 flop1 = 2.0 * m * n * B * K
-for mode in (0, 1):
+for mode in (0, 1, 2):
     ts = []
     for i in range(a.reps + 2):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        ops.dladmm_lena(X, A, E, L, 0.45, B, coef=None if mode == 0 else coef)
+        ops.dladmm_lena(X, A, E, L, 0.45, B, coef=None if mode == 0 else coef, sums=mode != 1)
         e1.record()
         torch.cuda.synchronize()
         if i >= 2:
