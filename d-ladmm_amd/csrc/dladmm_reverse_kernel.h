@@ -42,7 +42,9 @@
 #ifndef REV_ABL
 #define REV_ABL 0  // timing / register-pressure experiments only (WRONG results): 1 no prologue
                    // rows, 2 no G2' rows, 4 no G1' rows, 8 no Z_k loads, 16 no gU stores, 32 no
-                   // G2' operand loads, 64 no Var / adjoint-of-E stores
+                   // G2' operand loads, 64 no Var / adjoint-of-E stores; through a null buffer
+                   // view (instructions kept, no memory traffic): 128 the adjoint of E (loads and
+                   // stores), 256 X, 512 P, 1024 E, 2048 L
 #endif
 
 #ifndef REV_LOAD_AUX
@@ -477,12 +479,12 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
       return;
     }
     const uint32_t so = wPT.at(rr);
-    pw[rr][S_P] = ld(o.P, vo, so);
-    pw[rr][S_L] = ld(o.L, vo, so);
-    pw[rr][S_X] = ld(rx, vx, wX.at(rr));
+    pw[rr][S_P] = ld((REV_ABL & 512) ? none : o.P, vo, so);
+    pw[rr][S_L] = ld((REV_ABL & 2048) ? none : o.L, vo, so);
+    pw[rr][S_X] = ld((REV_ABL & 256) ? none : rx, vx, wX.at(rr));
     if constexpr (kAE) {
-      pw[rr][S_E] = ld(o.E, vo, so);
-      pw[rr][S_AE] = ld(rv, vw, wA.at(rr));
+      pw[rr][S_E] = ld((REV_ABL & 1024) ? none : o.E, vo, so);
+      pw[rr][S_AE] = ld((REV_ABL & 128) ? none : rv, vw, wA.at(rr));
     }
     if constexpr (kV1) {
       pw[rr][S_B1K] = ld(o.B1K, vo, so);
@@ -736,7 +738,7 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
       const float vark = lk + b1k * t;
       if constexpr (!(REV_ABL & 64)) {
         bstore_s(rv, vw, vas4 + wV.at(r), vark);
-        if constexpr (kAE) bstore_s(rv, vw, wV.at(r) + aeo, gEp);  // adjoint of E_{k-2}
+        if constexpr (kAE) bstore_s((REV_ABL & 128) ? none : rv, vw, wV.at(r) + aeo, gEp);  // adjoint of E_{k-2}
       } else {
         asm volatile("" ::"v"(gEp), "v"(vark));
       }
