@@ -491,8 +491,12 @@ class _DLADMMLenaLossFunction(torch.autograd.Function):
         K = mod.layers
         m, n = mod.A.shape
         ck = (ctx.c * g_total).contiguous()                     # device-side, no host sync
-        gE, gL = ctx.gEL
+        gE, gL = ctx.gEL if ctx.gEL is not None else (None, None)
         ctx.gEL = None
+        if gE is None:
+            # a second backward through a retained graph: the first scaled the forward's
+            # cotangents in place, so form them again (mode 1)
+            gE, gL = dladmm_lena(x, mod.A, E, L, ctx.alpha, ctx.denom, coef=ctx.c, sums=False)
         g1 = g_total.to(torch.float32).reshape(1).contiguous()
         dladmm_scale_(gE, g1)   # a launch that returns at once for total.backward()'s 1
         dladmm_scale_(gL, g1)

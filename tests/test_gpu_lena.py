@@ -246,8 +246,8 @@ def test_lena_graph_training_step(dl):
 def test_lena_upstream_scale_and_eval(dl):
     """The training forward forms the cotangents of sum_k c_k l_k in the same pass as the sums
     (mode 2); the backward multiplies them by the upstream gradient on the device: (2.5 * total)
-    .backward() gives 2.5x the gradients, and a no-grad evaluation (mode 0) returns the same
-    loss values."""
+    .backward() gives 2.5x the gradients, a no-grad evaluation (mode 0) returns the same loss
+    values, and a retained graph can be backed through twice."""
     defn = dict(P.FIXTURES["v1_lena_cfg1"], B=200, seed=4421, perturb=0.1, wscale=0.4)
     K = 3
     net, inp, _ = build(dl, defn, K)
@@ -269,3 +269,12 @@ def test_lena_upstream_scale_and_eval(dl):
     with torch.no_grad():
         tot3, per3 = net.training_loss(X, ALPHA, [0.6, 0.6, 1.0], kind="lena")
     assert torch.equal(tot3, tot.detach()) and torch.equal(per3, per.detach())
+    # a retained graph backed through twice: the second backward forms the cotangents again
+    # (mode 1; the first scaled the forward's in place) -- the gradients accumulate to 2x
+    net.zero_grad(set_to_none=True)
+    tot4, _ = net.training_loss(X, ALPHA, [0.6, 0.6, 1.0], kind="lena")
+    tot4.backward(retain_graph=True)
+    tot4.backward()
+    for k, p in net.named_parameters():
+        g, r = p.grad.double(), 2.0 * g1[k].double()
+        assert float((g - r).norm()) <= 1e-6 * float(r.norm()), k
