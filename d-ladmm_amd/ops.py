@@ -338,6 +338,18 @@ def dladmm_lena(X: torch.Tensor, A: torch.Tensor, E: torch.Tensor, L: torch.Tens
     for t in (E, L):
         if tuple(t.shape) != (K, m, B) or t.dtype != torch.float32 or not t.is_contiguous():
             raise ValueError("dladmm: E and L must be contiguous fp32 (K, m, B) tensors")
+    if tuple(X.shape) != (m, B) or tuple(A.shape) != (m, n) or X.dtype != torch.float32 or \
+            A.dtype != torch.float32:
+        raise ValueError(f"dladmm: X must be fp32 ({m}, {B}) and A fp32 ({m}, n); got "
+                         f"{tuple(X.shape)} {X.dtype}, {tuple(A.shape)} {A.dtype}")
+    if dev.type != "cuda" or any(t.device != dev for t in (A, E, L)):
+        raise ValueError("dladmm: X, A, E and L must be on one GPU")
+    if K == 0 or B == 0:   # nothing to reduce: zero sums, empty cotangents, no launch
+        sm = torch.zeros((K, 4), device=dev, dtype=torch.float64)
+        gE, gL = torch.zeros_like(E), torch.zeros_like(L)
+        if coef is None:
+            return sm
+        return (sm, gE, gL) if sums else (gE, gL)
     X = X.contiguous()
     A = A.contiguous()
     d = _lib.LenaDesc()

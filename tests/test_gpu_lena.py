@@ -167,6 +167,23 @@ def test_lena_descriptor_validation(dl):
     assert L.dladmm_lena_workspace_bytes(ctypes.byref(d)) == 0
 
 
+def test_lena_host_checks(dl):
+    """Host-only: ops.dladmm_lena refuses operands the descriptor cannot describe before any
+    launch -- X of another shape than (m, B), A of another row count, host tensors."""
+    from importlib import import_module
+    ops = import_module("d-ladmm_amd.ops")
+    K, m, n, B = 2, 8, 16, 5
+    E = torch.zeros(K, m, B)
+    L = torch.zeros(K, m, B)
+    A = torch.zeros(m, n)
+    with pytest.raises(ValueError, match="X must be"):
+        ops.dladmm_lena(torch.zeros(m, B + 1), A, E, L, 0.45, B)
+    with pytest.raises(ValueError, match="X must be"):
+        ops.dladmm_lena(torch.zeros(m, B), torch.zeros(m + 1, n), E, L, 0.45, B)
+    with pytest.raises(ValueError, match="one GPU"):
+        ops.dladmm_lena(torch.zeros(m, B), A, E, L, 0.45, B)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("variant", ["v1", "v4"])
 def test_lena_column_shards_sum_to_full_batch(variant, dl):
@@ -278,3 +295,21 @@ def test_lena_upstream_scale_and_eval(dl):
     for k, p in net.named_parameters():
         g, r = p.grad.double(), 2.0 * g1[k].double()
         assert float((g - r).norm()) <= 1e-6 * float(r.norm()), k
+
+
+@pytest.mark.gpu
+def test_lena_empty_batch(dl):
+    """B = 0 (the reference's ops on an empty batch give zero sums): zero sums and empty
+    cotangents, no launch."""
+    from importlib import import_module
+    ops = import_module("d-ladmm_amd.ops")
+    K, m, n = 3, 16, 32
+    dev = torch.device("cuda", 0)
+    E = torch.zeros(K, m, 0, device=dev)
+    L = torch.zeros(K, m, 0, device=dev)
+    X = torch.zeros(m, 0, device=dev)
+    A = torch.randn(m, n, device=dev)
+    sm = ops.dladmm_lena(X, A, E, L, 0.45, 1.0)
+    assert sm.shape == (K, 4) and not sm.any()
+    sm, gE, gL = ops.dladmm_lena(X, A, E, L, 0.45, 1.0, coef=torch.ones(K, device=dev))
+    assert not sm.any() and gE.shape == (K, m, 0) and gL.shape == (K, m, 0)
