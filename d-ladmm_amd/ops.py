@@ -312,7 +312,7 @@ def dladmm_scale_(x: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
     """x *= s in place (s: a one-element fp32 device tensor) through dladmm_scale_f32, which skips
     the pass on the device when s == 1 -- no host synchronisation."""
     if x.dtype != torch.float32 or not x.is_contiguous() or s.dtype != torch.float32 or \
-            s.numel() != 1 or s.device != x.device:
+            s.numel() != 1 or s.device != x.device or x.device.type != "cuda":
         raise ValueError("dladmm: scale needs a contiguous fp32 tensor and an fp32 device scalar")
     s = s.contiguous()
     stream = torch.cuda.current_stream(x.device).cuda_stream
