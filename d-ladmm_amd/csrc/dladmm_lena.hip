@@ -36,35 +36,46 @@ namespace dladmm {
 // dual_gap(y, a) = softplus(y - a) + softplus(-y - a) = ln((1 + e^(y-a)) (1 + e^(-y-a)))
 //                 = ln(c1 + c2 (e^y + e^-y)),  c1 = 1 + e^-2a, c2 = e^-a,
 // and its derivative softplus'(y - a) - softplus'(-y - a) = (e^y - e^-y) / (e^y + e^-y + c3),
-// c3 = e^a + e^-a: two transcendentals less per element than the four softplus terms, no
-// cancellation in the log (its argument is >= 1).  Past |y| = 30 they are |y| - a and sgn(y)
-// (what torch's softplus threshold of 20 gives to fp32 precision).  Hardware v_exp_f32 /
+// c3 = e^a + e^-a.  With t = e^|y| (>= 1) both need ONE exponential:
+//   dual_gap = ln(c2 t^2 + c1 t + c2) - |y|,   derivative = sgn(y) (t^2 - 1) / (t^2 + c3 t + 1)
+// -- exp + log for the value, exp + rcp for the derivative, exp + log + rcp for both (the
+// e^y, e^-y form needed one transcendental more each); no cancellation in the log (its
+// argument is >= c2 (1 + t)^2 > 0) and t^2 - 1 as one fma, so the derivative near y = 0 is as
+// exact as t.  Past |y| = 30 they are |y| - a and sgn(y) (what torch's softplus threshold of 20
+// gives to fp32 precision; t^2 may overflow there and is discarded).  Hardware v_exp_f32 /
 // v_log_f32 / v_rcp_f32 (~1 ulp each): within ~1e-7 of the torch values, relative to the
 // terms' scale; branch-free (selects), so no lane diverges around the transcendental work.
+// dual_gap and dual_gap_vd (dual_gap_d and dual_gap_vd) form the value (the derivative) by the
+// same operations, so modes 0, 1 and 2 agree bit for bit.
 struct Gap { float a, c1, c2, c3; };
 __device__ __forceinline__ float exp_h(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
+__device__ __forceinline__ float gap_v(float t, float ay, const Gap& G) {
+  return 0.693147180559945309f * __builtin_amdgcn_logf(fmaf(fmaf(G.c2, t, G.c1), t, G.c2)) - ay;
+}
+__device__ __forceinline__ float gap_d(float t, const Gap& G) {
+  return fmaf(t, t, -1.0f) * __builtin_amdgcn_rcpf(fmaf(t + G.c3, t, 1.0f));
+}
 __device__ __forceinline__ float dual_gap(float y, const Gap& G) {
-  const float e = exp_h(y), ei = __builtin_amdgcn_rcpf(e);
-  float v = 0.693147180559945309f * __builtin_amdgcn_logf(G.c1 + G.c2 * (e + ei));
-  asm("" : "+v"(v));  // computed on every lane: the select below must not become a branch
   const float ay = fabsf(y);
+  float v = gap_v(exp_h(ay), ay, G);
+  asm("" : "+v"(v));  // computed on every lane: the select below must not become a branch
   return ay > 30.0f ? ay - G.a : v;
 }
-// both at once (mode 2): the two share e^y and e^-y
+// both at once (mode 2): they share t
 __device__ __forceinline__ void dual_gap_vd(float y, const Gap& G, float& val, float& der) {
-  const float e = exp_h(y), ei = __builtin_amdgcn_rcpf(e);
-  float v = 0.693147180559945309f * __builtin_amdgcn_logf(G.c1 + G.c2 * (e + ei));
-  float d = (e - ei) * __builtin_amdgcn_rcpf((e + ei) + G.c3);
-  asm("" : "+v"(v), "+v"(d));
   const float ay = fabsf(y);
+  const float t = exp_h(ay);
+  float v = gap_v(t, ay, G);
+  float d = gap_d(t, G);
+  asm("" : "+v"(v), "+v"(d));
   val = ay > 30.0f ? ay - G.a : v;
-  der = ay > 30.0f ? copysignf(1.0f, y) : d;
+  der = copysignf(ay > 30.0f ? 1.0f : d, y);
 }
 __device__ __forceinline__ float dual_gap_d(float y, const Gap& G) {
-  const float e = exp_h(y), ei = __builtin_amdgcn_rcpf(e);
-  float v = (e - ei) * __builtin_amdgcn_rcpf((e + ei) + G.c3);
-  asm("" : "+v"(v));
-  return fabsf(y) > 30.0f ? copysignf(1.0f, y) : v;
+  const float ay = fabsf(y);
+  float d = gap_d(exp_h(ay), G);
+  asm("" : "+v"(d));
+  return copysignf(ay > 30.0f ? 1.0f : d, y);
 }
 
 // Static VM-operation counts of one layer body, for the counted ring barriers (the scheme of the
