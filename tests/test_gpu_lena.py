@@ -313,3 +313,37 @@ def test_lena_empty_batch(dl):
     assert sm.shape == (K, 4) and not sm.any()
     sm, gE, gL = ops.dladmm_lena(X, A, E, L, 0.45, 1.0, coef=torch.ones(K, device=dev))
     assert not sm.any() and gE.shape == (K, m, 0) and gL.shape == (K, m, 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scale", [1.0, 40.0])
+def test_lena_op_vs_fp64_incl_large_arguments(dl, scale):
+    """dladmm_lena (mode 2) against fp64 torch: the four sums and the E / L cotangents, with L
+    scaled so that many |A^T L| and |L| pass 30 (the linear branch; e^|y| squared overflows there
+    and must be discarded by the select, not leak as inf / NaN)."""
+    from importlib import import_module
+    ops = import_module("d-ladmm_amd.ops")
+    dev = torch.device("cuda", 0)
+    K, m, n, B = 2, 64, 256, 37
+    g = torch.Generator().manual_seed(4431)
+    X = torch.randn(m, B, generator=g, dtype=torch.float64)
+    A = torch.randn(m, n, generator=g, dtype=torch.float64) / 8
+    E = torch.randn(K, m, B, generator=g, dtype=torch.float64) * 0.1
+    E[:, :3] = 0.0   # sgn(0) = 0
+    L = torch.randn(K, m, B, generator=g, dtype=torch.float64) * scale
+    X, A, E, L = (t.float().double() for t in (X, A, E, L))  # the fp32 operands, exactly
+    c = torch.tensor([0.6, 1.0], dtype=torch.float64)
+    f = lambda t: t.float().to(dev)  # noqa: E731
+    sm, gE, gL = ops.dladmm_lena(f(X), f(A), f(E), f(L), ALPHA, B, coef=f(c))
+    Xd, Ad = X, A
+    Ed, Ld = E.clone().requires_grad_(True), L.clone().requires_grad_(True)
+    Y = torch.einsum("mn,kmb->knb", Ad, Ld)
+    ref = torch.stack([Ed.abs().sum((1, 2)), dual_gap(Y, ALPHA).sum((1, 2)),
+                       dual_gap(Ld, 1).sum((1, 2)), (Ld * Xd).sum((1, 2))], 1)
+    assert torch.isfinite(sm).all() and torch.isfinite(gE).all() and torch.isfinite(gL).all()
+    sc = ref.detach().abs().sum(0)  # per-term scale
+    assert float(((sm.cpu() - ref.detach()).abs().max(0).values / sc).max()) <= 1e-5
+    loss = (c * (ref[:, 0] / (m * B) + ref[:, 1] / (n * B) + (ref[:, 2] + ref[:, 3]) / (m * B))).sum()
+    loss.backward()
+    assert nrel(gE.cpu(), Ed.grad) <= 1e-5
+    assert nrel(gL.cpu(), Ld.grad) <= 1e-5
