@@ -597,13 +597,49 @@ def world_check(gpus, environ=None):
     return None
 
 
+def visible_gpu_count(environ=None, kfd="/sys/class/kfd/kfd/topology/nodes"):
+    """GPUs this process could use, counted WITHOUT any HIP or torch.cuda call (the launcher
+    parent must not initialise the runtime: torch.cuda.device_count() falls back to
+    hipGetDeviceCount when amdsmi is not importable).  The KFD topology lists one node per agent;
+    GPU nodes have a non-zero simd_count.  A *_VISIBLE_DEVICES list narrows the count the way
+    the runtime applies it (ROCR first, then HIP / CUDA on top).  None when the topology is
+    unreadable (no KFD driver: the ranks' own start-up then decides)."""
+    environ = os.environ if environ is None else environ
+    try:
+        nodes = sorted(int(d) for d in os.listdir(kfd) if d.isdigit())
+    except OSError:
+        return None
+    gpus = 0
+    for nd in nodes:
+        try:
+            props = open(os.path.join(kfd, str(nd), "properties")).read().split("\n")
+        except OSError:
+            continue
+        for ln in props:
+            kv = ln.split()
+            if len(kv) == 2 and kv[0] == "simd_count" and kv[1].isdigit() and int(kv[1]) > 0:
+                gpus += 1
+                break
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = environ.get(var)
+        if not v:   # unset or empty: no narrowing (the ranks' own start-up decides)
+            continue
+        ids = [x for x in v.split(",") if x.strip() != ""]
+        gpus = min(gpus, len(ids))
+    return gpus
+
+
 def self_launch(argv, n) -> int:
     """Start n ranks (see above); print rank 0's JSON line; return the launcher's exit status."""
     import subprocess
     backend = os.environ.get("DLADMM_BENCH_BACKEND", "nccl")
-    if backend == "nccl" and "--launch-selftest" not in argv:
-        have = torch.cuda.device_count()   # counts devices without initialising HIP here
-        if have < n:
+    # DLADMM_KFD_TOPOLOGY points the count at another topology tree (the CPU tests' fake one);
+    # the self-test ranks touch no device, so without it they skip the count
+    topo = os.environ.get("DLADMM_KFD_TOPOLOGY")
+    if backend == "nccl" and ("--launch-selftest" not in argv or topo):
+        # from the KFD topology: no HIP call in this process
+        have = visible_gpu_count(kfd=topo) if topo else visible_gpu_count()
+        if have is not None and have < n:
             print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
             return 2
     cmd, env = launch_plan(argv, n, free_port())

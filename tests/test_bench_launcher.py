@@ -67,6 +67,65 @@ def test_self_launch_spawns_n_gloo_ranks():
     assert r["n_gpus"] == 3 and r["rank_sum"] == 3.0 and r["ranks"] == [0, 1, 2]
 
 
+def _fake_topology(root, gpus, cpus=1):
+    """A KFD topology tree: `cpus` CPU agents (simd_count 0), then `gpus` GPU agents."""
+    for i in range(cpus + gpus):
+        d = root / str(i)
+        d.mkdir(parents=True)
+        simd = 0 if i < cpus else 1024
+        (d / "properties").write_text(f"cpu_cores_count 8\nsimd_count {simd}\nmax_waves_per_simd 8\n")
+    return str(root)
+
+
+def test_visible_gpu_count_from_topology(tmp_path):
+    b = _bench()
+    topo = _fake_topology(tmp_path / "nodes", gpus=8, cpus=2)
+    assert b.visible_gpu_count({}, kfd=topo) == 8
+    assert b.visible_gpu_count({"HIP_VISIBLE_DEVICES": "0,1,2"}, kfd=topo) == 3
+    assert b.visible_gpu_count({"ROCR_VISIBLE_DEVICES": "4", "HIP_VISIBLE_DEVICES": "0"},
+                               kfd=topo) == 1
+    assert b.visible_gpu_count({"CUDA_VISIBLE_DEVICES": ""}, kfd=topo) == 8
+    assert b.visible_gpu_count({}, kfd=str(tmp_path / "absent")) is None
+
+
+# the launcher parent under test: every way torch could reach hipGetDeviceCount raises, so a
+# launcher that initialises HIP (VERDICT r04 #6) fails the test
+_NO_HIP = r"""
+import runpy, sys, torch
+def _boom(*a, **k):
+    raise RuntimeError("launcher parent called the HIP runtime")
+torch._C._cuda_getDeviceCount = _boom
+torch.cuda.device_count = _boom
+torch.cuda.is_available = _boom
+torch.cuda.init = _boom
+sys.argv = [sys.argv[1]] + sys.argv[2:]
+runpy.run_path(sys.argv[0], run_name="__main__")
+"""
+
+
+def test_launcher_parent_never_calls_hip(tmp_path):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("DLADMM_BENCH_BACKEND", None)
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        env.pop(var, None)
+    # too few GPUs in the topology: refused before any rank starts, without a HIP call
+    env["DLADMM_KFD_TOPOLOGY"] = _fake_topology(tmp_path / "two", gpus=2)
+    p = subprocess.run([sys.executable, "-c", _NO_HIP, BENCH, "--gpus", "3",
+                        "--launch-selftest"], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 2, p.stderr[-2000:]
+    assert "only 2 GPU(s) visible" in p.stderr and "HIP runtime" not in p.stderr
+    # enough GPUs: the three ranks start and report
+    env["DLADMM_KFD_TOPOLOGY"] = _fake_topology(tmp_path / "four", gpus=4)
+    p = subprocess.run([sys.executable, "-c", _NO_HIP, BENCH, "--gpus", "3",
+                        "--launch-selftest"], env=env, capture_output=True, text=True,
+                       timeout=180)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and json.loads(lines[0])["ranks"] == [0, 1, 2]
+
+
 def test_granted_cores_rules(monkeypatch, tmp_path):
     """cpu_baseline's thread count: the cgroup quota when set, else OMP_NUM_THREADS, else the
     affinity -- never more than the affinity."""
