@@ -111,7 +111,7 @@ class LenaDesc(ctypes.Structure):
     _fields_ = [
         ("abi_version", _i32), ("m", _i32), ("n", _i32), ("batch", _i32), ("layers", _i32),
         ("mode", _i32), ("alpha", ctypes.c_float), ("inv_mb", ctypes.c_float),
-        ("inv_nb", ctypes.c_float), ("pad0", _i32),
+        ("inv_nb", ctypes.c_float), ("lx_negate", _i32),
         ("X", _fp), ("ld_x", _i64), ("A", _fp), ("ld_a", _i64),
         ("E", _fp), ("L", _fp), ("layer_stride", _i64), ("ld", _i64),
         ("sums", _fp),

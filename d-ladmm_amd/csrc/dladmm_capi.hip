@@ -1260,6 +1260,7 @@ inline int lena_plan(const dladmm_lena_desc* d, LenaPlan* p) {
   if (d->m < 1 || d->n < 1 || d->batch < 1) return DLADMM_E_SHAPE;
   if (d->layers < 1 || d->layers > 65535) return DLADMM_E_LAYERS;  // grid.y
   if (d->mode < 0 || d->mode > 2) return DLADMM_E_UNSUPPORTED;
+  if (d->lx_negate != 0 && d->lx_negate != 1) return DLADMM_E_UNSUPPORTED;
   if (!d->X || !d->A || !d->E || !d->L) return DLADMM_E_NULL;
   if (d->mode != 1 && !d->sums) return DLADMM_E_NULL;
   if (d->mode != 0 && (!d->gE || !d->gL || !d->coef)) return DLADMM_E_NULL;
@@ -1270,17 +1271,23 @@ inline int lena_plan(const dladmm_lena_desc* d, LenaPlan* p) {
     if (d->ld_g < B) return DLADMM_E_SHAPE;
     if (d->layers > 1 && d->g_layer_stride < (int64_t)d->m * d->ld_g) return DLADMM_E_SHAPE;
   }
-  const int64_t lim = (int64_t)1 << 31;  // 32-bit buffer offsets per layer
-  if ((int64_t)d->m * d->ld * 4 >= lim || (int64_t)d->m * d->ld_x * 4 >= lim ||
-      (d->mode != 0 && (int64_t)d->m * d->ld_g * 4 >= lim))
-    return DLADMM_E_UNSUPPORTED;
   const int s = pick_shape(d->m, d->n);
   if (s < 0) return DLADMM_E_UNSUPPORTED;
+  // 32-bit buffer offsets per layer.  The kernel walks the instantiation's padded rows
+  // (kShapeMP[s] >= m), and a lane outside the batch starts at kOOB = 2^31 plus the row offset:
+  // that sum must stay below 2^32 to land out of range, so the padded extent is what is bounded
+  // (ADVICE r04).  The same holds for the loss-partial rows (4K rows of ldl floats).
+  const int64_t lim = (int64_t)1 << 31;
+  const int64_t MPs = kShapeMP[s];
+  if (MPs * d->ld * 4 >= lim || MPs * d->ld_x * 4 >= lim ||
+      (d->mode != 0 && MPs * d->ld_g * 4 >= lim))
+    return DLADMM_E_UNSUPPORTED;
   p->shape = s;
   p->MP = kShapeMP[s];
   p->NP = kShapeNP[s];
   p->tiles = ceil_div(d->batch, kTileCols);
   p->ldl = p->tiles * kTileCols;
+  if (d->mode != 1 && (int64_t)16 * d->layers * p->ldl >= lim) return DLADMM_E_UNSUPPORTED;
   const size_t fb = (size_t)p->MP * p->NP * sizeof(float);
   p->off_ap = 0;
   p->off_atp = align256(fb);
@@ -1318,6 +1325,7 @@ int dladmm_lena_f32(const dladmm_lena_desc* d, void* stream) {
   LenaArgs a{};
   a.m = d->m; a.n = d->n; a.B = d->batch; a.K = d->layers; a.mode = d->mode; a.ldl = p.ldl;
   a.alpha = d->alpha; a.inv_mb = d->inv_mb; a.inv_nb = d->inv_nb;
+  a.xsign = d->lx_negate ? -1.0f : 1.0f;
   for (int i = 0; i < 2; ++i) {  // dual_gap constants (dladmm_lena.hip)
     const double c = i == 0 ? (double)d->alpha : 1.0;
     a.gc[4 * i + 0] = (float)c;

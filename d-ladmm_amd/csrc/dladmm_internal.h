@@ -229,7 +229,7 @@ hipError_t launch_reverse_shape(int shape, int variant, const RevArgs& a, int gr
 struct LenaArgs {
   int m, n, B, K, mode, ldl;
   float alpha, inv_mb, inv_nb;
-  int pad0;
+  float xsign;  // +1 / -1: the sign of X in gL (main_lena.py:226 / main_syn_l1l1-dgap_ltheta.py:205)
   float gc[8];  // dual_gap constants (a, 1 + e^-2a, e^-a, e^a + e^-a) for a = alpha, then a = 1
   const float* X; int64_t ldx;
   const float* E; const float* L; int64_t ls, ld;  // layer k at + k*ls, row stride ld

@@ -2,7 +2,7 @@
 // forward's saved layers (include/dladmm.h, dladmm_lena_f32): main_lena.py:221-228 with
 // dual_gap of :145-147,
 //   l_k = a/(nN) sum|Z_k| + 1/(mN) sum|E_k| + 1/(nN) sum dual_gap(A^T L_k, a)
-//         + 1/(mN) sum dual_gap(L_k, 1) + 1/(mN) sum L_k * X,
+//         + 1/(mN) sum dual_gap(L_k, 1) +/- 1/(mN) sum L_k * X   (- : main_syn_l1l1-dgap_ltheta.py:205),
 //   dual_gap(x, c) = softplus(x - c) + softplus(-x - c).
 // The reference builds it from the returned E_k, L_k with torch ops: K products A^T L_k (n x B
 // each, 128 MB per layer at B = 65,536) and a dozen elementwise passes over them forward, as many
@@ -373,7 +373,7 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
     } else {
       // ---- G2: G = A S, blocks (2p, 2p+1) of the m rows over kb = 0..NB-1; epilogue gL, gE
       const float c = a.coef[k];
-      const float cn = c * a.inv_nb, cm = c * a.inv_mb;
+      const float cn = c * a.inv_nb, cm = c * a.inv_mb, xsg = a.xsign;
       const uint32_t vg = cv ? (uint32_t)((col + (int64_t)(4 * g) * a.ldg) * 4) : kOOB;
       const uint32_t gbytes = (uint32_t)((int64_t)m * a.ldg * 4);
       const rsrc_t rgl = mkrsrc(a.gL + (int64_t)k * a.gls, gbytes);
@@ -412,7 +412,7 @@ __global__ __launch_bounds__(256, 1) void lena_kernel(const LenaArgs a) {
                 } else {
                   dl = dual_gap_d(l, G1c);
                 }
-                base[h][r] = cm * (dl + xv[r]);
+                base[h][r] = cm * (dl + xsg * xv[r]);  // xsg = +-1: exact
                 gsg[h][r] = cm * ((e > 0.f ? 1.f : 0.f) - (e < 0.f ? 1.f : 0.f));
               }
             }

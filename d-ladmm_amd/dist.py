@@ -43,10 +43,14 @@ def allreduce_grads(module: torch.nn.Module, group: Optional[dist.ProcessGroup] 
     n x m plus per-layer scalars), then scattered back.  With `training_loss(..., batch=B_global)`
     each rank's gradient is its shard's share of the global-batch objective, so SUM (the default)
     gives the full-batch gradient; `average=True` divides by the world size instead (losses
-    normalised by the local batch)."""
+    normalised by the local batch).
+    Rank-local parameters -- V1's per-sample betas of a module made a batch shard by
+    `shard_batch_` (main_lena.py:35-36: one column per sample) -- are not in the bucket: their
+    gradient is already complete on the rank that holds those columns."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return
-    ps = [p for p in module.parameters() if p.grad is not None]
+    ps = [p for p in module.parameters()
+          if p.grad is not None and not getattr(p, "_dladmm_rank_local", False)]
     if not ps:
         return
     flat = torch.cat([p.grad.reshape(-1) for p in ps])
@@ -58,3 +62,32 @@ def allreduce_grads(module: torch.nn.Module, group: Optional[dist.ProcessGroup] 
         n = p.grad.numel()
         p.grad.copy_(flat[o:o + n].view_as(p.grad))
         o += n
+
+
+def gather_state_dict(module: torch.nn.Module, group: Optional[dist.ProcessGroup] = None):
+    """The reference-layout state_dict of a batch-sharded module (`shard_batch_`), for saving
+    (main_lena.py:243 `torch.save(model.state_dict(), ...)`): every rank-local per-sample beta
+    is all-gathered along its columns back to (m, batch_size); replicated entries are this
+    rank's (equal on every rank).  A collective: every rank calls it.  Unsharded modules (or one
+    rank) return their own state_dict."""
+    sd = module.state_dict()
+    shard = getattr(module, "batch_shard", None)
+    if shard is None:
+        return sd
+    c0, c1, B = shard
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    local = {f"{nm}.{k}" for nm in module._elem_names() for k in range(module.layers)}
+    if world == 1:
+        if c1 - c0 != B:
+            raise RuntimeError("dladmm: a batch shard needs its process group to gather")
+        return sd
+    spans = [shard_columns(B, r, world) for r in range(world)]
+    wmax = max(b - a for a, b in spans)
+    for key in sorted(local):
+        v = sd[key]
+        pad = torch.zeros((v.shape[0], wmax), dtype=v.dtype, device=v.device)
+        pad[:, :v.shape[1]] = v
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad, group=group)
+        sd[key] = torch.cat([p[:, :b - a] for p, (a, b) in zip(parts, spans)], 1)
+    return sd

@@ -61,6 +61,7 @@ class _DLADMMBase(nn.Module):
         self.E0 = _dev(E0)
         self.L0 = _dev(L0)
         self.layers = layers
+        self.batch_shard = None   # (c0, c1, batch_size) after shard_batch_ (data parallel)
         self._register_params()
         self._init_fc()
         # the reference follows construction with model.cuda() (main_lena.py:191); do it here
@@ -90,6 +91,67 @@ class _DLADMMBase(nn.Module):
 
     def name(self):
         return self.NAME
+
+    # --- data parallelism ----------------------------------------------
+    def _elem_param_lists(self) -> list:
+        """The ParameterLists whose entries are per-sample (m, batch_size): V1's beta1 / beta2
+        (main_lena.py:35-36).  Other variants: none (their parameters are replicated)."""
+        return []
+
+    def shard_batch_(self, rank: int, world: int):
+        """Make this module rank `rank`'s share of a data-parallel run over `world` ranks (in
+        place): it keeps only its contiguous column span c0:c1 = dist.shard_columns(batch_size,
+        rank, world) of everything that is per sample -- Z0, E0, L0 and V1's per-sample betas
+        (main_lena.py:35-36), which become (m, c1 - c0) Parameters holding their current values'
+        columns and are marked rank-local.  Then:
+          * forward / training_loss take the rank's (m, c1 - c0) shard of X; training_loss's
+            mean runs over the global batch_size by default, so the ranks' gradients SUM to the
+            whole batch's;
+          * dist.allreduce_grads all-reduces only the replicated parameters (W_k, scalar and
+            per-row ones): a per-sample beta's gradient is rank-local;
+          * load_state_dict slices a global checkpoint's (m, batch_size) betas to the span, and
+            dist.gather_state_dict assembles the reference layout again for saving.
+        Per rank, V1's betas then cost 2 K m (B / world) floats instead of 2 K m B.  Returns
+        self."""
+        from .dist import shard_columns
+        if self.batch_shard is not None:
+            raise RuntimeError("dladmm: the module is already a batch shard")
+        B = self.Z0.shape[1]
+        for pl in self._elem_param_lists():
+            if any(q.shape[1] != B for q in pl):
+                raise ValueError("dladmm: per-sample parameters and Z0 disagree on the batch")
+        c0, c1 = shard_columns(B, rank, world)
+        self.Z0 = self.Z0[:, c0:c1].contiguous()
+        self.E0 = self.E0[:, c0:c1].contiguous()
+        self.L0 = self.L0[:, c0:c1].contiguous()
+        for pl in self._elem_param_lists():
+            for i in range(len(pl)):
+                p = nn.Parameter(pl[i].detach()[:, c0:c1].contiguous(),
+                                 requires_grad=pl[i].requires_grad)
+                p._dladmm_rank_local = True
+                pl[i] = p
+        self.batch_shard = (c0, c1, B)
+        self.world = (rank, world)
+        return self
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        """nn.Module.load_state_dict; on a batch shard (shard_batch_) a per-sample beta given in
+        the global (m, batch_size) layout of a reference checkpoint is sliced to the shard's
+        columns first."""
+        if self.batch_shard is not None:
+            c0, c1, B = self.batch_shard
+            names = {f"{nm}.{k}" for nm in self._elem_names() for k in range(self.layers)}
+            sd = OrderedDict(state_dict)
+            for key in names & set(sd):
+                v = sd[key]
+                if torch.is_tensor(v) and v.dim() == 2 and v.shape[1] == B and c1 - c0 != B:
+                    sd[key] = v[:, c0:c1]
+            state_dict = sd
+        return super().load_state_dict(state_dict, strict=strict, assign=assign)
+
+    def _elem_names(self) -> list:
+        return [nm for nm, mod in self.named_children() if any(mod is pl for pl in
+                                                               self._elem_param_lists())]
 
     # --- fused forward ----------------------------------------------------------------
     def _weights(self) -> List[torch.Tensor]:
@@ -184,7 +246,8 @@ class _DLADMMBase(nn.Module):
         return r, obj
 
     def training_loss(self, x, alpha: float, coeffs=None, kind: str = "l1l1",
-                      batch: Optional[int] = None, cols=None):
+                      batch: Optional[int] = None, cols=None, lx_sign: float = 1.0,
+                      save_cotangents: bool = True):
         """The reference training objective as one fused, differentiable op:
             total = sum_k coeffs[k] * (alpha * sum(|Z_k|,0).mean() + sum(|X - A Z_k|,0).mean())
         (main_syn_l1l1_scalar.py:283-296; kind='lasso': 0.5*sum((X - A Z_k)^2,0), lasso
@@ -192,8 +255,14 @@ class _DLADMMBase(nn.Module):
             l_k = alpha*mean|Z_k| + mean|E_k| + mean(dual_gap(A^T L_k, alpha))
                   + mean(dual_gap(L_k, 1)) + mean(L_k * X),
         dual_gap(x, c) = softplus(x - c) + softplus(-x - c) (:145-147), the means over all
-        elements; m <= 256, n <= 512).  coeffs default: all 1; the reference uses decay
-        0.6**epoch for k < K-1.
+        elements; m <= 256, n <= 512; lx_sign=-1 gives main_syn_l1l1-dgap_ltheta.py:201-207's
+        `- mean(L_k * X)`, whose loop also zeroes the layers below loss_start_layer = layers - 1:
+        coeffs [0, ..., 0, 1]).  coeffs default: all 1; the reference uses decay 0.6**epoch
+        for k < K-1.
+        kind='lena' keeps, between forward and backward, the E_k / L_k cotangents the training
+        forward forms in the same pass as the sums (2 K m B fp32 beside the saved layers, outside
+        save_for_backward: saved-tensor hooks do not see them); save_cotangents=False forms them
+        in the backward instead (one more pass over the K products A^T L_k).
         Returns (total, per-layer losses [K]); call total.backward() as the reference does.
         Mathematically the same gradients as building the loss from forward()'s outputs with
         torch ops, without the K products A Z_k.
@@ -209,6 +278,11 @@ class _DLADMMBase(nn.Module):
             raise ValueError(f"dladmm: coeffs must have {K} entries")
         if kind not in ("l1l1", "lasso", "lena"):
             raise ValueError(f"dladmm: unknown loss kind {kind!r}")
+        if cols is not None and self.batch_shard is not None:
+            raise ValueError("dladmm: cols= slices a replicated model; a batch shard "
+                             "(shard_batch_) takes its own columns' x directly")
+        if batch is None and self.batch_shard is not None:
+            batch = self.batch_shard[2]   # the mean over the global batch
         if cols is not None:
             cols = (int(cols[0]), int(cols[1]))
             # an empty shard (c0 == c1: dist.shard_columns when the batch has fewer columns
@@ -219,10 +293,23 @@ class _DLADMMBase(nn.Module):
                                  f"model's batch of {self.Z0.shape[1]} columns")
         denom = float(batch if batch is not None else x.shape[1])
         if kind == "lena":
-            if x.requires_grad:
-                raise RuntimeError("dladmm: gradients w.r.t. the input X are not supported")
-            return _DLADMMLenaLossFunction.apply(self, x, coeffs, float(alpha), denom, cols,
-                                                 *self.parameters())
+            lx_sign = float(lx_sign)
+            if lx_sign not in (1.0, -1.0):
+                raise ValueError(f"dladmm: lx_sign must be +1 or -1 (got {lx_sign})")
+            if self._needs_grad():
+                if x.requires_grad:
+                    raise RuntimeError("dladmm: gradients w.r.t. the input X are not supported")
+                return _DLADMMLenaLossFunction.apply(self, x, coeffs, float(alpha), denom, cols,
+                                                     lx_sign, bool(save_cotangents),
+                                                     *self.parameters())
+            # evaluation: the module's own precision, nothing saved, the sums only (mode 0)
+            with torch.no_grad():
+                r = self._run_shard(x, cols, loss_kind=_lib.LOSS_L1L1, want_T=False)
+                sums = dladmm_lena(x, self.A, r.E, r.L, float(alpha), denom, lx_sign=lx_sign)
+                per_layer = _lena_per_layer(r.loss_sums, sums, float(alpha), self.A.shape,
+                                            denom, lx_sign)
+                c = _coef_tensor(coeffs, per_layer.device)
+                return (c * per_layer).sum().to(torch.float32), per_layer.to(torch.float32)
         if self._needs_grad():
             if x.requires_grad:
                 raise RuntimeError("dladmm: gradients w.r.t. the input X are not supported")
@@ -453,7 +540,7 @@ class _DLADMMLenaLossFunction(torch.autograd.Function):
     Outputs: total (0-dim) and the per-layer losses [K] (non-differentiable)."""
 
     @staticmethod
-    def forward(ctx, mod, x, coeffs, alpha, denom, cols, *params):
+    def forward(ctx, mod, x, coeffs, alpha, denom, cols, lx_sign, save_cot, *params):
         dev = mod.A.device
         tables = mod._tables(dev, cols)
         W = [w.detach() for w in mod._weights()]
@@ -461,22 +548,22 @@ class _DLADMMLenaLossFunction(torch.autograd.Function):
         r = dladmm_forward(mod.VARIANT, x, mod.A, W, Z0, E0, L0, keep_all=True, want_T=True,
                            loss_kind=_lib.LOSS_L1L1, want_P=True, precision=_train_precision(mod),
                            **tables)
-        m, n = mod.A.shape
         c = _coef_tensor(coeffs, dev)
         c32 = c.to(torch.float32)
-        ctx.grad = any(ctx.needs_input_grad[6:])
-        if ctx.grad:
+        ctx.grad = any(ctx.needs_input_grad[8:])
+        if ctx.grad and save_cot:
             # a training forward: the sums and the cotangents of sum_k c_k l_k in one pass
             # (mode 2); the backward scales the cotangents by its upstream gradient
-            sums, gE, gL = dladmm_lena(x, mod.A, r.E, r.L, alpha, denom, coef=c32)
+            sums, gE, gL = dladmm_lena(x, mod.A, r.E, r.L, alpha, denom, coef=c32,
+                                       lx_sign=lx_sign)
         else:
-            sums = dladmm_lena(x, mod.A, r.E, r.L, alpha, denom)  # fp64 (K, 4)
+            # the sums only (mode 0); a backward forms the cotangents itself (mode 1)
+            sums = dladmm_lena(x, mod.A, r.E, r.L, alpha, denom, lx_sign=lx_sign)
             gE = gL = None
-        per_layer = (alpha * r.loss_sums[:, 0] / n + sums[:, 1] / n +
-                     (sums[:, 0] + sums[:, 2] + sums[:, 3]) / m) / denom
+        per_layer = _lena_per_layer(r.loss_sums, sums, alpha, mod.A.shape, denom, lx_sign)
         total = (c * per_layer).sum().to(torch.float32)
         ctx.mod, ctx.tables, ctx.W, ctx.cols = mod, tables, W, cols
-        ctx.alpha, ctx.denom = alpha, denom
+        ctx.alpha, ctx.denom, ctx.lx_sign = alpha, denom, lx_sign
         ctx.c = c32
         ctx.gEL = (gE, gL)
         ctx.save_for_backward(x, r.Z, r.E, r.L, r.T, r.P)
@@ -496,7 +583,8 @@ class _DLADMMLenaLossFunction(torch.autograd.Function):
         if gE is None:
             # a second backward through a retained graph: the first scaled the forward's
             # cotangents in place, so form them again (mode 1)
-            gE, gL = dladmm_lena(x, mod.A, E, L, ctx.alpha, ctx.denom, coef=ctx.c, sums=False)
+            gE, gL = dladmm_lena(x, mod.A, E, L, ctx.alpha, ctx.denom, coef=ctx.c, sums=False,
+                                 lx_sign=ctx.lx_sign)
         g1 = g_total.to(torch.float32).reshape(1).contiguous()
         dladmm_scale_(gE, g1)   # a launch that returns at once for total.backward()'s 1
         dladmm_scale_(gL, g1)
@@ -512,7 +600,16 @@ class _DLADMMLenaLossFunction(torch.autograd.Function):
         reach = {"z": [True] * K, "e": [True] * K, "l": [True] * K}
         grads = mod._param_grads(res, K, reach, ctx.cols)
         names = [n_ for n_, _ in mod.named_parameters()]
-        return (None,) * 6 + tuple(grads.get(n_) for n_ in names)
+        return (None,) * 8 + tuple(grads.get(n_) for n_ in names)
+
+
+def _lena_per_layer(loss_sums, sums, alpha, shape, denom, lx_sign):
+    """fp64 [K] per-layer values of main_lena.py:221-228 from the forward's sum|Z_k| (loss_sums
+    [:, 0]) and dladmm_lena's four sums (|E_k|, dual_gap(A^T L_k, alpha), dual_gap(L_k, 1),
+    L_k X); lx_sign -1: main_syn_l1l1-dgap_ltheta.py:205."""
+    m, n = shape
+    return (alpha * loss_sums[:, 0] / n + sums[:, 1] / n +
+            (sums[:, 0] + sums[:, 2] + lx_sign * sums[:, 3]) / m) / denom
 
 
 def _reachable(K: int, g, has_t: bool) -> dict:
@@ -613,6 +710,9 @@ class DLADMMNet(_DLADMMBase):
     def _table_spec(self):
         return {"scalar": dict(thz=self.active_para.float(), the=self.active_para1.float(),
                                s1=1.0)}
+
+    def _elem_param_lists(self) -> list:
+        return [self.beta1, self.beta2]
 
     def _elem_betas(self, cols=None):
         def sl(b):

@@ -322,16 +322,20 @@ def dladmm_scale_(x: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
 
 
 def dladmm_lena(X: torch.Tensor, A: torch.Tensor, E: torch.Tensor, L: torch.Tensor, alpha: float,
-                denom: float, coef: Optional[torch.Tensor] = None, sums: bool = True):
+                denom: float, coef: Optional[torch.Tensor] = None, sums: bool = True,
+                lx_sign: float = 1.0):
     """The fused main_lena.py objective terms over a forward's saved E_k, L_k ((K, m, B) each;
     main_lena.py:221-228 with dual_gap :145-147) through `dladmm_lena_f32` (include/dladmm.h,
     csrc/dladmm_lena.hip).  coef None (mode 0): returns the fp64 (K, 4) sums
     [sum|E_k|, sum dual_gap(A^T L_k, alpha), sum dual_gap(L_k, 1), sum L_k X].  coef = device
     fp32 (K,) (mode 1): returns the cotangents (gE, gL), each (K, m, B), of
     sum_k coef[k] * (mean|E_k| + mean dual_gap(A^T L_k, alpha) + mean dual_gap(L_k, 1)
-    + mean(L_k X)), the means over m*denom (n*denom for A^T L_k) elements; with coef and sums
-    (mode 2, one pass) returns (sums, gE, gL)."""
+    + lx_sign mean(L_k X)), the means over m*denom (n*denom for A^T L_k) elements; with coef and
+    sums (mode 2, one pass) returns (sums, gE, gL).  lx_sign: +1 main_lena.py:226, -1
+    main_syn_l1l1-dgap_ltheta.py:205 (the sums are unsigned either way)."""
     Lb = _lib.lib()
+    if lx_sign not in (1.0, -1.0):
+        raise ValueError(f"dladmm: lx_sign must be +1 or -1 (got {lx_sign})")
     K, m, B = L.shape
     n = A.shape[1]
     dev = X.device
@@ -356,6 +360,7 @@ def dladmm_lena(X: torch.Tensor, A: torch.Tensor, E: torch.Tensor, L: torch.Tens
     d.abi_version = _lib.ABI_VERSION
     d.m, d.n, d.batch, d.layers = m, n, B, K
     d.alpha = float(alpha)
+    d.lx_negate = 1 if lx_sign < 0 else 0
     d.inv_mb, d.inv_nb = 1.0 / (m * float(denom)), 1.0 / (n * float(denom))
     d.X, d.ld_x = X.data_ptr(), X.stride(0)
     d.A, d.ld_a = A.data_ptr(), A.stride(0)

@@ -235,7 +235,9 @@ size_t dladmm_bwd_workspace_bytes(const dladmm_bwd_desc* d);
 /* Which kernels the backward runs: 1 = one reverse-sweep kernel for every layer's adjoints,
    0 = per-layer kernels, <0 = DLADMM_E_* error.  The reverse sweep runs when ALL of these hold:
      - any variant V1-V6 (and the newS models built on V4 / V5);
-     - the forward ran on the fused fp32 path and saved P (fwd.P != NULL, keep_all);
+     - the forward saved P (fwd.P != NULL, keep_all): the fused fp32 path or the split-f16
+       path (precision DLADMM_PREC_F32_SPLIT), both of which store the product A Z_k their
+       E / L / T updates consumed;
      - cotangents (gZ, gE, gL, gT; any subset, any depth) only with ld_g == fwd.ld_out;
      - fwd.ld_e0 == fwd.ld_l0 == fwd.ld_out; V1: fwd.ld_beta == fwd.ld_out;
      - its 32-bit workspace offsets hold and its workspace, about
@@ -317,7 +319,7 @@ int dladmm_colobj_f32(const dladmm_colobj_desc* d, void* stream);
  * Fused main_lena.py training objective over a forward's saved layers (SURVEY.md section 8 rows
  * a11 / f1; main_lena.py:221-228, dual_gap :145-147), for any variant:
  *   l_k = alpha/(n N) sum|Z_k| + 1/(m N) sum|E_k| + 1/(n N) sum dual_gap(A^T L_k, alpha)
- *         + 1/(m N) sum dual_gap(L_k, 1) + 1/(m N) sum L_k * X,
+ *         + 1/(m N) sum dual_gap(L_k, 1) +/- 1/(m N) sum L_k * X,
  *   dual_gap(x, c) = softplus(x - c) + softplus(-x - c)   (torch softplus: beta 1, threshold 20),
  * N = the batch of the mean (a data-parallel shard passes the global batch).  The sum|Z_k| term is
  * the forward's own loss_sums[k*2+0] (loss_kind DLADMM_LOSS_L1L1); this call forms the other four
@@ -334,13 +336,16 @@ int dladmm_colobj_f32(const dladmm_colobj_desc* d, void* stream);
  * E_k and L_k (m x batch) sit at E + k*layer_stride (row stride ld), likewise the outputs (gE, gL
  * at + k*g_layer_stride, row stride ld_g).  coef: device [layers] (mode 1).  Shapes: m <= 256 and
  * n <= 512 (the fused forward's register-resident shapes); otherwise DLADMM_E_UNSUPPORTED.
+ * lx_negate: 0 = + mean(L_k X) (main_lena.py:226), 1 = - mean(L_k X)
+ * (main_syn_l1l1-dgap_ltheta.py:205-206): the sign of X in gL (modes 1, 2); sums[k*4+3] is the
+ * unsigned sum L_k X either way.
  */
 typedef struct dladmm_lena_desc {
   int32_t abi_version;
   int32_t m, n, batch, layers;
   int32_t mode;
   float alpha, inv_mb, inv_nb;
-  int32_t pad0;
+  int32_t lx_negate;                              /* 0: + mean(L_k X); 1: - mean(L_k X) */
   const float* X; int64_t ld_x;
   const float* A; int64_t ld_a;
   const float* E; const float* L; int64_t layer_stride; int64_t ld;

@@ -326,3 +326,23 @@ BF16_FIXTURES = {
     "bf16_v3": dict(variant="v3", m=96, n=200, B=24, K=6, seed=9313, perturb=0.1),
     "bf16_cfg5": dict(variant="v4", m=1024, n=4096, B=3, K=15, seed=9314, perturb=0.1),
 }
+
+
+# ------------------------------------------------ main_lena.py objective
+# Fixtures of the dual-gap training objective: the reference SCRIPT's own statements -- its
+# `dual_gap` function and the `for k in range(layers)` loss loop of its training step -- executed
+# on its own model class (tests/golden/make_golden_lena.py).  name -> forward problem, the script,
+# and the depth (the script's `layers` is set to K).
+#   main_lena.py:145-147 (dual_gap), :221-231 (loss loop, + mean(L_k X), every layer, alpha 0.45)
+#   main_syn_l1l1-dgap_ltheta.py:118-120, :196-209 (- mean(L_k X), only k >= loss_start_layer =
+#   layers - 1 (:175), alpha 0.01; V2 ltheta class at the script's own 250 x 500 shape)
+LENA_FIXTURES = {
+    "lena_v1_cfg1": dict(defn=dict(variant="v1", m=64, n=256, B=20, K=5, seed=1150, perturb=0.1,
+                                   wscale=0.4), script="main_lena.py"),
+    "lena_v1_med": dict(defn=dict(variant="v1", m=256, n=512, B=12, K=3, seed=1151, perturb=0.1,
+                                  wscale=0.4), script="main_lena.py"),
+    "lena_v1_init": dict(defn=dict(variant="v1", m=64, n=256, B=20, K=4, seed=1152),
+                         script="main_lena.py"),
+    "lena_dgap_v2": dict(defn=dict(variant="v2", m=250, n=500, B=20, K=4, seed=1153, perturb=0.1,
+                                   wscale=0.4), script="main_syn_l1l1-dgap_ltheta.py"),
+}

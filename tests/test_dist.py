@@ -205,3 +205,68 @@ def test_bench_synth_shard_is_global_slice():
     assert torch.equal(full[0], part[0])
     for f, p in zip(full[1:], part[1:]):
         assert torch.equal(f[:, 13:29], p)
+
+
+def _v1_shard_worker(rank, world, port, q):
+    """A V1 model made a batch shard (shard_batch_): betas hold the rank's columns, a global
+    checkpoint loads sliced, allreduce_grads leaves the rank-local beta gradients out of the
+    bucket, gather_state_dict restores the reference layout."""
+    import importlib
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    dl = importlib.import_module("d-ladmm_amd")
+    ddist = importlib.import_module("d-ladmm_amd.dist")
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m, n, B, K = 8, 16, 11, 3
+    g = torch.Generator().manual_seed(5)
+    A = torch.randn(m, n, generator=g)
+    mk = lambda: dl.DLADMMNet(m=m, n=0, d=n, batch_size=B, A=A,  # noqa: E731
+                              Z0=torch.rand(n, B, generator=g), E0=torch.zeros(m, B),
+                              L0=torch.zeros(m, B), layers=K)
+    torch.manual_seed(7)
+    full = mk()
+    sd_full = {k: torch.randn(v.shape, generator=g) for k, v in full.state_dict().items()}
+    full.load_state_dict(sd_full)
+    net = mk()
+    net.shard_batch_(rank, world)
+    net.load_state_dict(sd_full)            # the global checkpoint, sliced on load
+    c0, c1, Bg = net.batch_shard
+    shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+    # gradients: betas rank-local (their value = rank id), weights replicated (summed)
+    for p in net.parameters():
+        p.grad = torch.full_like(p, float(rank + 1))
+    ddist.allreduce_grads(net)
+    gb = float(net.beta1[0].grad.mean())
+    gw = float(net.fc[0].weight.grad.mean())
+    gathered = ddist.gather_state_dict(net)
+    same = all(torch.equal(gathered[k], sd_full[k]) for k in sd_full)
+    q.put((rank, (c0, c1, Bg), shapes, gb, gw, same, tuple(net.Z0.shape)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_v1_beta_shard():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_v1_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    m, n, B, K = 8, 16, 11, 3
+    assert [r[1] for r in res] == [(0, 6, 11), (6, 11, 11)]
+    for rank, (c0, c1, _), shapes, gb, gw, same, z0 in res:
+        for k in range(K):
+            assert shapes[f"beta1.{k}"] == (m, c1 - c0) == shapes[f"beta2.{k}"]
+            assert shapes[f"fc.{k}.weight"] == (n, m)
+        assert z0 == (n, c1 - c0)
+        assert gb == rank + 1.0      # not all-reduced: rank-local
+        assert gw == 3.0             # all-reduced: 1 + 2
+        assert same                  # gathered state_dict == the global checkpoint

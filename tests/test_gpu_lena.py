@@ -10,6 +10,10 @@ with torch ops, main_lena.py:221-228 with dual_gap of :145-147:
 Bar: loss values within 1e-5 (norm-relative, per layer) of fp64; every parameter gradient within
 max(GTOL, 3 x the torch-op GPU path's own distance to fp64) -- the GTOL of tests/test_gpu_backward.py
 (GEMM summation order and near-threshold shrink masks move fp32 gradients by more than rounding).
+
+The reference's own statements (tests/golden/lena_*.npz: main_lena.py's loss loop and
+main_syn_l1l1-dgap_ltheta.py's, executed on the scripts' own classes, make_golden_lena.py) pin
+the fused op directly in test_lena_vs_reference_statements.
 """
 import os
 import sys
@@ -35,15 +39,8 @@ def nrel(a, b):
     return float(np.linalg.norm(a - b) / nb) if nb > 0 else float(np.linalg.norm(a))
 
 
-def dual_gap(x, a):  # main_lena.py:145-147
-    return torch.nn.functional.softplus(x - a) + torch.nn.functional.softplus(-x - a)
-
-
-def lena_losses(Z, E, L, X, A, alpha, K):
-    """main_lena.py:221-228, one entry per layer."""
-    return [alpha * torch.mean(torch.abs(Z[k])) + torch.mean(torch.abs(E[k])) +
-            torch.mean(dual_gap(torch.mm(A.t(), L[k]), alpha)) +
-            torch.mean(dual_gap(L[k], 1)) + torch.mean(L[k] * X) for k in range(K)]
+from lena_checker import dual_gap, lena_losses  # noqa: E402  (pinned: test_oracle_lena.py)
+from conftest import load_golden  # noqa: E402
 
 
 def build(dl, defn, K):
@@ -164,6 +161,19 @@ def test_lena_descriptor_validation(dl):
     assert L.dladmm_lena_workspace_bytes(ctypes.byref(d)) == 0
     d.mode = 0
     d.ld = 50   # row stride below the batch
+    assert L.dladmm_lena_workspace_bytes(ctypes.byref(d)) == 0
+    # 32-bit offsets over the instantiation's PADDED rows: m = 200 runs on the
+    # 256-row instantiation, so ld = 2^21 + 64 passes m*ld*4 < 2^31 but not 256*ld*4
+    d.m, d.n = 200, 500
+    d.ld_a = 500
+    d.batch = d.ld = d.ld_x = (1 << 21) + 64
+    d.layer_stride = d.m * d.ld
+    assert L.dladmm_lena_workspace_bytes(ctypes.byref(d)) == 0
+    d.batch = d.ld = d.ld_x = (1 << 21) - 64 * 40
+    d.layer_stride = d.m * d.ld
+    assert L.dladmm_lena_workspace_bytes(ctypes.byref(d)) > 0
+    # loss-partial rows: 4K rows of the padded batch must stay under 2^31 bytes
+    d.layers = 300
     assert L.dladmm_lena_workspace_bytes(ctypes.byref(d)) == 0
 
 
@@ -316,15 +326,19 @@ def test_lena_empty_batch(dl):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("scale", [1.0, 40.0])
-def test_lena_op_vs_fp64_incl_large_arguments(dl, scale):
+@pytest.mark.parametrize("scale,shape", [(1.0, (64, 256, 37)), (40.0, (64, 256, 37)),
+                                         (1.0, (250, 500, 101))],
+                         ids=["64x256", "64x256-large", "250x500-ragged"])
+def test_lena_op_vs_fp64_incl_large_arguments(dl, scale, shape):
     """dladmm_lena (mode 2) against fp64 torch: the four sums and the E / L cotangents, with L
     scaled so that many |A^T L| and |L| pass 30 (the linear branch; e^|y| squared overflows there
-    and must be discarded by the select, not leak as inf / NaN)."""
+    and must be discarded by the select, not leak as inf / NaN); and a ragged shape (m, n not
+    multiples of 16, B not of 64) whose padded rows and columns must contribute nothing."""
     from importlib import import_module
     ops = import_module("d-ladmm_amd.ops")
     dev = torch.device("cuda", 0)
-    K, m, n, B = 2, 64, 256, 37
+    K = 2
+    m, n, B = shape
     g = torch.Generator().manual_seed(4431)
     X = torch.randn(m, B, generator=g, dtype=torch.float64)
     A = torch.randn(m, n, generator=g, dtype=torch.float64) / 8
@@ -347,3 +361,94 @@ def test_lena_op_vs_fp64_incl_large_arguments(dl, scale):
     loss.backward()
     assert nrel(gE.cpu(), Ed.grad) <= 1e-5
     assert nrel(gL.cpu(), Ld.grad) <= 1e-5
+
+
+LENA_NAMES = sorted(P.LENA_FIXTURES)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", LENA_NAMES)
+def test_lena_vs_reference_statements(dl, name):
+    """training_loss(kind="lena") against the reference scripts' own loss loop + backward
+    (fixtures): main_lena.py (+ mean(L X), every layer, alpha 0.45) and
+    main_syn_l1l1-dgap_ltheta.py (- mean(L X), only the last layer, alpha 0.01, V2 at 250 x 500).
+    Total and per-layer values within max(1e-5, 2 x the reference's fp32-vs-fp64 gap) of the
+    reference's fp64 run; every gradient within max(GTOL, 3 x its fp32-vs-fp64 gap) of the
+    reference's fp32 gradient (the bar of tests/test_gpu_backward.py)."""
+    g, meta = load_golden(name)
+    d = meta["defn"]
+    K = d["K"]
+    start = meta["loss_start_layer"]
+    coeffs = [0.0 if k < start else 1.0 for k in range(K)]
+    net, inp, sd = build(dl, d, K)
+    net.requires_grad_(True)
+    X = torch.from_numpy(inp["X"]).cuda()
+    tot, per = net.training_loss(X, meta["alpha"], coeffs, kind="lena", lx_sign=meta["lx_sign"])
+    tot.backward()
+    t32, t64 = (float(v) for v in g["total"])
+    assert abs(float(tot) - t64) <= max(1e-5 * abs(t64), 2 * abs(t32 - t64)), (float(tot), t64)
+    p32, p64 = g["per_layer"]
+    mine = per.detach().double().cpu().numpy()[start:]
+    e = nrel(mine, p64[start:])
+    assert e <= max(1e-5, 2 * nrel(p32[start:], p64[start:])), e
+    worst = []
+    for key, p in net.named_parameters():
+        ref = g["g:" + key]
+        gm = np.zeros_like(ref) if p.grad is None else p.grad.detach().cpu().numpy()
+        if not np.any(ref):
+            assert not np.any(gm), key
+            continue
+        err = nrel(gm, ref)
+        bar = max(GTOL, 3 * float(g["gap:" + key]))
+        worst.append((err / bar, key, err))
+        assert err <= bar, (key, err, bar)
+    worst.sort(reverse=True)
+    print(f"{name}: total {float(tot):.8g} vs ref fp64 {t64:.8g}; worst grad {worst[0]}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lx_sign", [1.0, -1.0])
+def test_lena_cotangents_in_backward_bit_equal(dl, lx_sign):
+    """save_cotangents=False (mode 0 forward, mode 1 backward: no 2 K m B cotangent buffers held
+    between forward and backward) gives the same loss and gradients bit for bit as the default
+    mode-2 forward, for either sign of the L X term."""
+    defn = dict(P.FIXTURES["v1_lena_cfg1"], B=200, seed=4441, perturb=0.1, wscale=0.4)
+    K = 3
+    net, inp, _ = build(dl, defn, K)
+    net.requires_grad_(True)
+    X = torch.from_numpy(inp["X"]).cuda()
+    res = []
+    for save in (True, False):
+        net.zero_grad(set_to_none=True)
+        tot, per = net.training_loss(X, ALPHA, [0.6, 0.6, 1.0], kind="lena", lx_sign=lx_sign,
+                                     save_cotangents=save)
+        tot.backward()
+        res.append((tot.detach(), per.detach(),
+                    {k: p.grad.clone() for k, p in net.named_parameters()}))
+    (t0, p0, g0), (t1, p1, g1) = res
+    assert torch.equal(t0, t1) and torch.equal(p0, p1)
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k
+
+
+@pytest.mark.gpu
+def test_lena_evaluation_any_precision(dl):
+    """No parameter needs a gradient: training_loss(kind="lena") evaluates at the module's
+    precision (bf16 included, which training refuses) and equals the training forward's values
+    at f32."""
+    defn = dict(P.FIXTURES["v1_lena_cfg1"], B=300, seed=4451, perturb=0.1, wscale=0.4)
+    K = 3
+    net, inp, _ = build(dl, defn, K)
+    X = torch.from_numpy(inp["X"]).cuda()
+    net.requires_grad_(True)
+    tot_t, per_t = net.training_loss(X, ALPHA, [0.6, 0.6, 1.0], kind="lena", lx_sign=-1.0)
+    net.requires_grad_(False)
+    tot_e, per_e = net.training_loss(X, ALPHA, [0.6, 0.6, 1.0], kind="lena", lx_sign=-1.0)
+    assert torch.equal(tot_e, tot_t.detach()) and torch.equal(per_e, per_t.detach())
+    net.precision = "bf16"
+    tot_b, per_b = net.training_loss(X, ALPHA, [0.6, 0.6, 1.0], kind="lena", lx_sign=-1.0)
+    assert torch.isfinite(per_b).all()
+    assert float((per_b.double() - per_e.double()).norm() / per_e.double().norm()) <= 2e-2
+    net.requires_grad_(True)
+    with pytest.raises(RuntimeError, match="inference-only"):
+        net.training_loss(X, ALPHA, [0.6, 0.6, 1.0], kind="lena")

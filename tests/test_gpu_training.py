@@ -158,3 +158,53 @@ def test_more_ranks_than_columns(variant, dl):
         if p.grad is None:
             continue
         assert nrel(ps[key].grad.cpu().numpy(), p.grad.cpu().numpy()) <= 1e-5, key
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("kind", ["l1l1", "lena"])
+def test_v1_beta_shard_matches_whole_batch(world, kind, dl):
+    """V1's per-sample betas partitioned by column (shard_batch_).  Each
+    simulated rank holds beta1/beta2 as (m, its columns), loads the GLOBAL state_dict (sliced on
+    load), and runs its shard of X; its outputs equal the whole batch's columns bit for bit, its
+    beta gradients equal the whole-batch gradient's columns, and the replicated gradients (W_k)
+    summed over the ranks -- the only all-reduced bucket -- equal the whole batch's (<= 1e-5)."""
+    K, B = 3, 97
+    inp, sd = _problem("v1", B=B, K=K)
+    X = torch.from_numpy(inp["X"]).cuda()
+    coeffs = P.loss_coeffs(K)
+    alpha = P.GRAD_ALPHA if kind == "l1l1" else 0.45
+    full = make_train_net(dl, "v1", inp, sd, K)
+    tf, pf = full.training_loss(X, alpha, coeffs, kind)
+    tf.backward()
+    with torch.no_grad():
+        full.requires_grad_(False)
+        Zf, Ef, Lf = full(X)
+        full.requires_grad_(True)
+    gsum, tot = {}, 0.0
+    m = inp["A"].shape[0]
+    for r in range(world):
+        net = make_train_net(dl, "v1", inp, sd, K).shard_batch_(r, world)
+        net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+        c0, c1, Bg = net.batch_shard
+        assert Bg == B and all(p.shape == (m, c1 - c0) for p in (*net.beta1, *net.beta2))
+        t, _ = net.training_loss(X[:, c0:c1], alpha, coeffs, kind)   # mean over B by default
+        t.backward()
+        tot += float(t)
+        for key, p in net.named_parameters():
+            gf = dict(full.named_parameters())[key].grad
+            if getattr(p, "_dladmm_rank_local", False):
+                e = nrel(p.grad.cpu().numpy(), gf[:, c0:c1].cpu().numpy())
+                assert e <= 1e-5, (r, key, e)
+            elif p.grad is not None:
+                gsum[key] = p.grad.clone() if key not in gsum else gsum[key] + p.grad
+        with torch.no_grad():
+            net.requires_grad_(False)
+            Zs, Es, Ls = net(X[:, c0:c1])
+        for a, b in zip(Zs + Es + Ls, Zf + Ef + Lf):
+            assert torch.equal(a, b[:, c0:c1])
+    np.testing.assert_allclose(tot, float(tf), rtol=1e-5)
+    for key, p in full.named_parameters():
+        if key.startswith("beta") or p.grad is None:
+            continue
+        e = nrel(gsum[key].cpu().numpy(), p.grad.cpu().numpy())
+        assert e <= 1e-5, (key, e)
