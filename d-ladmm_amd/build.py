@@ -19,7 +19,9 @@ CSRC = os.path.join(HERE, "csrc")
 UNITS = ("dladmm_capi.hip", "dladmm_fused.hip", "dladmm_fused_savep.hip", "dladmm_fused_x3.hip",
          "dladmm_fused_x3_savep.hip",
          "dladmm_layered.hip", "dladmm_backward.hip", "dladmm_lskm.hip", "dladmm_eval.hip",
-         "dladmm_tile_bf16.hip", "dladmm_reverse.hip", "dladmm_lena.hip",
+         "dladmm_tile_bf16.hip", "dladmm_tile_bf16_pair.hip", "dladmm_tile_bf16_pipe.hip",
+         "dladmm_reverse.hip",
+         "dladmm_lena.hip",
          # reverse-sweep instantiations: one unit per E-step form and shape group (minutes each)
          "dladmm_reverse_vvar.hip", "dladmm_reverse_v1.hip", "dladmm_reverse_lasso.hip",
          "dladmm_reverse_vvar_small.hip", "dladmm_reverse_v1_small.hip",
@@ -35,7 +37,8 @@ FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", f"--offload-arch={AR
 # MFMAs (packed v_pk_* f32 ops issue slower there; MI355X_MICROARCH.md, price of one filler
 # beside MFMAs)
 UNIT_FLAGS = {u: ["-fno-slp-vectorize"] for u in UNITS
-              if u.startswith("dladmm_fused_x3") or u.startswith("dladmm_reverse")}
+              if u.startswith("dladmm_fused_x3") or u.startswith("dladmm_reverse") or
+              u == "dladmm_tile_bf16_pipe.hip"}
 
 
 def deps(path, seen=None):

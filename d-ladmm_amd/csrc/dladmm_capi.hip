@@ -313,6 +313,7 @@ struct Plan {
   int ldl;     // columns per slice
   int nbp;     // bf16 path: 16-column blocks of the packed state
   bool narrow;  // bf16 path: 128-column tiles (two workgroups per CU)
+  bool pipe1;   // bf16 path: G1 on the persistent pipelined kernel (dladmm_tile_bf16_pipe.hip)
   size_t off_ap, off_wp, off_v, off_zb, off_zw, off_ew, off_lw, off_loss, total;
   size_t off_btab;            // path 1, V1: device tables of the per-layer beta pointers
   size_t off_wexp, off_umax;  // path 4
@@ -377,6 +378,49 @@ inline bool shared_weight(const dladmm_fwd_desc* d) {
   for (int k = 1; k < d->layers; ++k)
     if (d->W[k] != d->W[0]) return false;
   return true;
+}
+
+// bf16 tiles: two column halves one phase apart per launch (dladmm_tile_bf16_pair.hip) when
+// the batch has at least two narrow column tiles.  DLADMM_BF16_PAIR=0 runs one phase per launch
+// (A/B measurements; the results are bit-identical)
+inline bool bf16_paired(const Plan& p) {
+  // measured slower than one phase per launch (profiles/r05_pair_ab.json): opt-in only
+  const char* e = getenv("DLADMM_BF16_PAIR");
+  return p.narrow && p.gx >= 2 && e && e[0] == '1';
+}
+
+// bf16 tiles: G1 as the persistent software-pipelined kernel (dladmm_tile_bf16_pipe.hip) when the
+// contraction (m) is 32 k-blocks of 32 (m = 993 .. 1024, config 5's 1024) and its 32-bit buffer
+// offsets hold (the padded rows of Z_{k-1} / Z_k and the packed copy); DLADMM_BF16_PIPE=0 keeps
+// the one-phase kernel (bit-identical outputs)
+inline bool bf16_pipe_g1(const dladmm_fwd_desc* d, const Plan& p) {
+  const char* e = getenv("DLADMM_BF16_PIPE");
+  if (!p.narrow || p.KB1 != 32 || (e && e[0] == '0')) return false;
+  const int64_t lim = (int64_t)1 << 31, rows = (int64_t)16 * p.MBp1;
+  const int64_t B = d->batch;
+  const int64_t ldmax = d->ld_z0 > d->ld_out ? d->ld_z0 : (d->ld_out > B ? d->ld_out : B);
+  return rows * ldmax * 4 < lim && (int64_t)p.KB2 * p.nbp * 1024 < lim;
+}
+
+// compute units of the current device (the persistent kernels' grid), cached per device
+inline int device_cus() {
+  // DLADMM_PIPE_GRID=<g>: at most g persistent workgroups (tests: many tiles per workgroup on a
+  // small problem)
+  if (const char* e = getenv("DLADMM_PIPE_GRID")) {
+    const int g = atoi(e);
+    if (g > 0) return g;
+  }
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        v <= 0)
+      v = 256;
+    cache[dev] = v;
+  }
+  return cache[dev];
 }
 
 inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
@@ -447,8 +491,11 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
   p->gx = ceil_div(d->batch, cols);
   p->ldl = p->gx * cols;
   p->nbp = p->ldl / 16;
-  // loss partial slots per column: one per slice (bf16 tiles: one per slice and wave row)
-  p->nslots = p->ldl * (p->slices1 > p->slices2 ? p->slices1 : p->slices2) * (bf16 ? 2 : 1);
+  p->pipe1 = bf16 && bf16_pipe_g1(d, *p);
+  // loss partial slots per column: one per slice (bf16 tiles: one per slice and wave row; the
+  // pipelined G1 kernel's waves cover 64 rows: 4 per slice)
+  p->nslots = p->ldl * (p->slices1 > p->slices2 ? p->slices1 : p->slices2) *
+              (bf16 ? (p->pipe1 ? 4 : 2) : 1);
   const size_t fb = (size_t)kFrag * sizeof(float);
   p->off_ap = 0;
   p->off_wp = align256(fb * p->KB2 * p->MBp2);
@@ -624,6 +671,44 @@ inline int run_fused_x3(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipSt
   return 0;
 }
 
+// Launch the collected phases ph[0 .. nph) (nph = 2K + 1: prologue, G1(0), G2(0), ...) as 2K + 2
+// launches: launch t runs phase t on column half 0 (tiles [0, gx0)) and phase t - 1 on half 1.
+inline int launch_paired(int variant, const Plan& p, const LayerArgs* ph, int nph, hipStream_t s) {
+  const int gx0 = (p.gx + 1) / 2, gx1 = p.gx - gx0;
+  // DLADMM_BF16_PAIR_F=<permille>: the G2-shaped tiles are spread over the first F of the blocks
+  const char* fe = getenv("DLADMM_BF16_PAIR_F");
+  const int fv = fe ? atoi(fe) : 1000;
+  const int fpm = fv < 1 ? 1 : (fv > 1000 ? 1000 : fv);
+  auto ptype = [](int q) { return q == 0 ? 2 : ((q & 1) ? 0 : 1); };  // 2 prologue, 0 G1, 1 G2
+  auto rows = [&](int q) { return ptype(q) == 0 ? p.slices1 : p.slices2; };
+  for (int t = 0; t <= nph; ++t) {
+    const int q0 = t < nph ? t : -1, q1 = t - 1;
+    TilePairArgs pa{};
+    int t0, t1;
+    if (q0 >= 0) {   // half 0 at phase t [, half 1 at t - 1]
+      pa.a[0] = ph[q0]; pa.gx[0] = gx0; pa.x0[0] = 0; pa.n[0] = gx0 * rows(q0);
+      t0 = ptype(q0);
+      if (q1 >= 0) {
+        pa.a[1] = ph[q1]; pa.gx[1] = gx1; pa.x0[1] = gx0; pa.n[1] = gx1 * rows(q1);
+        t1 = ptype(q1);
+      } else {
+        pa.a[1] = ph[q0]; pa.gx[1] = 1; pa.n[1] = 0;  // (2, 0): prologue alone
+        t1 = 0;
+      }
+    } else {         // the last launch: half 1's G2(K-1) alone, as half 0 of a (1, 0) launch
+      pa.a[0] = ph[q1]; pa.gx[0] = gx1; pa.x0[0] = gx0; pa.n[0] = gx1 * rows(q1);
+      pa.a[1] = ph[q1]; pa.gx[1] = 1; pa.n[1] = 0;
+      t0 = 1; t1 = 0;
+    }
+    const int LH = t0 != 0 ? 0 : 1;
+    const int total = pa.n[0] + pa.n[1];
+    const int F = (int)(((int64_t)total * fpm + 999) / 1000);
+    pa.F = F < pa.n[LH] ? pa.n[LH] : (F < 1 ? 1 : F);
+    if (hipError_t e = launch_tile_bf16_pair(t0, t1, variant, pa, s)) return (int)e;
+  }
+  return 0;
+}
+
 inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStream_t s) {
   const int K = d->layers, m = d->m, n = d->n;
   const int64_t B = d->batch;
@@ -639,7 +724,11 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
   const int sb1 = p.SB1, sb2 = p.SB2;
   char* Vb = ws + p.off_v;   // bf16: packed Var_k (B operand of G1)
   char* Zb = ws + p.off_zb;  // bf16: packed Z_k / Z0 (B operand of G2)
+  const bool pipe1 = bf && p.pipe1;
+  const int cus = pipe1 ? device_cus() : 0;
   auto launch = [&](int phase, const LayerArgs& la, dim3 grid, int sb) -> hipError_t {
+    if (pipe1 && phase == 0)
+      return launch_tile_bf16_pipe_g1(d->variant, la, p.gx, p.slices1, cus, s);
     return bf ? launch_tile_bf16(phase, d->variant, p.narrow, la, grid, s)
               : launch_layer(phase, d->variant, la, grid, sb, s);
   };
@@ -670,6 +759,15 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
   a.lossp = d->loss_kind ? lossp : nullptr;
   const dim3 g1(p.gx, p.slices1), g2(p.gx, p.slices2);
   const bool v1 = d->variant == DLADMM_V1_LENA;
+  // bf16 tiles, two column halves one phase apart per launch (dladmm_tile_bf16_pair.hip):
+  // the phases are collected first (prologue, G1(0), G2(0), ..., G2(K-1)) and launched in pairs
+  const bool paired = bf && bf16_paired(p);
+  std::vector<LayerArgs> ph(paired ? 2 * K + 1 : 0);
+  int nph = 0;
+  auto run = [&](int phase, const LayerArgs& la, dim3 grid, int sb) -> hipError_t {
+    if (paired) { ph[nph++] = la; return hipSuccess; }
+    return launch(phase, la, grid, sb);
+  };
   if (d->ev_kernel_start) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_start, s)) return (int)e;
   }
@@ -688,7 +786,7 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
     b.ldo = ldo;
     b.To = (d->T && !lean) ? d->T : nullptr;
     b.b1n_e = v1 ? d->beta1_elem[0] : nullptr;
-    if (hipError_t e = launch(2, b, g2, sb2)) return (int)e;
+    if (hipError_t e = run(2, b, g2, sb2)) return (int)e;
   }
   for (int k = 0; k < K; ++k) {
     const bool last = k == K - 1;
@@ -710,7 +808,7 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
     b.Zprev = Zp; b.ldzp = ldzp;
     b.Zo = Zo; b.ldo = ldout;
     if (bf) { b.Pb = Zb; b.pb_kb = p.KB2; }
-    if (hipError_t e = launch(0, b, g1, sb1)) return (int)e;
+    if (hipError_t e = run(0, b, g1, sb1)) return (int)e;
     // G2(k): P = A Z_k -> E_k, L_k, T_{k+1}, Var_{k+1}
     LayerArgs c = a;
     c.k = k; c.KB = p.KB2; c.MBp = p.MBp2; c.Krows = n; c.Wp = Ap;
@@ -724,7 +822,10 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
       c.b2e = d->beta2_elem[k];
       c.b1n_e = k + 1 < K ? d->beta1_elem[k + 1] : nullptr;
     }
-    if (hipError_t e = launch(1, c, g2, sb2)) return (int)e;
+    if (hipError_t e = run(1, c, g2, sb2)) return (int)e;
+  }
+  if (paired) {
+    if (const int e = launch_paired(d->variant, p, ph.data(), nph, s)) return e;
   }
   if (d->ev_kernel_stop) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_stop, s)) return (int)e;

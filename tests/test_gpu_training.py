@@ -192,6 +192,9 @@ def test_v1_beta_shard_matches_whole_batch(world, kind, dl):
         tot += float(t)
         for key, p in net.named_parameters():
             gf = dict(full.named_parameters())[key].grad
+            if p.grad is None or gf is None:   # unreached (the last layer's E step under l1l1)
+                assert p.grad is None and gf is None, key
+                continue
             if getattr(p, "_dladmm_rank_local", False):
                 e = nrel(p.grad.cpu().numpy(), gf[:, c0:c1].cpu().numpy())
                 assert e <= 1e-5, (r, key, e)
