@@ -391,11 +391,15 @@ inline bool bf16_paired(const Plan& p) {
 
 // bf16 tiles: G1 as the persistent software-pipelined kernel (dladmm_tile_bf16_pipe.hip) when the
 // contraction (m) is 32 k-blocks of 32 (m = 993 .. 1024, config 5's 1024) and its 32-bit buffer
-// offsets hold (the padded rows of Z_{k-1} / Z_k and the packed copy); DLADMM_BF16_PIPE=0 keeps
-// the one-phase kernel (bit-identical outputs)
+// offsets hold (the padded rows of Z_{k-1} / Z_k and the packed copy).  Measured slower than the
+// one-phase kernel at config 5 (322 vs 260 us per G1: the epilogue's loads and stores contend
+// with the main loop's operand DMA in each CU's vector-memory path; profiles/r05_pipe_ab.json,
+// profiles/r05_cfg5_pmc.json): opt-in only, DLADMM_BF16_PIPE=1 (bit-identical outputs)
 inline bool bf16_pipe_g1(const dladmm_fwd_desc* d, const Plan& p) {
   const char* e = getenv("DLADMM_BF16_PIPE");
-  if (!p.narrow || p.KB1 != 32 || (e && e[0] == '0')) return false;
+  if (!p.narrow || p.KB1 != 32 || !(e && e[0] == '1')) return false;
+  // per-row thresholds (V2 / V3): the one-phase kernel
+  if (d->variant == DLADMM_V2_LTHETA || d->variant == DLADMM_V3_FULL) return false;
   const int64_t lim = (int64_t)1 << 31, rows = (int64_t)16 * p.MBp1;
   const int64_t B = d->batch;
   const int64_t ldmax = d->ld_z0 > d->ld_out ? d->ld_z0 : (d->ld_out > B ? d->ld_out : B);
