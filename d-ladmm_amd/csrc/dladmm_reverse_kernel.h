@@ -44,7 +44,9 @@
                    // rows, 2 no G2' rows, 4 no G1' rows, 8 no Z_k loads, 16 no gU stores, 32 no
                    // G2' operand loads, 64 no Var / adjoint-of-E stores; through a null buffer
                    // view (instructions kept, no memory traffic): 128 the adjoint of E (loads and
-                   // stores), 256 X, 512 P, 1024 E, 2048 L
+                   // stores), 256 X, 512 P, 1024 E, 2048 L; one dwordx4 per G2' block instead of
+                   // a dword per row (fragment order; measured slower, profiles/r05_rev_x4.json):
+                   // 4096 X, 8192 P, 16384 the adjoint of E
 #endif
 
 #ifndef REV_LOAD_AUX
@@ -479,12 +481,22 @@ __global__ __launch_bounds__(256, 1) void reverse_kernel(const RevArgs a) {
       return;
     }
     const uint32_t so = wPT.at(rr);
-    pw[rr][S_P] = ld((REV_ABL & 512) ? none : o.P, vo, so);
+    // REV_ABL 4096 / 8192 / 16384 (timing only): X / P / the adjoint of E as ONE dwordx4 per
+    // block (row 0's slot, fragment order) instead of a dword per row
+    auto ld4 = [&](rsrc_t r, uint32_t soff, int S) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(lane * 16), (int)soff, REV_LOAD_AUX);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pw[q][S] = __builtin_bit_cast(float, v[q]);
+    };
+    if constexpr (REV_ABL & 8192) { if (rr == 0) ld4(o.P, so, S_P); }
+    else pw[rr][S_P] = ld((REV_ABL & 512) ? none : o.P, vo, so);
     pw[rr][S_L] = ld((REV_ABL & 2048) ? none : o.L, vo, so);
-    pw[rr][S_X] = ld((REV_ABL & 256) ? none : rx, vx, wX.at(rr));
+    if constexpr (REV_ABL & 4096) { if (rr == 0) ld4(rx, wX.at(0), S_X); }
+    else pw[rr][S_X] = ld((REV_ABL & 256) ? none : rx, vx, wX.at(rr));
     if constexpr (kAE) {
       pw[rr][S_E] = ld((REV_ABL & 1024) ? none : o.E, vo, so);
-      pw[rr][S_AE] = ld((REV_ABL & 128) ? none : rv, vw, wA.at(rr));
+      if constexpr (REV_ABL & 16384) { if (rr == 0) ld4(rv, wA.at(0), S_AE); }
+      else pw[rr][S_AE] = ld((REV_ABL & 128) ? none : rv, vw, wA.at(rr));
     }
     if constexpr (kV1) {
       pw[rr][S_B1K] = ld(o.B1K, vo, so);
