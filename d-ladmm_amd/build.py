@@ -20,6 +20,7 @@ UNITS = ("dladmm_capi.hip", "dladmm_fused.hip", "dladmm_fused_savep.hip", "dladm
          "dladmm_fused_x3_savep.hip",
          "dladmm_layered.hip", "dladmm_backward.hip", "dladmm_lskm.hip", "dladmm_eval.hip",
          "dladmm_tile_bf16.hip", "dladmm_tile_bf16_pair.hip", "dladmm_tile_bf16_pipe.hip",
+         "dladmm_tile_bf16_queue.hip",
          "dladmm_reverse.hip",
          "dladmm_lena.hip",
          # reverse-sweep instantiations: one unit per E-step form and shape group (minutes each)

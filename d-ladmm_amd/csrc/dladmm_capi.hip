@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "dladmm_common.h"
+#include "dladmm_queue.h"
 #include "dladmm_internal.h"
 
 namespace dladmm {
@@ -314,6 +315,9 @@ struct Plan {
   int nbp;     // bf16 path: 16-column blocks of the packed state
   bool narrow;  // bf16 path: 128-column tiles (two workgroups per CU)
   bool pipe1;   // bf16 path: G1 on the persistent pipelined kernel (dladmm_tile_bf16_pipe.hip)
+  bool queue;   // bf16 path: the whole forward as one persistent queue launch (wide tiles)
+  int lags;     // queue: diagonal lag classes
+  size_t off_qtab, off_qcnt;  // queue: phase-argument table, ticket / completion counters
   size_t off_ap, off_wp, off_v, off_zb, off_zw, off_ew, off_lw, off_loss, total;
   size_t off_btab;            // path 1, V1: device tables of the per-layer beta pointers
   size_t off_wexp, off_umax;  // path 4
@@ -406,6 +410,13 @@ inline bool bf16_pipe_g1(const dladmm_fwd_desc* d, const Plan& p) {
   return rows * ldmax * 4 < lim && (int64_t)p.KB2 * p.nbp * 1024 < lim;
 }
 
+// bf16 tiles: the whole forward as one persistent launch pulling tile units from work queues in
+// dependency order (dladmm_tile_bf16_queue.hip, bit-identical outputs): DLADMM_BF16_QUEUE=1
+inline bool bf16_queue() {
+  const char* e = getenv("DLADMM_BF16_QUEUE");
+  return e && e[0] == '1';
+}
+
 // compute units of the current device (the persistent kernels' grid), cached per device
 inline int device_cus() {
   // DLADMM_PIPE_GRID=<g>: at most g persistent workgroups (tests: many tiles per workgroup on a
@@ -491,11 +502,18 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
   // bf16 tile width: DLADMM_BF16_TILE=wide|narrow (A/B measurements), default below
   const char* tw = getenv("DLADMM_BF16_TILE");
   p->narrow = bf16 && (tw ? tw[0] == 'n' : kBf16NarrowDefault);
+  p->queue = bf16 && bf16_queue();
+  if (p->queue) {
+    p->narrow = false;  // the queue runs the wide tile body, one workgroup per CU
+    const char* le = getenv("DLADMM_BF16_QUEUE_LAGS");
+    const int lv = le ? atoi(le) : 2;
+    p->lags = lv < 1 ? 1 : (lv > 8 ? 8 : lv);
+  }
   const int cols = bf16 ? bf16_tile_cols(p->narrow) : kLayerCols;
   p->gx = ceil_div(d->batch, cols);
   p->ldl = p->gx * cols;
   p->nbp = p->ldl / 16;
-  p->pipe1 = bf16 && bf16_pipe_g1(d, *p);
+  p->pipe1 = bf16 && !p->queue && bf16_pipe_g1(d, *p);
   // loss partial slots per column: one per slice (bf16 tiles: one per slice and wave row; the
   // pipelined G1 kernel's waves cover 64 rows: 4 per slice)
   p->nslots = p->ldl * (p->slices1 > p->slices2 ? p->slices1 : p->slices2) *
@@ -511,7 +529,11 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
   p->off_ew = p->off_zw + (lean ? align256((size_t)d->n * B * sizeof(float)) : 0);
   p->off_lw = p->off_ew + (lean ? align256((size_t)d->m * B * sizeof(float)) : 0);
   p->off_loss = p->off_lw + (lean ? align256((size_t)d->m * B * sizeof(float)) : 0);
-  p->total = p->off_loss + align256((size_t)2 * K * p->nslots * sizeof(float));
+  p->off_qtab = p->off_loss + align256((size_t)2 * K * p->nslots * sizeof(float));
+  const int nph = 2 * K + 1;
+  p->off_qcnt = p->off_qtab + (p->queue ? align256((size_t)nph * sizeof(LayerArgs)) : 0);
+  p->total = p->off_qcnt +
+             (p->queue ? align256((size_t)queue_counter_words(nph, p->gx) * sizeof(int)) : 0);
   return 0;
 }
 
@@ -766,10 +788,11 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
   // bf16 tiles, two column halves one phase apart per launch (dladmm_tile_bf16_pair.hip):
   // the phases are collected first (prologue, G1(0), G2(0), ..., G2(K-1)) and launched in pairs
   const bool paired = bf && bf16_paired(p);
-  std::vector<LayerArgs> ph(paired ? 2 * K + 1 : 0);
+  const bool queue = bf && p.queue;
+  std::vector<LayerArgs> ph(paired || queue ? 2 * K + 1 : 0);
   int nph = 0;
   auto run = [&](int phase, const LayerArgs& la, dim3 grid, int sb) -> hipError_t {
-    if (paired) { ph[nph++] = la; return hipSuccess; }
+    if (paired || queue) { ph[nph++] = la; return hipSuccess; }
     return launch(phase, la, grid, sb);
   };
   if (d->ev_kernel_start) {
@@ -830,6 +853,19 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
   }
   if (paired) {
     if (const int e = launch_paired(d->variant, p, ph.data(), nph, s)) return e;
+  }
+  if (queue) {
+    LayerArgs* tab = (LayerArgs*)(ws + p.off_qtab);
+    int* cnt = (int*)(ws + p.off_qcnt);
+    if (hipError_t e = write_layer_table(ph.data(), nph, tab, s)) return (int)e;
+    if (hipError_t e = zero_async(cnt, (size_t)queue_counter_words(nph, p.gx) * sizeof(int), s))
+      return (int)e;
+    QueueArgs qa{};
+    qa.ph = tab; qa.nph = nph; qa.gx = p.gx;
+    qa.rows1 = p.slices1; qa.rows2 = p.slices2; qa.lags = p.lags;
+    qa.tickets = cnt; qa.done = cnt + 8 * 32;
+    qa.err = cnt + queue_counter_words(nph, p.gx) - 1;
+    if (hipError_t e = launch_tile_bf16_queue(d->variant, qa, device_cus(), s)) return (int)e;
   }
   if (d->ev_kernel_stop) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_stop, s)) return (int)e;

@@ -254,6 +254,46 @@ def test_bf16_pipelined_g1_bit_identical(variant, grid, dl, monkeypatch):
                                    rtol=1e-6)
 
 
+@pytest.mark.parametrize("variant,grid,lags", [("v4", "0", "2"), ("v4", "3", "1"), ("v4", "5", "3"),
+                                               ("v1", "7", "2"), ("v2", "4", "2"), ("v3", "0", "2"),
+                                               ("v5", "9", "2"), ("v6", "2", "2")])
+def test_bf16_queue_bit_identical(variant, grid, lags, dl, monkeypatch):
+    """The whole bf16 forward as one persistent launch pulling tile units from per-XCD queues
+    in dependency order (dladmm_tile_bf16_queue.hip, DLADMM_BF16_QUEUE=1): every unit is the
+    wide one-phase tile body, so Z/E/L/T (full and lean) and the fused sums are bitwise those of
+    one launch per product.  DLADMM_PIPE_GRID caps the persistent grid (workgroups serve other
+    XCDs' queues and run many units each); lags 1..3 order the tickets along different diagonals;
+    ragged batches of 4 and 11 column tiles."""
+    if grid != "0":
+        monkeypatch.setenv("DLADMM_PIPE_GRID", grid)
+    monkeypatch.setenv("DLADMM_BF16_QUEUE_LAGS", lags)
+    m, n, K = 300, 530, 3
+    for B in (850, 2600):
+        inp = P.make_inputs(m, n, B, 9331)
+        sd = P.make_state_dict(variant, m, n, B, K, inp["A"], 9331, perturb=0.1,
+                               wscale=P.VARIANT_SPECS[variant]["wscale"])
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+        net = dl.VARIANTS[variant](m=m, n=0, d=n, batch_size=B, A=t(inp["A"]), Z0=t(inp["Z0"]),
+                                   E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K)
+        net.load_state_dict({k: t(v) for k, v in sd.items()})
+        net.requires_grad_(False)
+        net.cuda()
+        net.precision = "bf16"
+        X = t(inp["X"]).cuda()
+        res = {}
+        for mode in ("0", "1"):
+            monkeypatch.setenv("DLADMM_BF16_QUEUE", mode)
+            with torch.no_grad():
+                res[mode] = (net.run(X, keep_all=True, loss_kind=1),
+                             net.run(X, keep_all=False, loss_kind=1))
+            torch.cuda.synchronize()
+        for r0, r1 in zip(res["0"], res["1"]):
+            for x, y in ((r0.Z, r1.Z), (r0.E, r1.E), (r0.L, r1.L), (r0.T, r1.T)):
+                if x is not None:
+                    assert torch.equal(x, y), (variant, B)
+            assert torch.equal(r0.loss_sums, r1.loss_sums), (variant, B)
+
+
 @pytest.mark.parametrize("name", sorted(P.BF16_FIXTURES))
 def test_bf16_matches_reference_bf16_gemms(name, dl):
     """Against the reference classes themselves run with bf16-operand GEMMs (exact accumulation,
