@@ -67,6 +67,9 @@ def parse():
                          "products, fp32 accumulation); bf16 = BASELINE config 5 mode (bf16 MFMA "
                          "operands, fp32 state): --precision bf16 --m 1024 --n 4096 --batch 16384")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-train", action="store_true",
+                    help="skip the training-step line (SURVEY row f1: V4 forward + fused L1L1 "
+                         "objective + reverse-sweep backward + Adam at the headline shape)")
     ap.add_argument("--no-split", action="store_true",
                     help="skip the secondary f32_split measurement of the f32 headline run")
     ap.add_argument("--cpu-batch", type=str, default="10000,65536",
@@ -377,6 +380,17 @@ def main():
             del w_
             torch.cuda.empty_cache()
     torch.cuda.synchronize()
+    # SURVEY row f1 at N = 1: the headline shape's training step (tools/bench_train.py: forward +
+    # fused per-layer L1L1 objective + reverse-sweep backward + Adam), timed after everything above
+    train = None
+    if world == 1 and not strong and not a.no_train and a.variant == "v4" and \
+            a.precision == "f32" and (m, n, K) == (256, 512, 15):
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import bench_train
+        ta = bench_train.parser().parse_args(["--variant", "v4", "--fused-loss", "--batch", str(B),
+                                              "--steps", "10", "--warmup", "3"])
+        train = bench_train.run(ta)
+        torch.cuda.empty_cache()
 
     if rank == 0:
         path = {1: "fused", 2: "per-layer", 3: "bf16-tiles", 4: "fused-split-f16"}.get(
@@ -538,6 +552,14 @@ def main():
                 "roofline_frac": f3 / cfg3["kern"] / PEAK_F32_MFMA,
                 "objective_last_layer": cfg3["obj"],
             }
+        if train is not None:
+            res["train"] = {k: train[k] for k in (
+                "metric", "batch", "step_ms", "samples_per_s", "forward_ms", "backward_ms",
+                "backward_tflops", "backward_frac_fp32_mfma", "loss_path")}
+            res["train"]["note"] = ("V4 m=256 n=512 K=15 training step (zero_grad, forward with "
+                                    "saved A Z_k, fused L1L1 objective with decay, reverse-sweep "
+                                    "backward + split-K weight gradients, torch Adam); backward "
+                                    "FLOP = 6 m n K B performed (tools/bench_train.py)")
         if world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(
                 m, n, K, [int(x) for x in a.cpu_batch.split(",") if x], a.cpu_runs, a.variant)

@@ -31,7 +31,7 @@ import bench  # noqa: E402  (synthetic inputs)
 PEAK = 157.3e12
 
 
-def main():
+def parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=10)
@@ -56,7 +56,11 @@ def main():
     ap.add_argument("--fused-loss", action="store_true",
                     help="net.training_loss (objective fused into the kernels) instead of the "
                          "reference's torch-op loss over the returned Z_k")
-    a = ap.parse_args()
+    return ap
+
+
+def run(a) -> dict:
+    """One training-step measurement (the parsed options of parser()); returns the JSON dict."""
     dl = importlib.import_module("d-ladmm_amd")
     dev = torch.device("cuda", 0)
     m, n, K, B = a.m, a.n, a.layers, a.batch
@@ -158,7 +162,12 @@ def main():
         "backward_frac_fp32_mfma_reference_equiv": flop_r / (med(bw) * 1e-3) / PEAK,
         "loss": float(loss.detach()),
     }
-    print(json.dumps(res), flush=True)
+    del opt, net
+    return res
+
+
+def main():
+    print(json.dumps(run(parser().parse_args())), flush=True)
 
 
 if __name__ == "__main__":
