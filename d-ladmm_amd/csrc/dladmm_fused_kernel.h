@@ -53,6 +53,9 @@
 #ifndef DLADMM_CHUNK
 #define DLADMM_CHUNK 16
 #endif
+#ifndef DLADMM_VR_AGPR
+#define DLADMM_VR_AGPR 1  // Var pinned to AGPRs (0: the compiler places it; A/B experiment)
+#endif
 
 #ifndef DLADMM_G2_CHAINS
 // accumulation chains per output of A Z_k: the k sub-steps x, z of every 16-k block run on one
@@ -308,7 +311,7 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
         if constexpr (kEState) Er[b][r] = bload(re, oe + (uint32_t)((16 * b + r) * a.lde0 * 4));
         Lr[b][r] = bload(rl, ol + (uint32_t)((16 * b + r) * a.ldl0 * 4));
         Vr[b][r] = 0.0f;
-        pin_agpr(Vr[b][r]);
+        if constexpr (DLADMM_VR_AGPR) pin_agpr(Vr[b][r]);
       }
       xs[(w * MB + b) * 64 + lane] = xv;  // read back only by this wave (no barrier needed)
     }
@@ -431,7 +434,7 @@ __global__ __launch_bounds__(256, 1) void fused_kernel(const FusedArgs a) {
     fit2 = __builtin_fmaf(res, res, fit2);                   // (X - A Z)^2
     // Var of the next layer: L + b1*T  (main_lena.py:85); unused after the last layer
     Vr[b][r] = l + b1n * t;
-    pin_agpr(Vr[b][r]);
+    if constexpr (DLADMM_VR_AGPR) pin_agpr(Vr[b][r]);
     if (r == 3) mw.next();
   };
   // per-column objective of layer k (k < 0: just reset the prologue's sums): the column's
