@@ -866,6 +866,10 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
     qa.tickets = cnt; qa.done = cnt + 8 * 32;
     qa.err = cnt + queue_counter_words(nph, p.gx) - 1;
     if (hipError_t e = launch_tile_bf16_queue(d->variant, qa, device_cus(), s)) return (int)e;
+    float* z_last = lean ? d->Z : d->Z + (int64_t)(K - 1) * zl;
+    if (hipError_t e = launch_queue_check(qa, z_last, d->loss_kind ? lossp : nullptr, 2 * K,
+                                          p.nslots, s))
+      return (int)e;
   }
   if (d->ev_kernel_stop) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_stop, s)) return (int)e;

@@ -28,4 +28,9 @@ hipError_t write_layer_table(const LayerArgs* host, int n, LayerArgs* dst, hipSt
 // grid = persistent workgroups (one per CU: 8 waves, 128 KiB of LDS ring)
 hipError_t launch_tile_bf16_queue(int variant, const QueueArgs& q, int grid, hipStream_t s);
 
+// after the queue launch: if a dependency wait timed out, poison z_last[0] and lossp[i * stride]
+// for i < rows (NaN), so a failed schedule never returns plausible numbers
+hipError_t launch_queue_check(const QueueArgs& q, float* z_last, float* lossp, int rows,
+                              int64_t stride, hipStream_t s);
+
 }  // namespace dladmm

@@ -159,6 +159,17 @@ __global__ __launch_bounds__(512, 1) void tile_bf16_queue_kernel(const QueueArgs
   }
 }
 
+// a timed-out dependency wait (err set) poisons the results instead of passing silently: the
+// first element of the last layer's Z and every (layer, term) row of the loss partials
+__global__ __launch_bounds__(64) void queue_err_kernel(const int* err, float* z, float* lossp,
+                                                       int rows, int64_t stride) {
+  if (*err == 0) return;
+  const float nan = __builtin_nanf("");
+  if (threadIdx.x == 0 && z) z[0] = nan;
+  if (lossp)
+    for (int i = threadIdx.x; i < rows; i += 64) lossp[(int64_t)i * stride] = nan;
+}
+
 template <int EMODE, int PKIND>
 hipError_t launch_q(const QueueArgs& q, int grid, hipStream_t s) {
   hipLaunchKernelGGL((tile_bf16_queue_kernel<EMODE, PKIND>), dim3(grid), dim3(512), 0, s, q);
@@ -177,6 +188,13 @@ hipError_t write_layer_table(const LayerArgs* host, int n, LayerArgs* dst, hipSt
     if (hipError_t e = hipGetLastError()) return e;
   }
   return hipSuccess;
+}
+
+hipError_t launch_queue_check(const QueueArgs& q, float* z_last, float* lossp, int rows,
+                              int64_t stride, hipStream_t s) {
+  hipLaunchKernelGGL(queue_err_kernel, dim3(1), dim3(64), 0, s, (const int*)q.err, z_last, lossp,
+                     rows, stride);
+  return hipGetLastError();
 }
 
 hipError_t launch_tile_bf16_queue(int variant, const QueueArgs& q, int grid, hipStream_t s) {
