@@ -28,6 +28,8 @@ struct PackArgs {
   int trans;           // 1: pack the transpose (element (row, c) = src[c][row])
   int t0;              // scal row of source t is t0 + t
   int bf16;            // 1: v_mfma_f32_16x16x32_bf16 A fragments (16 x 32, 8 bf16 per lane)
+  int vec;             // 1: every source 16-B aligned and ld % 4 == 0: a lane's in-range
+                       // piece is read with 16-B loads (the same values, fewer instructions)
 };
 static_assert(sizeof(PackArgs) <= 2048, "kernel argument size");
 
@@ -49,6 +51,17 @@ __global__ __launch_bounds__(256) void pack_frags_kernel(const PackArgs p) {
     const int c8 = 32 * jb + 8 * (lane >> 4);
     const float* s8 = p.src[t];
     bf16x8 v;
+    if (p.vec && !p.trans && row < p.R && c8 + 8 <= p.C) {
+      const f32x4* q4 = reinterpret_cast<const f32x4*>(s8 + (int64_t)row * p.ld + c8);
+      const f32x4 lo = q4[0], hi = q4[1];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[q] = (__bf16)(f * lo[q]);
+        v[4 + q] = (__bf16)(f * hi[q]);
+      }
+      reinterpret_cast<bf16x8*>(p.dst)[((int64_t)t * p.RB * p.CB + fr) * 64 + lane] = v;
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const float x = (row < p.R && c8 + q < p.C)
@@ -63,6 +76,13 @@ __global__ __launch_bounds__(256) void pack_frags_kernel(const PackArgs p) {
   const int c0 = 16 * jb + 4 * (lane >> 4);
   const float* s = p.src[t];
   f32x4 v;
+  if (p.vec && !p.trans && row < p.R && c0 + 4 <= p.C) {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(s + (int64_t)row * p.ld + c0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = f * x[q];
+    reinterpret_cast<f32x4*>(p.dst)[((int64_t)t * p.RB * p.CB + fr) * 64 + lane] = v;
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < 4; ++q)
     v[q] = (row < p.R && c0 + q < p.C)
@@ -551,6 +571,9 @@ inline hipError_t pack(const float* const* srcs, int T, int R, int C, int64_t ld
     pa.R = R; pa.C = C; pa.RB = RB; pa.CB = CB; pa.order = order; pa.ld = ld;
     pa.dst = dst + (size_t)b * RB * CB * kFrag;
     pa.sign = sign; pa.scal = scal; pa.bf16 = bf16;
+    pa.vec = ld % 4 == 0 ? 1 : 0;
+    for (int t = 0; t < nb; ++t)
+      if ((uintptr_t)pa.src[t] & 15) pa.vec = 0;
     hipLaunchKernelGGL(pack_frags_kernel, dim3((RB * CB + 3) / 4, nb), dim3(256), 0, s, pa);
     if (hipError_t e = hipGetLastError()) return e;
   }
