@@ -57,7 +57,9 @@ struct PipeSched {
   }
   // stores of block c: its packed copy; odd c also the Z_k rows of c - 1 and c (a 128-B line is
   // the row segments of two column blocks: both halves leave together); the last its loss partials
-  static constexpr int st_blk(int c) { return (c % 2 ? 9 : 1) + (c == NB - 1 ? 4 : 0); }
+  static constexpr int st_blk(int c) {
+    return (c % 2 ? ((DLADMM_PIPE_EXP & 32) ? 3 : 9) : 1) + (c == NB - 1 ? 4 : 0);
+  }
   static constexpr int stores_at(int t) { return (t >= 0 && t % 2) ? st_blk(t / 2) : 0; }
   static constexpr int E(int t, bool epi) { return epi ? loads_at(t) + stores_at(t) : 0; }
   // top of position t: this wave's pieces of stage t + 1 went out at the top of t - (NST - 2)
@@ -254,10 +256,29 @@ __global__ __launch_bounds__(512, 1) void tile_pipe_g1_kernel(const LayerArgs a,
     float u = av[r];
     if constexpr (PKIND == PK_SCALAR) u = s1 * u;
     const float z = shrink(ez[r] - u, thz_s);                       // main_lena.py:79-80
-    // Z_k rows leave in pairs of column blocks (j even held until j + 1): the two 64-B halves of
-    // each 128-B line reach the L2 back to back (one at a time, two positions apart, the L2
-    // wrote many lines back half-filled: 1.4x the write requests, profiles/r05_cfg5_pmc.json)
-    if constexpr (j % 2 == 0) {
+    // Z_k rows leave in pairs of column blocks (j even held until j + 1), so the two 64-B halves
+    // of each 128-B line reach the L2 back to back (measured: no change against one block at a
+    // time, profiles/r05_pipe_ab.json)
+    if constexpr (DLADMM_PIPE_EXP & 32) {
+      // timing probe (WRONG values): the pair's 2 KiB as two 16-B-per-lane stores of whole
+      // 128-B row segments, 8 rows each
+      if constexpr (j % 2 == 1) {
+        if (r == 3) {
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int row = 8 * q + (lane >> 3);
+            const uint32_t so = (uint32_t)((int64_t)(16 * ib + row) * a.ldo * 4);
+            const int64_t col = (int64_t)(bx * G::CBT + WCB * wc + j - 1) * 16 + 4 * (lane & 7);
+            const uint32_t vo = col < a.B ? (uint32_t)(col * 4) : kOOB;
+            const u32x4_t d4 = {__builtin_bit_cast(uint32_t, z), __builtin_bit_cast(uint32_t, zh[0]),
+                                __builtin_bit_cast(uint32_t, zh[1]), __builtin_bit_cast(uint32_t, zh[2])};
+            __builtin_amdgcn_raw_buffer_store_b128(d4, rzo, (int)vo, (int)so, DLADMM_PIPE_ZPOL);
+          }
+        }
+      } else {
+        zh[r] = z;
+      }
+    } else if constexpr (j % 2 == 0) {
       zh[r] = z;
     } else {
       const uint32_t so = (uint32_t)((int64_t)(16 * ib + r) * a.ldo * 4);

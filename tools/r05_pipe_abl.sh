@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 B="--precision bf16 --m 1024 --n 4096 --batch 16384 --no-cpu-baseline --steps 3 --warmup 1"
 for v in ${VARIANTS:-full pnoepi pnomfma pskel}; do
   if [ $v = full ]; then L=""; else L=$R/d-ladmm_amd/lib/abl/$v/libdladmm_hip.so; fi
-  DLADMM_LIB=$L timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/$v -o run -- python3 $R/bench.py $B > $O/$v.log 2>&1 || exit 1
+  DLADMM_BF16_PIPE=1 DLADMM_LIB=$L timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/$v -o run -- python3 $R/bench.py $B > $O/$v.log 2>&1 || exit 1
   python3 - $O/$v $v <<'PY'
 import csv, glob, sys, collections
 d = collections.defaultdict(list)
