@@ -20,7 +20,7 @@ UNITS = ("dladmm_capi.hip", "dladmm_fused.hip", "dladmm_fused_savep.hip", "dladm
          "dladmm_fused_x3_savep.hip",
          "dladmm_layered.hip", "dladmm_backward.hip", "dladmm_lskm.hip", "dladmm_eval.hip",
          "dladmm_tile_bf16.hip", "dladmm_tile_bf16_pair.hip", "dladmm_tile_bf16_pipe.hip",
-         "dladmm_tile_bf16_queue.hip",
+         "dladmm_tile_bf16_queue.hip", "dladmm_wgrad_x3.hip",
          "dladmm_reverse.hip",
          "dladmm_lena.hip",
          # reverse-sweep instantiations: one unit per E-step form and shape group (minutes each)
@@ -40,6 +40,9 @@ FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", f"--offload-arch={AR
 UNIT_FLAGS = {u: ["-fno-slp-vectorize"] for u in UNITS
               if u.startswith("dladmm_fused_x3") or u.startswith("dladmm_reverse") or
               u == "dladmm_tile_bf16_pipe.hip"}
+# the split-f16 weight gradient unscales every MFMA result with VALU: MFMA results in VGPRs
+# (no v_accvgpr_read per element)
+UNIT_FLAGS["dladmm_wgrad_x3.hip"] = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
 
 
 def deps(path, seen=None):

@@ -8,6 +8,7 @@
 
 #include "dladmm_common.h"
 #include "dladmm_queue.h"
+#include "dladmm_wgrad_x3.h"
 #include "dladmm_internal.h"
 
 namespace dladmm {
@@ -435,6 +436,13 @@ inline bool bf16_pipe_g1(const dladmm_fwd_desc* d, const Plan& p) {
 inline bool bf16_queue() {
   const char* e = getenv("DLADMM_BF16_QUEUE");
   return e && e[0] == '1';
+}
+
+// the split-f16 weight-gradient kernel: precision "f32_split", whole 64-column sub-chunks,
+// unless DLADMM_WGRAD_X3=0
+inline bool use_wgrad_x3(bool x3w, const WgradArgs& wa) {
+  const char* e = getenv("DLADMM_WGRAD_X3");
+  return x3w && wgrad_x3_fits(wa) && !(e && e[0] == '0');
 }
 
 // compute units of the current device (the persistent kernels' grid), cached per device
@@ -909,6 +917,7 @@ struct BwdPlan {
   int wtiles, nchunks; int64_t chunk;
   int wgl;  // reverse path: layers per batched weight-gradient launch
   bool saved_p;                   // BK1 reads the forward's A Z_k (fwd_desc.P)
+  bool x3w;                       // weight gradient on the f16 cores (precision "f32_split")
   size_t off_a1, off_at, off_m, off_mt, off_az, off_ae, off_al, off_at_, off_gp, off_var,
       off_part, off_part2, off_wpart, off_s1dot, total;
   // reverse-sweep kernel (dladmm_reverse.hip): packed A^T and M_k^T, gU_k / Var_k of every
@@ -938,7 +947,9 @@ inline int validate_bwd(const dladmm_bwd_desc* d) {
   if (int e = validate(&d->fwd)) return e;
   const dladmm_fwd_desc& f = d->fwd;
   if (!f.keep_all || !f.T) return DLADMM_E_UNSUPPORTED;
-  if (f.precision != DLADMM_PREC_F32) return DLADMM_E_UNSUPPORTED;  // backward is fp32
+  // backward kernels are fp32; F32_SPLIT moves only the weight-gradient GEMM (make_bwd_plan)
+  if (f.precision != DLADMM_PREC_F32 && f.precision != DLADMM_PREC_F32_SPLIT)
+    return DLADMM_E_UNSUPPORTED;
   // the backward epilogues address every per-layer matrix with 32-bit buffer offsets
   if (!fits_32bit(&f)) return DLADMM_E_UNSUPPORTED;
   {
@@ -984,7 +995,13 @@ inline size_t rev_ws_cap() {
 inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   *p = BwdPlan{};
   const dladmm_fwd_desc& f = d->fwd;
-  if (int e = make_plan(&f, &p->fwd)) return e;
+  // the backward's kernels are planned on the fp32 forward's geometry whatever GEMM form produced
+  // the saved state; fwd_desc.precision "f32_split" (a split-f16 training forward) also moves
+  // the weight-gradient GEMM to the f16 matrix cores (x3w)
+  dladmm_fwd_desc f32 = f;
+  f32.precision = DLADMM_PREC_F32;
+  if (int e = make_plan(&f32, &p->fwd)) return e;
+  p->x3w = f.precision == DLADMM_PREC_F32_SPLIT;
   // the forward stored A Z_k only on the fused paths, fp32 and split-f16 (fwd_desc.P)
   p->saved_p = f.P != nullptr && f.keep_all && (p->fwd.path == 1 || p->fwd.path == 4);
   const int m = f.m, n = f.n;
@@ -1192,7 +1209,10 @@ inline int run_reverse(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hip
     wa.NBp16 = (int)(p.Rn2 / 16); wa.MBp16 = (int)(p.Rm2 / 16);
     wa.Bpad = p.Bpad; wa.chunk = p.chunk; wa.nchunks = p.nchunks; wa.part = wpart;
     wa.gls = gus; wa.vls = vas; wa.pls = (int64_t)p.nchunks * n * m;
-    if (hipError_t e = launch_wgrad(wa, p.wtiles, s, nl)) return (int)e;
+    // precision "f32_split": the weight-gradient GEMM on the f16 matrix cores with exactly split
+    // operands too (dladmm_wgrad_x3.hip; DLADMM_WGRAD_X3=0 keeps the fp32-MFMA kernel)
+    if (hipError_t e = (use_wgrad_x3(p.x3w, wa) ? launch_wgrad_x3 : launch_wgrad)(wa, p.wtiles, s, nl))
+      return (int)e;
     WredArgs ra{};
     ra.part = wpart; ra.pls = wa.pls; ra.nchunks = p.nchunks; ra.nm = (int64_t)n * m;
     ra.scal = f.scalar_params; ra.klo = klo; ra.nl = nl; ra.tied = tied ? 1 : 0;

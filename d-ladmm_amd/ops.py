@@ -249,6 +249,9 @@ def dladmm_backward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[
     d = _lib.BwdDesc()
     keep = _fill_fwd_desc(d.fwd, variant, X, A, W, Z0, E0, L0, scalar_params, row_params,
                           beta1_elem, beta2_elem, True, 0, saved)
+    # a split-f16 training forward (path 4) also runs the weight-gradient GEMM on the f16
+    # matrix cores (csrc/dladmm_wgrad_x3.hip); every other backward kernel is the fp32 one
+    d.fwd.precision = _PRECISIONS["f32_split"] if saved.path == 4 else _PRECISIONS["f32"]
     counts = {"gZ": (K, n), "gE": (K, m), "gL": (K, m), "gT": (K + 1, m)}
     for nm, seq in (("gZ", gZ), ("gE", gE), ("gL", gL), ("gT", gT)):
         if seq is None or all(g is None for g in seq):

@@ -243,3 +243,42 @@ def test_split_training_saves_product_and_matches_fp32(variant, dl):
                               gZ=[torch.ones_like(r.Z[k]) for k in range(K)],
                               tied=net._shared_weight(), **net._tables(net.A.device))
     assert res.path == 1
+
+
+@pytest.mark.parametrize("variant", ["v4", "v5", "v6"])
+def test_split_weight_gradient_on_f16_cores(variant, dl, monkeypatch):
+    """Under precision "f32_split" the backward's weight-gradient GEMM (gU_k Var_k^T over the
+    batch) also runs on the f16 matrix cores with exactly split operands
+    (csrc/dladmm_wgrad_x3.hip): its gradients equal the fp32-MFMA kernel's (DLADMM_WGRAD_X3=0)
+    within fp32 GEMM accuracy, every other gradient is unchanged bitwise, and it is
+    deterministic.  B = 4,096: whole 32-column sub-chunks of the split-K chunks."""
+    from test_gpu_backward import make_train_net
+    m, n, B, K = 256, 512, 4096, 3
+    inp = P.make_inputs(m, n, B, 7713)
+    sd = P.make_state_dict(variant, m, n, B, K, inp["A"], 7713, perturb=0.1)
+    X = torch.from_numpy(inp["X"]).cuda()
+    kind = "lasso" if variant == "v6" else "l1l1"
+    coeffs = [0.6] * (K - 1) + [1.0]
+    grads = {}
+    for mode in ("0", "1", "1b"):
+        monkeypatch.setenv("DLADMM_WGRAD_X3", mode[0])
+        net = make_train_net(dl, variant, inp, sd, K)
+        net.precision = "f32_split"
+        tot, _ = net.training_loss(X, 1e-3, coeffs, kind)
+        tot.backward()
+        torch.cuda.synchronize()
+        grads[mode] = {k: p.grad.detach().clone() for k, p in net.named_parameters()
+                       if p.grad is not None}
+    assert grads["0"].keys() == grads["1"].keys()
+    # the weights' gradients and V5's ss1 (its gradient is <W, gU Var^T> of the same sums)
+    wkeys = [k for k in grads["0"] if k.startswith(("fc", "ss1"))]
+    assert wkeys
+    # the split-f16 GEMM ran: a different rounding sequence of the same sums
+    assert any(not torch.equal(grads["1"][k], grads["0"][k]) for k in wkeys)
+    for k in grads["0"]:
+        assert torch.equal(grads["1"][k], grads["1b"][k]), k  # deterministic
+        a, b = grads["1"][k].double(), grads["0"][k].double()
+        if k in wkeys:
+            assert float((a - b).norm() / b.norm()) <= 1e-5, k
+        else:
+            assert torch.equal(grads["1"][k], grads["0"][k]), k
