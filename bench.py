@@ -391,6 +391,14 @@ def main():
                                               "--steps", "10", "--warmup", "3"])
         train = bench_train.run(ta)
         torch.cuda.empty_cache()
+        if not a.no_split:  # the same step on the split-f16 kernels (forward + weight gradient)
+            ts = bench_train.parser().parse_args(["--variant", "v4", "--fused-loss", "--batch",
+                                                  str(B), "--steps", "10", "--warmup", "3",
+                                                  "--precision", "f32_split"])
+            train["split_f16"] = {k: v for k, v in bench_train.run(ts).items()
+                                  if k in ("step_ms", "samples_per_s", "forward_ms",
+                                           "backward_ms")}
+            torch.cuda.empty_cache()
 
     if rank == 0:
         path = {1: "fused", 2: "per-layer", 3: "bf16-tiles", 4: "fused-split-f16"}.get(
@@ -555,7 +563,8 @@ def main():
         if train is not None:
             res["train"] = {k: train[k] for k in (
                 "metric", "batch", "step_ms", "samples_per_s", "forward_ms", "backward_ms",
-                "backward_tflops", "backward_frac_fp32_mfma", "loss_path")}
+                "backward_tflops", "backward_frac_fp32_mfma", "loss_path", "split_f16")
+                if k in train}
             res["train"]["note"] = ("V4 m=256 n=512 K=15 training step (zero_grad, forward with "
                                     "saved A Z_k, fused L1L1 objective with decay, reverse-sweep "
                                     "backward + split-K weight gradients, torch Adam); backward "
