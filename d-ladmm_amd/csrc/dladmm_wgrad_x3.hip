@@ -29,11 +29,6 @@
 #include "dladmm_internal.h"
 #include "dladmm_wgrad_x3.h"
 
-#ifndef WX3_EXP
-#define WX3_EXP 0  // timing probe (WRONG results): 1 read G / V as if column-blocked
-                   // [Bpad / 32][rows][32] (a sub-chunk tile = one contiguous 16 KiB)
-#endif
-
 namespace dladmm {
 
 namespace {
@@ -82,58 +77,61 @@ __device__ __forceinline__ void split8(const f32x4& p0, const f32x4& p1, float s
   }
 }
 
-constexpr int kSub = 32;                 // batch columns per sub-chunk (one k-step of 32)
-constexpr int kPieces = 32;              // 1-KiB pieces per sub-chunk: 16 G + 16 V
-#ifndef WX3_BUFS
-#define WX3_BUFS 2  // sub-chunk buffers per workgroup (4 at one workgroup per CU: 820 vs 677 us)
-#endif
-#ifndef WX3_OCC
-#define WX3_OCC 2   // workgroups per CU (two waves per SIMD hide the operand stream's latency)
-#endif
-constexpr int kBufs = WX3_BUFS;          // sub-chunk buffers: kBufs - 1 in flight beside the one read
+constexpr int kSub = 32;   // batch columns per sub-chunk (one k-step of 32)
+constexpr int kBufs = 2;   // sub-chunk buffers: the next one streams in while this one is read
 
-__global__ __launch_bounds__(256, WX3_OCC) void wgrad_x3_kernel(const WgradArgs a) {
-  __shared__ f32x4 img[kBufs * kPieces * 64];  // kBufs sub-chunk buffers of 32 KiB
+// Tile geometry by V-tile width TJ: 128 G rows x TJ V rows, waves of 64 x 64 (2 wave rows x
+// TJ / 64 wave columns); a sub-chunk is 16 G pieces + TJ / 8 V pieces of 1 KiB.  TJ = 128: 4
+// waves, 64 KiB of LDS, two workgroups per CU; TJ = 256: 8 waves, 96 KiB, one workgroup per CU
+// -- the same two waves per SIMD, and every G row is read once per V tile instead of twice.
+template <int TJ>
+struct WgX3 {
+  static constexpr int WC = TJ / 64, NW = 2 * WC;
+  static constexpr int GP = 16, VP = TJ / 8, PIECES = GP + VP, PPW = PIECES / NW;
+  static constexpr int OCC = TJ == 128 ? 2 : 1;
+  static_assert(PIECES % NW == 0, "even DMA share per wave");
+};
+
+template <int TJ>
+__global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_kernel(
+    const WgradArgs a) {
+  using T = WgX3<TJ>;
+  __shared__ f32x4 img[kBufs * T::PIECES * 64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = w >> 1, wc = w & 1;
-  const int tiles_m = a.MBp16 / 8;
+  const int wr = w / T::WC, wc = w % T::WC;
+  const int tiles_j = a.MBp16 / (TJ / 16);
   const int tile = blockIdx.x;
   const int64_t zl = blockIdx.z;
-  const int ti = tile / tiles_m, tj = tile % tiles_m;
+  const int ti = tile / tiles_j, tj = tile % tiles_j;
   const int64_t b0 = (int64_t)blockIdx.y * a.chunk;
   int64_t b1 = b0 + a.chunk;
   if (b1 > a.Bpad) b1 = a.Bpad;
   const int nsub = b1 > b0 ? (int)((b1 - b0) / kSub) : 0;
   const int r = lane & 15, g = lane >> 4;
 
-  // DMA: piece p = 16 op + 2 blk + hf (op 0 = G, 1 = V; blk = 16-row block of the tile; hf =
-  // 4-column half of the lane's 8): lane l copies row 16 blk + (l & 15), columns 8 (l >> 4) +
-  // 4 hf .. +3 of the sub-chunk.  Wave w issues pieces 8 w .. 8 w + 7: waves 0, 1 the G pieces,
-  // waves 2, 3 the V pieces.
-  const float* opb = w < 2 ? a.G + zl * a.gls + (int64_t)(ti * 128) * a.ld
-                           : a.V + zl * a.vls + (int64_t)(tj * 128) * a.ld;
+  // DMA: piece p < GP is G's (row block p / 2), else V's (row block (p - GP) / 2); hf = p & 1
+  // is the 4-column half of the lane's 8: lane l copies row 16 blk + (l & 15), columns
+  // 8 (l >> 4) + 4 hf .. +3 of the sub-chunk.  Wave w issues pieces PPW w .. PPW w + PPW - 1.
+  const float* gb = a.G + zl * a.gls + (int64_t)(ti * 128) * a.ld;
+  const float* vb = a.V + zl * a.vls + (int64_t)(tj * TJ) * a.ld;
   const uint32_t vl = (uint32_t)(((int64_t)r * a.ld + 8 * g) * 4);
-  const int64_t rows_b = (int64_t)(w < 2 ? a.NBp16 : a.MBp16) * 16;  // probe: rows per block
-  const float* opx = w < 2 ? a.G + zl * a.gls + (int64_t)(ti * 128) * 32
-                           : a.V + zl * a.vls + (int64_t)(tj * 128) * 32;
-  const uint32_t vlx = (uint32_t)((r * 32 + 8 * g) * 4);
   auto issue = [&](int sub, int buf) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int p = 8 * w + q, pp = p & 15;
-      const int blk = pp >> 1, hf = pp & 1;
-      if constexpr (WX3_EXP & 1) {
-        uint64_t sb = (uint64_t)(opx + ((b0 / kSub) + sub) * rows_b * 32 + (int64_t)(16 * blk) * 32 +
-                                 4 * hf);
-        asm volatile("" : "+s"(sb));
-        glds16((const float*)sb, vlx, img + (buf * kPieces + p) * 64);
-      } else {
-        uint64_t sb = (uint64_t)(opb + (int64_t)(16 * blk) * a.ld + b0 + (int64_t)kSub * sub +
-                                 4 * hf);
-        asm volatile("" : "+s"(sb));
-        glds16((const float*)sb, vl, img + (buf * kPieces + p) * 64);
-      }
+    for (int q = 0; q < T::PPW; ++q) {
+      const int p = T::PPW * w + q;
+      const bool isg = p < T::GP;
+      const int pp = isg ? p : p - T::GP;
+      const float* base = isg ? gb : vb;
+      uint64_t sb = (uint64_t)(base + (int64_t)(16 * (pp >> 1)) * a.ld + b0 +
+                               (int64_t)kSub * sub + 4 * (pp & 1));
+      // both halves through uint32_t: readfirstlane returns int, and a sign-extended low half
+      // (address bit 31 set) would overwrite the high half
+      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)sb);
+      const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(sb >> 32));
+      sb = ((uint64_t)hi << 32) | lo;
+      asm volatile("" : "+s"(sb));
+      glds16((const float*)sb, vl, img + (buf * T::PIECES + p) * 64);
     }
   };
 
@@ -143,11 +141,9 @@ __global__ __launch_bounds__(256, WX3_OCC) void wgrad_x3_kernel(const WgradArgs 
 #pragma unroll
     for (int y = 0; y < 4; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#pragma unroll
-  for (int b = 0; b < kBufs - 1; ++b)
-    if (b < nsub) issue(b, b);
+  if (nsub > 0) issue(0, 0);
   // Software-pipelined: iteration s reads and splits sub-chunk s, then runs the MFMAs of s - 1
-  // (split in the previous iteration) while the LDS reads of s + 1 ... are not yet needed.
+  // (split in the previous iteration) while the LDS reads of s land.
   h8 ah[4], al[4], bh[4], bl[4];
   float uns = 0.f;
   auto mfmas = [&]() {
@@ -164,26 +160,19 @@ __global__ __launch_bounds__(256, WX3_OCC) void wgrad_x3_kernel(const WgradArgs 
       }
   };
   for (int s = 0; s < nsub; ++s) {
-    // sub-chunk s landed for every wave; this wave's DMAs of the (up to two) sub-chunks after it
-    // may stay in flight (8 per sub-chunk)
-    const int younger = (nsub - 1 - s) < (kBufs - 2) ? (nsub - 1 - s) : (kBufs - 2);
-    if (younger >= 3) asm volatile("s_waitcnt vmcnt(24)\n\ts_barrier" ::: "memory");
-    else if (younger == 2) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    const f32x4* im = img + (s % kBufs) * kPieces * 64;
-    // this wave's operand values: G blocks 4 wr + x, V blocks 4 wc + x, both halves
+    // sub-chunk s landed for every wave; every wave is past its reads of sub-chunk s - 1
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    const f32x4* im = img + (s % kBufs) * T::PIECES * 64;
     f32x4 fa[4][2], fb[4][2];
 #pragma unroll
     for (int x = 0; x < 4; ++x)
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
         fa[x][hf] = im[((4 * wr + x) * 2 + hf) * 64 + lane];
-        fb[x][hf] = im[(16 + (4 * wc + x) * 2 + hf) * 64 + lane];
+        fb[x][hf] = im[(T::GP + (4 * wc + x) * 2 + hf) * 64 + lane];
       }
-    // the buffer of sub-chunk s - 1 is free (every wave's reads of it ended before the barrier
-    // above): it receives sub-chunk s + kBufs - 1
-    if (s + kBufs - 1 < nsub) issue(s + kBufs - 1, (s + kBufs - 1) % kBufs);
+    // the other buffer (sub-chunk s - 1's) is free: it receives sub-chunk s + 1
+    if (s + 1 < nsub) issue(s + 1, (s + 1) % kBufs);
     if (s > 0) mfmas();  // sub-chunk s - 1, while the reads above land
     float ma = 0.f, mb = 0.f;
 #pragma unroll
@@ -207,7 +196,7 @@ __global__ __launch_bounds__(256, WX3_OCC) void wgrad_x3_kernel(const WgradArgs 
   if (nsub > 0) mfmas();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA in flight when the LDS is released
   // C/D layout: lane holds column (l & 15) = V row j, rows 4 g + q = G rows
-  const int i0 = ti * 128 + wr * 64, j0 = tj * 128 + wc * 64;
+  const int i0 = ti * 128 + wr * 64, j0 = tj * TJ + wc * 64;
   float* out = a.part + zl * a.pls + (int64_t)blockIdx.y * a.n * a.m;
 #pragma unroll
   for (int x = 0; x < 4; ++x)
@@ -224,8 +213,20 @@ __global__ __launch_bounds__(256, WX3_OCC) void wgrad_x3_kernel(const WgradArgs 
 }  // namespace
 
 hipError_t launch_wgrad_x3(const WgradArgs& a, int tiles, hipStream_t s, int layers) {
+  (void)tiles;  // the tile count follows the V-tile width chosen here
   if (!wgrad_x3_fits(a)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(wgrad_x3_kernel, dim3(tiles, a.nchunks, layers), dim3(256), 0, s, a);
+  // 256-row V tiles where the padded V rows allow (DLADMM_WGRAD_X3_TJ=128 forces the narrow
+  // form: A/B)
+  const char* e = getenv("DLADMM_WGRAD_X3_TJ");
+  const bool wide = a.MBp16 % 16 == 0 && !(e && atoi(e) == 128);
+  const int ti = a.NBp16 / 8;
+  if (wide) {
+    hipLaunchKernelGGL((wgrad_x3_kernel<256>), dim3(ti * (a.MBp16 / 16), a.nchunks, layers),
+                       dim3(WgX3<256>::NW * 64), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((wgrad_x3_kernel<128>), dim3(ti * (a.MBp16 / 8), a.nchunks, layers),
+                       dim3(WgX3<128>::NW * 64), 0, s, a);
+  }
   return hipGetLastError();
 }
 
