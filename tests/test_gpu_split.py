@@ -282,3 +282,32 @@ def test_split_weight_gradient_on_f16_cores(variant, dl, monkeypatch):
             assert float((a - b).norm() / b.norm()) <= 1e-5, k
         else:
             assert torch.equal(grads["1"][k], grads["0"][k]), k
+
+
+@pytest.mark.parametrize("tj", ["256", "128"])
+def test_split_weight_gradient_full_batch(tj, dl, monkeypatch):
+    """The split-f16 weight gradient at the bench's batch (B = 65,536: 32 sub-chunks per split-K
+    chunk, multi-GiB operand buffers whose addresses cross bit 31) in both V-tile widths
+    (DLADMM_WGRAD_X3_TJ): the fc* gradients stay within 1e-5 of the fp32-MFMA kernel's."""
+    from test_gpu_backward import make_train_net
+    m, n, B, K = 256, 512, 65536, 2
+    inp = P.make_inputs(m, n, B, 7717)
+    sd = P.make_state_dict("v4", m, n, B, K, inp["A"], 7717, perturb=0.1)
+    X = torch.from_numpy(inp["X"]).cuda()
+    monkeypatch.setenv("DLADMM_WGRAD_X3_TJ", tj)
+    grads = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DLADMM_WGRAD_X3", mode)
+        net = make_train_net(dl, "v4", inp, sd, K)
+        net.precision = "f32_split"
+        tot, _ = net.training_loss(X, 1e-3, [0.6, 1.0], "l1l1")
+        tot.backward()
+        torch.cuda.synchronize()
+        grads[mode] = {k: p.grad.detach().clone() for k, p in net.named_parameters()
+                       if p.grad is not None and k.startswith("fc")}
+        del net, tot
+    assert grads["0"]
+    for k, b in grads["0"].items():
+        a = grads["1"][k].double()
+        assert torch.isfinite(a).all(), k
+        assert float((a - b.double()).norm() / b.double().norm()) <= 1e-5, k
