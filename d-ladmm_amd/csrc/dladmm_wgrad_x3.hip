@@ -62,23 +62,33 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // 8 consecutive k-values (two 16-B pieces) -> hi / lo halves at scale sc: hi = f16(x sc),
-// lo = f16(x sc - hi), each one RNE rounding of an exact value (the forms lower to
-// v_fma_mix{lo,hi}_f16, as in the split-f16 forward)
+// lo = f16(x sc - hi), each one RNE rounding of an exact value.  Per pair of values: one packed
+// multiply and one v_cvt_pk_f16_f32 form the hi pair; v_fma_mixlo / mixhi form each lo straight
+// from x, sc and the f16 hi (2 VALU per value; the compiler's own lowering of the same
+// expressions converted hi back to f32 first, ~2.9 per value)
 __device__ __forceinline__ void split8(const f32x4& p0, const f32x4& p1, float sc, h8& hi,
                                        h8& lo) {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  uint32_t H[4], L[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const _Float16 h0 = (_Float16)__builtin_fmaf(p0[q], sc, 0.0f);
-    const _Float16 h1 = (_Float16)__builtin_fmaf(p1[q], sc, 0.0f);
-    hi[q] = h0;
-    hi[4 + q] = h1;
-    lo[q] = (_Float16)__builtin_fmaf(p0[q], sc, -(float)h0);
-    lo[4 + q] = (_Float16)__builtin_fmaf(p1[q], sc, -(float)h1);
+  for (int k = 0; k < 4; ++k) {
+    const float x0 = k < 2 ? p0[2 * k] : p1[2 * k - 4];
+    const float x1 = k < 2 ? p0[2 * k + 1] : p1[2 * k - 3];
+    const f32x2 y = f32x2{x0, x1} * f32x2{sc, sc};  // exact: sc is a power of two
+    const h2 hp = __builtin_convertvector(y, h2);
+    H[k] = __builtin_bit_cast(uint32_t, hp);
+    asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]"
+        : "=v"(L[k]) : "v"(x0), "v"(sc), "v"(H[k]));
+    asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "+v"(L[k]) : "v"(x1), "v"(sc), "v"(H[k]));
   }
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  hi = __builtin_bit_cast(h8, u32x4{H[0], H[1], H[2], H[3]});
+  lo = __builtin_bit_cast(h8, u32x4{L[0], L[1], L[2], L[3]});
 }
 
 constexpr int kSub = 32;   // batch columns per sub-chunk (one k-step of 32)
-constexpr int kBufs = 2;   // sub-chunk buffers: the next one streams in while this one is read
 
 // Tile geometry by V-tile width TJ: 128 G rows x TJ V rows, waves of 64 x 64 (2 wave rows x
 // TJ / 64 wave columns); a sub-chunk is 16 G pieces + TJ / 8 V pieces of 1 KiB.  TJ = 128: 4
@@ -92,19 +102,38 @@ struct WgX3 {
   static_assert(PIECES % NW == 0, "even DMA share per wave");
 };
 
-template <int TJ>
+// RUN: one running scale per operand over the chunk (below) instead of one per sub-chunk.
+// NBUF sub-chunk buffers: NBUF - 1 sub-chunks stream in while one is read.
+template <int TJ, bool RUN, int NBUF>
 __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_kernel(
-    const WgradArgs a) {
+    const WgradArgs a, int xcd) {
   using T = WgX3<TJ>;
+  constexpr int kBufs = NBUF;
+  static_assert(NBUF == 2 || NBUF == 3, "two or three sub-chunk buffers");
   __shared__ f32x4 img[kBufs * T::PIECES * 64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = w / T::WC, wc = w % T::WC;
   const int tiles_j = a.MBp16 / (TJ / 16);
-  const int tile = blockIdx.x;
-  const int64_t zl = blockIdx.z;
+  const int ntiles = (a.NBp16 / 8) * tiles_j;
+  // 1-D grid over (tile, chunk, layer).  Workgroups are dispatched to the 8 XCDs round-robin by
+  // linear id; xcd: the ntiles tiles of one (chunk, layer) go to ONE XCD, back to back, so its
+  // L2 serves their shared operand rows (each V row block is read by every G tile) once from
+  // HBM.  Otherwise consecutive ids: the tiles of a chunk spread over XCDs.
+  const int L = blockIdx.x;
+  int tile, grp;
+  if (xcd) {
+    const int slot = L >> 3;
+    tile = slot % ntiles;
+    grp = (slot / ntiles) * 8 + (L & 7);
+  } else {
+    tile = L % ntiles;
+    grp = L / ntiles;
+  }
+  const int64_t zl = grp / a.nchunks;
+  const int cy = grp % a.nchunks;
   const int ti = tile / tiles_j, tj = tile % tiles_j;
-  const int64_t b0 = (int64_t)blockIdx.y * a.chunk;
+  const int64_t b0 = (int64_t)cy * a.chunk;
   int64_t b1 = b0 + a.chunk;
   if (b1 > a.Bpad) b1 = a.Bpad;
   const int nsub = b1 > b0 ? (int)((b1 - b0) / kSub) : 0;
@@ -142,26 +171,54 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
     for (int y = 0; y < 4; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (nsub > 0) issue(0, 0);
+  if (kBufs == 3 && nsub > 1) issue(1, 1);
   // Software-pipelined: iteration s reads and splits sub-chunk s, then runs the MFMAs of s - 1
   // (split in the previous iteration) while the LDS reads of s land.
   h8 ah[4], al[4], bh[4], bl[4];
   float uns = 0.f;
+  // RUN: the accumulators hold the sum at scale 2^(ea + eb), where 2^ea / 2^eb put the largest
+  // G / V magnitude of this wave's rows SO FAR in the chunk in [2^14, 2^15); a sub-chunk that
+  // exceeds it (any lane at or above lim) lowers the exponent and rescales the accumulators by
+  // the exact power of two, so the MFMAs accumulate straight into them and the per-sub-chunk
+  // unscale and both wave maxima drop out of the steady state.  127: no magnitude >= 2^-112 seen.
+  int ea = 127, eb = 127;
+  float sa = ldexpf(1.0f, 127), sbs = sa, lima = ldexpf(1.0f, -112), limb = lima;
   auto mfmas = [&]() {
+    if constexpr (RUN) {
+      // three passes over the 16 independent accumulators (no back-to-back dependent MFMAs)
 #pragma unroll
-    for (int x = 0; x < 4; ++x)
+      for (int x = 0; x < 4; ++x)
 #pragma unroll
-      for (int y = 0; y < 4; ++y) {
-        f32x4 c = {0.f, 0.f, 0.f, 0.f};
-        c = mfma_h(ah[x], bh[y], c);
-        c = mfma_h(ah[x], bl[y], c);
-        c = mfma_h(al[x], bh[y], c);
+        for (int y = 0; y < 4; ++y) acc[x][y] = mfma_h(ah[x], bh[y], acc[x][y]);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[x][y][q] = __builtin_fmaf(c[q], uns, acc[x][y][q]);
-      }
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = mfma_h(ah[x], bl[y], acc[x][y]);
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = mfma_h(al[x], bh[y], acc[x][y]);
+    } else {
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          f32x4 c = {0.f, 0.f, 0.f, 0.f};
+          c = mfma_h(ah[x], bh[y], c);
+          c = mfma_h(ah[x], bl[y], c);
+          c = mfma_h(al[x], bh[y], c);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[x][y][q] = __builtin_fmaf(c[q], uns, acc[x][y][q]);
+        }
+    }
   };
   for (int s = 0; s < nsub; ++s) {
-    // sub-chunk s landed for every wave; every wave is past its reads of sub-chunk s - 1
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    // sub-chunk s landed for every wave (three buffers: this wave's PPW DMAs of s + 1 may stay
+    // in flight); every wave is past its reads of sub-chunk s - 1
+    if (kBufs == 3 && s + 1 < nsub)
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(T::PPW) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     const f32x4* im = img + (s % kBufs) * T::PIECES * 64;
     f32x4 fa[4][2], fb[4][2];
 #pragma unroll
@@ -171,8 +228,8 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
         fa[x][hf] = im[((4 * wr + x) * 2 + hf) * 64 + lane];
         fb[x][hf] = im[(T::GP + (4 * wc + x) * 2 + hf) * 64 + lane];
       }
-    // the other buffer (sub-chunk s - 1's) is free: it receives sub-chunk s + 1
-    if (s + 1 < nsub) issue(s + 1, (s + 1) % kBufs);
+    // sub-chunk s - 1's buffer is free: it receives sub-chunk s + kBufs - 1
+    if (s + kBufs - 1 < nsub) issue(s + kBufs - 1, (s + kBufs - 1) % kBufs);
     if (s > 0) mfmas();  // sub-chunk s - 1, while the reads above land
     float ma = 0.f, mb = 0.f;
 #pragma unroll
@@ -184,9 +241,34 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
           ma = fmaxf(ma, fabsf(fa[x][hf][q]));
           mb = fmaxf(mb, fabsf(fb[x][hf][q]));
         }
-    const int ea = split_exp(wave_max(ma)), eb = split_exp(wave_max(mb));
-    const float sa = ldexpf(1.0f, ea), sbs = ldexpf(1.0f, eb);
-    uns = ldexpf(1.0f, -(ea + eb));
+    if constexpr (RUN) {
+      // (after the MFMAs of s - 1, which used the old scales)
+      const bool ga = __builtin_amdgcn_ballot_w64(ma >= lima) != 0;
+      const bool gb = __builtin_amdgcn_ballot_w64(mb >= limb) != 0;
+      if (ga || gb) {
+        const int na = ga ? split_exp(wave_max(ma)) : ea;
+        const int nb = gb ? split_exp(wave_max(mb)) : eb;
+        const float fa2 = ldexpf(1.0f, na - ea), fb2 = ldexpf(1.0f, nb - eb);
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int y = 0; y < 4; ++y)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[x][y][q] = acc[x][y][q] * fa2 * fb2;
+        ea = na;
+        eb = nb;
+        sa = ldexpf(1.0f, ea);
+        sbs = ldexpf(1.0f, eb);
+        lima = ldexpf(1.0f, 15 - ea);
+        limb = ldexpf(1.0f, 15 - eb);
+      }
+    } else {
+      ea = split_exp(wave_max(ma));
+      eb = split_exp(wave_max(mb));
+      sa = ldexpf(1.0f, ea);
+      sbs = ldexpf(1.0f, eb);
+      uns = ldexpf(1.0f, -(ea + eb));
+    }
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       split8(fa[x][0], fa[x][1], sa, ah[x], al[x]);
@@ -194,10 +276,20 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
     }
   }
   if (nsub > 0) mfmas();
+  if constexpr (RUN) {
+    // one exact unscale (two factors: 2^-(ea + eb) alone could leave the float range)
+    const float ua = ldexpf(1.0f, -ea), ub = ldexpf(1.0f, -eb);
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[x][y][q] = acc[x][y][q] * ua * ub;
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA in flight when the LDS is released
   // C/D layout: lane holds column (l & 15) = V row j, rows 4 g + q = G rows
   const int i0 = ti * 128 + wr * 64, j0 = tj * TJ + wc * 64;
-  float* out = a.part + zl * a.pls + (int64_t)blockIdx.y * a.n * a.m;
+  float* out = a.part + zl * a.pls + (int64_t)cy * a.n * a.m;
 #pragma unroll
   for (int x = 0; x < 4; ++x)
 #pragma unroll
@@ -220,13 +312,25 @@ hipError_t launch_wgrad_x3(const WgradArgs& a, int tiles, hipStream_t s, int lay
   const char* e = getenv("DLADMM_WGRAD_X3_TJ");
   const bool wide = a.MBp16 % 16 == 0 && !(e && atoi(e) == 128);
   const int ti = a.NBp16 / 8;
-  if (wide) {
-    hipLaunchKernelGGL((wgrad_x3_kernel<256>), dim3(ti * (a.MBp16 / 16), a.nchunks, layers),
-                       dim3(WgX3<256>::NW * 64), 0, s, a);
-  } else {
-    hipLaunchKernelGGL((wgrad_x3_kernel<128>), dim3(ti * (a.MBp16 / 8), a.nchunks, layers),
-                       dim3(WgX3<128>::NW * 64), 0, s, a);
-  }
+  // running scales over the chunk (DLADMM_WGRAD_X3_RUN=0: one scale per sub-chunk, A/B);
+  // XCD-grouped tiles where the (chunk, layer) count is a multiple of 8 (DLADMM_WGRAD_X3_XCD=0:
+  // consecutive ids, A/B)
+  const char* r = getenv("DLADMM_WGRAD_X3_RUN");
+  const bool run = !(r && atoi(r) == 0);
+  const char* x = getenv("DLADMM_WGRAD_X3_XCD");
+  const int groups = a.nchunks * layers;
+  const int xcd = groups % 8 == 0 && !(x && atoi(x) == 0) ? 1 : 0;
+  const int nt = ti * (wide ? a.MBp16 / 16 : a.MBp16 / 8);
+  // three sub-chunk buffers at the 256 width (144 KiB: two sub-chunks in flight;
+  // DLADMM_WGRAD_X3_BUFS=2: one, A/B)
+  const char* b = getenv("DLADMM_WGRAD_X3_BUFS");
+  const bool b3 = wide && run && !(b && atoi(b) == 2);
+  const dim3 grid(nt * groups), bw(WgX3<256>::NW * 64), bn(WgX3<128>::NW * 64);
+  if (b3) hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 3>), grid, bw, 0, s, a, xcd);
+  else if (wide && run) hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 2>), grid, bw, 0, s, a, xcd);
+  else if (wide) hipLaunchKernelGGL((wgrad_x3_kernel<256, false, 2>), grid, bw, 0, s, a, xcd);
+  else if (run) hipLaunchKernelGGL((wgrad_x3_kernel<128, true, 2>), grid, bn, 0, s, a, xcd);
+  else hipLaunchKernelGGL((wgrad_x3_kernel<128, false, 2>), grid, bn, 0, s, a, xcd);
   return hipGetLastError();
 }
 

@@ -284,17 +284,24 @@ def test_split_weight_gradient_on_f16_cores(variant, dl, monkeypatch):
             assert torch.equal(grads["1"][k], grads["0"][k]), k
 
 
-@pytest.mark.parametrize("tj", ["256", "128"])
-def test_split_weight_gradient_full_batch(tj, dl, monkeypatch):
+@pytest.mark.parametrize("tj,run,ramp", [("256", "1", False), ("128", "1", False),
+                                         ("256", "1", True), ("256", "0", True)])
+def test_split_weight_gradient_full_batch(tj, run, ramp, dl, monkeypatch):
     """The split-f16 weight gradient at the bench's batch (B = 65,536: 32 sub-chunks per split-K
     chunk, multi-GiB operand buffers whose addresses cross bit 31) in both V-tile widths
-    (DLADMM_WGRAD_X3_TJ): the fc* gradients stay within 1e-5 of the fp32-MFMA kernel's."""
+    (DLADMM_WGRAD_X3_TJ) and both scale policies (DLADMM_WGRAD_X3_RUN: running per-chunk scales,
+    or one per sub-chunk): the fc* gradients stay within 1e-5 of the fp32-MFMA kernel's.  ramp:
+    X's columns grow by 2^12 across every 1,024-column chunk, so the running scales drop many
+    times inside a chunk (each an exact power-of-two rescale of the accumulators)."""
     from test_gpu_backward import make_train_net
     m, n, B, K = 256, 512, 65536, 2
     inp = P.make_inputs(m, n, B, 7717)
     sd = P.make_state_dict("v4", m, n, B, K, inp["A"], 7717, perturb=0.1)
     X = torch.from_numpy(inp["X"]).cuda()
+    if ramp:
+        X = X * torch.exp2(12.0 * (torch.arange(B, device=X.device) % 1024) / 1024 - 6.0)
     monkeypatch.setenv("DLADMM_WGRAD_X3_TJ", tj)
+    monkeypatch.setenv("DLADMM_WGRAD_X3_RUN", run)
     grads = {}
     for mode in ("0", "1"):
         monkeypatch.setenv("DLADMM_WGRAD_X3", mode)
