@@ -8,23 +8,27 @@
 // backward at the headline shape).  Here each 16 x 16 x 32 block is three
 // v_mfma_f32_16x16x32_f16 (hi hi + hi lo + lo hi) at 16x the f32 MFMA's rate per instruction.
 //
-// Numerics.  Per 32-column sub-chunk every wave scales its own operand values (its 64 G rows and
-// its 64 V rows) by powers of two that put their largest magnitude in [2^14, 2^15), splits each
-// x into hi = f16(x s), lo = f16(x s - hi) (22 significant bits; both roundings exact-input RNE),
-// accumulates the three products in fp32 by MFMA over the sub-chunk, and adds the sub-chunk's sum
-// to the running fp32 accumulator after one exact power-of-two unscale.  The dropped lo lo term is
-// 2^-22 of a product; elements more than 2^-29 below their sub-tile's largest go subnormal in
-// f16, i.e. contribute below 2^-29 of that largest product.  Fixed order throughout: the result is
-// deterministic.  Not bit-equal to wgrad_kernel (a different rounding sequence of the same sum).
+// Numerics.  Every wave scales its own operand values (its 64 G rows and its 64 V rows) by powers
+// of two that put their largest magnitude SO FAR in the chunk in [2^14, 2^15), splits each x into
+// hi = f16(x s), lo = f16(x s - hi) (22 significant bits; both roundings exact-input RNE) and
+// accumulates the three products by MFMA straight into fp32 accumulators held at scale
+// 2^(ea + eb).  A 32-column sub-chunk with a larger magnitude (one ballot per sub-chunk detects
+// it) lowers the exponent and rescales the accumulators by the exact power of two; one exact
+// unscale at the end.  The dropped lo lo term is 2^-22 of a product; elements more than 2^-29
+// below the running largest go subnormal in f16, i.e. contribute below 2^-29 of that largest
+// product.  Fixed order throughout: the result is deterministic.  Not bit-equal to wgrad_kernel
+// (a different rounding sequence of the same sum).  DLADMM_WGRAD_X3_RUN=0: one scale per
+// sub-chunk and an unscale-add per sub-chunk (the first form, A/B).
 //
-// Geometry.  Grid and partial layout of wgrad_kernel: a workgroup = 4 waves over a 128 x 128
-// output tile (wave (wr, wc): G rows 64 wr .., V rows 64 wc ..), one chunk of batch columns.
-// Operands reach LDS by LDS-DMA in MFMA fragment order (a 1-KiB piece = 16 rows x 4 columns per
-// lane-quarter, so every fragment read is one conflict-free ds_read_b128): per 32-column
-// sub-chunk 16 G and 16 V pieces (32 KiB), two buffers (64 KiB), two workgroups per CU: the
-// operands stream from HBM and the second workgroup's waves cover their latency (measured: 677
-// us per 8-layer launch against 820 for four buffers at one workgroup per CU and 990 for
-// wgrad_kernel, profiles/r05_wgrad_x3.json).
+// Geometry.  Partial layout of wgrad_kernel, a 1-D grid over (tile, chunk, layer).  A workgroup
+// covers 128 G rows x TJ V rows (TJ = 256 where the padded V rows allow: 8 waves of 64 x 64, one
+// workgroup per CU; else 128: 4 waves, two per CU), one chunk of batch columns; the tiles of one
+// (chunk, layer) run on one XCD so its L2 serves their shared V rows.  Operands reach LDS by
+// LDS-DMA in MFMA fragment order (a 1-KiB piece = 16 rows x 4 columns per lane-quarter, so every
+// fragment read is one conflict-free ds_read_b128); per 32-column sub-chunk 16 G and TJ / 8 V
+// pieces, three buffers at TJ = 256 (144 KiB: two sub-chunks in flight), two at 128.  Measured
+// (profiles/r05_wgrad_x3.json, r05_wgrad_tj.json, r05_wgrad_x3_steps.json): 561 us per 8-layer
+// launch at the headline shape against 662 for the round's first form and 990 for wgrad_kernel.
 #include "dladmm_common.h"
 #include "dladmm_internal.h"
 #include "dladmm_wgrad_x3.h"
@@ -103,8 +107,11 @@ struct WgX3 {
 };
 
 // RUN: one running scale per operand over the chunk (below) instead of one per sub-chunk.
-// NBUF sub-chunk buffers: NBUF - 1 sub-chunks stream in while one is read.
-template <int TJ, bool RUN, int NBUF>
+// NBUF sub-chunk buffers: NBUF - 1 sub-chunks stream in while one is read.  SPEC (with RUN):
+// split each sub-chunk speculatively at the running scales in the same straight-line block as the
+// previous sub-chunk's MFMAs (two operand register sets), re-splitting in the rare case a
+// magnitude reached them.
+template <int TJ, bool RUN, int NBUF, bool SPEC = false>
 __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_kernel(
     const WgradArgs a, int xcd) {
   using T = WgX3<TJ>;
@@ -212,70 +219,163 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
         }
     }
   };
-  for (int s = 0; s < nsub; ++s) {
+  auto wait_bar = [&](int s) {
     // sub-chunk s landed for every wave (three buffers: this wave's PPW DMAs of s + 1 may stay
     // in flight); every wave is past its reads of sub-chunk s - 1
     if (kBufs == 3 && s + 1 < nsub)
       asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(T::PPW) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    const f32x4* im = img + (s % kBufs) * T::PIECES * 64;
-    f32x4 fa[4][2], fb[4][2];
+  };
+  if constexpr (RUN && SPEC) {
+    struct Ops { h8 ah[4], al[4], bh[4], bl[4]; };
+    Ops P, Q;
+    // sub-chunk s split at the current scales into o; ma / mb: this lane's magnitudes; true when
+    // one reached its scale's limit somewhere in the wave (o then holds overflowed halves)
+    auto split_sub = [&](int s, Ops& o, float& ma, float& mb) -> bool {
+      const f32x4* im = img + (s % kBufs) * T::PIECES * 64;
+      ma = 0.f;
+      mb = 0.f;
 #pragma unroll
-    for (int x = 0; x < 4; ++x)
+      for (int x = 0; x < 4; ++x) {
+        const f32x4 p0 = im[((4 * wr + x) * 2) * 64 + lane], p1 = im[((4 * wr + x) * 2 + 1) * 64 + lane];
 #pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        fa[x][hf] = im[((4 * wr + x) * 2 + hf) * 64 + lane];
-        fb[x][hf] = im[(T::GP + (4 * wc + x) * 2 + hf) * 64 + lane];
+        for (int q = 0; q < 4; ++q) ma = fmaxf(ma, fmaxf(fabsf(p0[q]), fabsf(p1[q])));
+        split8(p0, p1, sa, o.ah[x], o.al[x]);
       }
-    // sub-chunk s - 1's buffer is free: it receives sub-chunk s + kBufs - 1
-    if (s + kBufs - 1 < nsub) issue(s + kBufs - 1, (s + kBufs - 1) % kBufs);
-    if (s > 0) mfmas();  // sub-chunk s - 1, while the reads above land
-    float ma = 0.f, mb = 0.f;
 #pragma unroll
-    for (int x = 0; x < 4; ++x)
+      for (int y = 0; y < 4; ++y) {
+        const f32x4 p0 = im[(T::GP + (4 * wc + y) * 2) * 64 + lane];
+        const f32x4 p1 = im[(T::GP + (4 * wc + y) * 2 + 1) * 64 + lane];
 #pragma unroll
-      for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          ma = fmaxf(ma, fabsf(fa[x][hf][q]));
-          mb = fmaxf(mb, fabsf(fb[x][hf][q]));
-        }
-    if constexpr (RUN) {
-      // (after the MFMAs of s - 1, which used the old scales)
+        for (int q = 0; q < 4; ++q) mb = fmaxf(mb, fmaxf(fabsf(p0[q]), fabsf(p1[q])));
+        split8(p0, p1, sbs, o.bh[y], o.bl[y]);
+      }
+      return (__builtin_amdgcn_ballot_w64(ma >= lima) | __builtin_amdgcn_ballot_w64(mb >= limb)) != 0;
+    };
+    // rare: lower the scales, rescale the accumulators (every MFMA at the old scales precedes
+    // this in program order) and split sub-chunk s again
+    auto grow = [&](int s, Ops& o, float ma, float mb) {
       const bool ga = __builtin_amdgcn_ballot_w64(ma >= lima) != 0;
       const bool gb = __builtin_amdgcn_ballot_w64(mb >= limb) != 0;
-      if (ga || gb) {
-        const int na = ga ? split_exp(wave_max(ma)) : ea;
-        const int nb = gb ? split_exp(wave_max(mb)) : eb;
-        const float fa2 = ldexpf(1.0f, na - ea), fb2 = ldexpf(1.0f, nb - eb);
+      const int na = ga ? split_exp(wave_max(ma)) : ea;
+      const int nb = gb ? split_exp(wave_max(mb)) : eb;
+      const float fa2 = ldexpf(1.0f, na - ea), fb2 = ldexpf(1.0f, nb - eb);
 #pragma unroll
-        for (int x = 0; x < 4; ++x)
+      for (int x = 0; x < 4; ++x)
 #pragma unroll
-          for (int y = 0; y < 4; ++y)
+        for (int y = 0; y < 4; ++y)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) acc[x][y][q] = acc[x][y][q] * fa2 * fb2;
-        ea = na;
-        eb = nb;
-        sa = ldexpf(1.0f, ea);
-        sbs = ldexpf(1.0f, eb);
-        lima = ldexpf(1.0f, 15 - ea);
-        limb = ldexpf(1.0f, 15 - eb);
-      }
-    } else {
-      ea = split_exp(wave_max(ma));
-      eb = split_exp(wave_max(mb));
+          for (int q = 0; q < 4; ++q) acc[x][y][q] = acc[x][y][q] * fa2 * fb2;
+      ea = na;
+      eb = nb;
       sa = ldexpf(1.0f, ea);
       sbs = ldexpf(1.0f, eb);
-      uns = ldexpf(1.0f, -(ea + eb));
-    }
+      lima = ldexpf(1.0f, 15 - ea);
+      limb = ldexpf(1.0f, 15 - eb);
+      float m2a, m2b;
+      (void)split_sub(s, o, m2a, m2b);
+    };
+    auto mf = [&](const Ops& o) {
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      split8(fa[x][0], fa[x][1], sa, ah[x], al[x]);
-      split8(fb[x][0], fb[x][1], sbs, bh[x], bl[x]);
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = mfma_h(o.ah[x], o.bh[y], acc[x][y]);
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = mfma_h(o.ah[x], o.bl[y], acc[x][y]);
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = mfma_h(o.al[x], o.bh[y], acc[x][y]);
+    };
+    // iteration s: MFMAs of s - 1 (cur) and the split of s (nxt) in one block
+    auto step = [&](int s, Ops& cur, Ops& nxt) {
+      wait_bar(s);
+      if (s + kBufs - 1 < nsub) issue(s + kBufs - 1, (s + kBufs - 1) % kBufs);
+      mf(cur);
+      float ma, mb;
+      if (split_sub(s, nxt, ma, mb)) grow(s, nxt, ma, mb);
+    };
+    if (nsub > 0) {
+      wait_bar(0);
+      if (kBufs - 1 < nsub) issue(kBufs - 1, (kBufs - 1) % kBufs);
+      float ma, mb;
+      if (split_sub(0, P, ma, mb)) grow(0, P, ma, mb);
+      int s = 1;
+      for (; s + 1 < nsub; s += 2) {
+        step(s, P, Q);
+        step(s + 1, Q, P);
+      }
+      if (s < nsub) {
+        step(s, P, Q);
+        mf(Q);
+      } else {
+        mf(P);
+      }
     }
+  } else {
+    for (int s = 0; s < nsub; ++s) {
+      wait_bar(s);
+      const f32x4* im = img + (s % kBufs) * T::PIECES * 64;
+      f32x4 fa[4][2], fb[4][2];
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          fa[x][hf] = im[((4 * wr + x) * 2 + hf) * 64 + lane];
+          fb[x][hf] = im[(T::GP + (4 * wc + x) * 2 + hf) * 64 + lane];
+        }
+      // sub-chunk s - 1's buffer is free: it receives sub-chunk s + kBufs - 1
+      if (s + kBufs - 1 < nsub) issue(s + kBufs - 1, (s + kBufs - 1) % kBufs);
+      if (s > 0) mfmas();  // sub-chunk s - 1, while the reads above land
+      float ma = 0.f, mb = 0.f;
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            ma = fmaxf(ma, fabsf(fa[x][hf][q]));
+            mb = fmaxf(mb, fabsf(fb[x][hf][q]));
+          }
+      if constexpr (RUN) {
+        // (after the MFMAs of s - 1, which used the old scales)
+        const bool ga = __builtin_amdgcn_ballot_w64(ma >= lima) != 0;
+        const bool gb = __builtin_amdgcn_ballot_w64(mb >= limb) != 0;
+        if (ga || gb) {
+          const int na = ga ? split_exp(wave_max(ma)) : ea;
+          const int nb = gb ? split_exp(wave_max(mb)) : eb;
+          const float fa2 = ldexpf(1.0f, na - ea), fb2 = ldexpf(1.0f, nb - eb);
+#pragma unroll
+          for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) acc[x][y][q] = acc[x][y][q] * fa2 * fb2;
+          ea = na;
+          eb = nb;
+          sa = ldexpf(1.0f, ea);
+          sbs = ldexpf(1.0f, eb);
+          lima = ldexpf(1.0f, 15 - ea);
+          limb = ldexpf(1.0f, 15 - eb);
+        }
+      } else {
+        ea = split_exp(wave_max(ma));
+        eb = split_exp(wave_max(mb));
+        sa = ldexpf(1.0f, ea);
+        sbs = ldexpf(1.0f, eb);
+        uns = ldexpf(1.0f, -(ea + eb));
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        split8(fa[x][0], fa[x][1], sa, ah[x], al[x]);
+        split8(fb[x][0], fb[x][1], sbs, bh[x], bl[x]);
+      }
+    }
+    if (nsub > 0) mfmas();
   }
-  if (nsub > 0) mfmas();
   if constexpr (RUN) {
     // one exact unscale (two factors: 2^-(ea + eb) alone could leave the float range)
     const float ua = ldexpf(1.0f, -ea), ub = ldexpf(1.0f, -eb);
@@ -326,7 +426,12 @@ hipError_t launch_wgrad_x3(const WgradArgs& a, int tiles, hipStream_t s, int lay
   const char* b = getenv("DLADMM_WGRAD_X3_BUFS");
   const bool b3 = wide && run && !(b && atoi(b) == 2);
   const dim3 grid(nt * groups), bw(WgX3<256>::NW * 64), bn(WgX3<128>::NW * 64);
-  if (b3) hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 3>), grid, bw, 0, s, a, xcd);
+  // speculative split beside the MFMAs: opt-in (DLADMM_WGRAD_X3_SPEC=1), measured slower
+  // (609-613 vs 561 us, profiles/r05_wgrad_x3_steps.json)
+  const char* sp = getenv("DLADMM_WGRAD_X3_SPEC");
+  const bool spec = b3 && sp && atoi(sp) == 1;
+  if (spec) hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 3, true>), grid, bw, 0, s, a, xcd);
+  else if (b3) hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 3>), grid, bw, 0, s, a, xcd);
   else if (wide && run) hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 2>), grid, bw, 0, s, a, xcd);
   else if (wide) hipLaunchKernelGGL((wgrad_x3_kernel<256, false, 2>), grid, bw, 0, s, a, xcd);
   else if (run) hipLaunchKernelGGL((wgrad_x3_kernel<128, true, 2>), grid, bn, 0, s, a, xcd);
