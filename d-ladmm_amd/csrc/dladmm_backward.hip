@@ -486,15 +486,31 @@ __global__ __launch_bounds__(NW * 64, BWD_MIN_WG) void bwd_kernel(const BwdArgs 
 // per CU.  (The previous form loaded the operands into registers one step ahead: 178 us per
 // layer at B = 65,536, latency-bound.)
 constexpr int kWgStages = 4;
-__global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
+//
+// 1-D grid over (tile, chunk, layer).  Workgroups reach the 8 XCDs round-robin by linear id; with
+// xcd set the tiles of one (chunk, layer) run on one XCD back to back, so its L2 serves the G and
+// V row blocks they share (each V block is read by every G tile, each G block by every V tile)
+// once from HBM.  Without it, consecutive ids spread a chunk's tiles over the XCDs.
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a, int xcd) {
   __shared__ f32x4 ring[kWgStages * 16 * 64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tiles_m = a.MBp16 / 8;  // 128-column tiles (of V rows)
-  const int tile = blockIdx.x;
-  const int64_t zl = blockIdx.z;   // layer of a batched launch
+  const int ntiles = (a.NBp16 / 8) * tiles_m;
+  const int L = blockIdx.x;
+  int tile, grp;
+  if (xcd) {
+    const int slot = L >> 3;
+    tile = slot % ntiles;
+    grp = (slot / ntiles) * 8 + (L & 7);
+  } else {
+    tile = L % ntiles;
+    grp = L / ntiles;
+  }
+  const int64_t zl = grp / a.nchunks;  // layer of a batched launch
+  const int cy = grp % a.nchunks;
   const int ti = tile / tiles_m, tj = tile % tiles_m;
-  const int64_t b0 = (int64_t)blockIdx.y * a.chunk;
+  const int64_t b0 = (int64_t)cy * a.chunk;
   int64_t b1 = b0 + a.chunk;
   if (b1 > a.Bpad) b1 = a.Bpad;
   const int steps = b1 > b0 ? (int)((b1 - b0) / 16) : 0;
@@ -547,7 +563,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA in flight when the LDS is released
   // C/D layout: lane holds column (l & 15) = V row j, rows 4g + r' = G rows
   const int i0 = ti * 128 + (w >> 1) * 64, j0 = tj * 128 + (w & 1) * 64;
-  float* out = a.part + zl * a.pls + (int64_t)blockIdx.y * a.n * a.m;
+  float* out = a.part + zl * a.pls + (int64_t)cy * a.n * a.m;
 #pragma unroll
   for (int x = 0; x < 4; ++x)
 #pragma unroll
@@ -702,7 +718,13 @@ hipError_t launch_bwd(int phase, int variant, const BwdArgs& a, dim3 grid, int s
 }
 
 hipError_t launch_wgrad(const WgradArgs& a, int tiles, hipStream_t s, int layers) {
-  hipLaunchKernelGGL(wgrad_kernel, dim3(tiles, a.nchunks, layers), dim3(256), 0, s, a);
+  // XCD-grouped tiles where the (chunk, layer) count is a multiple of 8 (DLADMM_WGRAD_XCD=0:
+  // consecutive ids, A/B)
+  const char* x = getenv("DLADMM_WGRAD_XCD");
+  const int groups = a.nchunks * layers;
+  const int xcd = groups % 8 == 0 && !(x && atoi(x) == 0) ? 1 : 0;
+  if (tiles != (a.NBp16 / 8) * (a.MBp16 / 8)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(wgrad_kernel, dim3(tiles * groups), dim3(256), 0, s, a, xcd);
   return hipGetLastError();
 }
 
