@@ -1380,7 +1380,9 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
     wa.G = AZ; wa.V = VAR; wa.ld = ldw; wa.n = n; wa.m = m;
     wa.NBp16 = (int)(p.Rn / 16); wa.MBp16 = (int)(p.Rm / 16);
     wa.Bpad = p.Bpad; wa.chunk = p.chunk; wa.nchunks = p.nchunks; wa.part = wpart;
-    if (hipError_t e = launch_wgrad(wa, p.wtiles, s)) return (int)e;
+    // split-f16 GEMM after a split-f16 forward, as on the reverse sweep
+    if (hipError_t e = (use_wgrad_x3(p.x3w, wa) ? launch_wgrad_x3 : launch_wgrad)(wa, p.wtiles, s, 1))
+      return (int)e;
     float* gWk = tied ? d->gW : d->gW + (int64_t)k * n * d->ld_gw;
     if (hipError_t e = launch_wgrad_reduce(wpart, p.nchunks, n, m,
                                            has_s1 ? f.scalar_params : nullptr, k, tied ? 1 : 0,

@@ -405,8 +405,8 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
 }  // namespace
 
 hipError_t launch_wgrad_x3(const WgradArgs& a, int tiles, hipStream_t s, int layers) {
-  (void)tiles;  // the tile count follows the V-tile width chosen here
-  if (!wgrad_x3_fits(a)) return hipErrorInvalidValue;
+  // tiles: the caller's 128 x 128 count (the launch re-tiles at the V-tile width chosen here)
+  if (!wgrad_x3_fits(a) || tiles != (a.NBp16 / 8) * (a.MBp16 / 8)) return hipErrorInvalidValue;
   // 256-row V tiles where the padded V rows allow (DLADMM_WGRAD_X3_TJ=128 forces the narrow
   // form: A/B)
   const char* e = getenv("DLADMM_WGRAD_X3_TJ");

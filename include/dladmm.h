@@ -196,10 +196,10 @@ int dladmm_fwd_f32(const dladmm_fwd_desc* d, void* stream);
  */
 typedef struct dladmm_bwd_desc {
   /* the forward's descriptor (keep_all, T, and P where it was saved).  fwd.precision:
-     DLADMM_PREC_F32, or DLADMM_PREC_F32_SPLIT after a split-f16 training forward -- then, on the
-     reverse-sweep path (dladmm_bwd_path() == 1) with whole 32-column chunks, the weight-gradient
-     GEMM (gU_k Var_k^T over the batch) also runs on the f16 matrix cores with exactly split
-     operands (fp32 GEMM accuracy); every other backward kernel is fp32 either way */
+     DLADMM_PREC_F32, or DLADMM_PREC_F32_SPLIT after a split-f16 training forward -- then, with
+     whole 32-column chunks, the weight-gradient GEMM (gU_k Var_k^T over the batch) also runs on
+     the f16 matrix cores with exactly split operands (fp32 GEMM accuracy), on the reverse sweep
+     and on the per-layer backward alike; every other backward kernel is fp32 either way */
   dladmm_fwd_desc fwd;
 
   /* upstream cotangents: HOST arrays of device pointers, one per layer (gT: K+1), each a

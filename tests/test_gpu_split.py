@@ -318,3 +318,35 @@ def test_split_weight_gradient_full_batch(tj, run, ramp, dl, monkeypatch):
         a = grads["1"][k].double()
         assert torch.isfinite(a).all(), k
         assert float((a - b.double()).norm() / b.double().norm()) <= 1e-5, k
+
+
+def test_split_weight_gradient_per_layer_backward(dl, monkeypatch):
+    """The per-layer backward (DLADMM_BWD_REV=0: the fallback when the reverse sweep's workspace
+    does not fit) also runs the weight-gradient GEMM split-f16 after a split-f16 forward: fc*
+    gradients within 1e-5 of the fp32-MFMA kernel's and not bitwise equal to them; every other
+    gradient bitwise equal."""
+    from test_gpu_backward import make_train_net
+    m, n, B, K = 256, 512, 4096, 3
+    inp = P.make_inputs(m, n, B, 7719)
+    sd = P.make_state_dict("v4", m, n, B, K, inp["A"], 7719, perturb=0.1)
+    X = torch.from_numpy(inp["X"]).cuda()
+    monkeypatch.setenv("DLADMM_BWD_REV", "0")
+    grads = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DLADMM_WGRAD_X3", mode)
+        net = make_train_net(dl, "v4", inp, sd, K)
+        net.precision = "f32_split"
+        tot, _ = net.training_loss(X, 1e-3, [0.6, 0.6, 1.0], "l1l1")
+        tot.backward()
+        torch.cuda.synchronize()
+        grads[mode] = {k: p.grad.detach().clone() for k, p in net.named_parameters()
+                       if p.grad is not None}
+    wkeys = [k for k in grads["0"] if k.startswith("fc")]
+    assert wkeys
+    assert any(not torch.equal(grads["1"][k], grads["0"][k]) for k in wkeys)
+    for k in grads["0"]:
+        a, b = grads["1"][k].double(), grads["0"][k].double()
+        if k in wkeys:
+            assert float((a - b).norm() / b.norm()) <= 1e-5, k
+        else:
+            assert torch.equal(grads["1"][k], grads["0"][k]), k
