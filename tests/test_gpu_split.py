@@ -350,3 +350,37 @@ def test_split_weight_gradient_per_layer_backward(dl, monkeypatch):
             assert float((a - b).norm() / b.norm()) <= 1e-5, k
         else:
             assert torch.equal(grads["1"][k], grads["0"][k]), k
+
+
+@pytest.mark.parametrize("prec,var,val", [
+    ("f32_split", "DLADMM_WGRAD_X3_TJ", "128"),
+    ("f32_split", "DLADMM_WGRAD_X3_XCD", "0"),
+    ("f32_split", "DLADMM_WGRAD_X3_BUFS", "2"),
+    ("f32_split", "DLADMM_WGRAD_X3_SPEC", "1"),
+    ("f32", "DLADMM_WGRAD_XCD", "0"),
+])
+def test_weight_gradient_schedules_bit_identical(prec, var, val, dl, monkeypatch):
+    """The weight-gradient schedule switches change only where and when the work runs, not its
+    arithmetic: V-tile width (each wave keeps its 64 G x 64 V rows and their scales), workgroup
+    order over the XCDs, buffer count, the speculative split -- every gradient bitwise equal to
+    the default schedule's.  B = 65,536 with the magnitude ramp, so the running scales move."""
+    from test_gpu_backward import make_train_net
+    m, n, B, K = 256, 512, 65536, 2
+    inp = P.make_inputs(m, n, B, 7723)
+    sd = P.make_state_dict("v4", m, n, B, K, inp["A"], 7723, perturb=0.1)
+    X = torch.from_numpy(inp["X"]).cuda()
+    X = X * torch.exp2(12.0 * (torch.arange(B, device=X.device) % 1024) / 1024 - 6.0)
+    grads = {}
+    for mode in ("default", "switched"):
+        if mode == "switched":
+            monkeypatch.setenv(var, val)
+        net = make_train_net(dl, "v4", inp, sd, K)
+        net.precision = prec
+        tot, _ = net.training_loss(X, 1e-3, [0.6, 1.0], "l1l1")
+        tot.backward()
+        torch.cuda.synchronize()
+        grads[mode] = {k: p.grad.detach().clone() for k, p in net.named_parameters()
+                       if p.grad is not None}
+        del net, tot
+    for k in grads["default"]:
+        assert torch.equal(grads["default"][k], grads["switched"][k]), k
