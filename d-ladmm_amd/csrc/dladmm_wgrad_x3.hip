@@ -28,7 +28,8 @@
 // fragment read is one conflict-free ds_read_b128); per 32-column sub-chunk 16 G and TJ / 8 V
 // pieces, three buffers at TJ = 256 (144 KiB: two sub-chunks in flight), two at 128.  Measured
 // (profiles/r05_wgrad_x3.json, r05_wgrad_tj.json, r05_wgrad_x3_steps.json): 561 us per 8-layer
-// launch at the headline shape against 662 for the round's first form and 990 for wgrad_kernel.
+// launch at the headline shape against 662 for the round's first form and 990 for wgrad_kernel;
+// the LDS-DMA issued after the MFMAs rather than beside the fragment reads: ~545 us.
 #include "dladmm_common.h"
 #include "dladmm_internal.h"
 #include "dladmm_wgrad_x3.h"
@@ -111,7 +112,11 @@ struct WgX3 {
 // split each sub-chunk speculatively at the running scales in the same straight-line block as the
 // previous sub-chunk's MFMAs (two operand register sets), re-splitting in the rare case a
 // magnitude reached them.
-template <int TJ, bool RUN, int NBUF, bool SPEC = false>
+// DPOS: where the LDS-DMA of sub-chunk s + NBUF - 1 is issued in iteration s (non-SPEC loop):
+// 0 right after the fragment reads, 1 after the MFMAs of s - 1, 2 one piece per operand split
+// (an LDS-DMA instruction costs its wave ~60 cycles among MFMAs / VALU but 100-185 beside
+// ds_reads, MI355X_MICROARCH.md)
+template <int TJ, bool RUN, int NBUF, bool SPEC = false, int DPOS = 0>
 __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_kernel(
     const WgradArgs a, int xcd) {
   using T = WgX3<TJ>;
@@ -152,9 +157,8 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
   const float* gb = a.G + zl * a.gls + (int64_t)(ti * 128) * a.ld;
   const float* vb = a.V + zl * a.vls + (int64_t)(tj * TJ) * a.ld;
   const uint32_t vl = (uint32_t)(((int64_t)r * a.ld + 8 * g) * 4);
-  auto issue = [&](int sub, int buf) {
-#pragma unroll
-    for (int q = 0; q < T::PPW; ++q) {
+  auto issue_piece = [&](int sub, int buf, int q) {
+    {
       const int p = T::PPW * w + q;
       const bool isg = p < T::GP;
       const int pp = isg ? p : p - T::GP;
@@ -169,6 +173,10 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
       asm volatile("" : "+s"(sb));
       glds16((const float*)sb, vl, img + (buf * T::PIECES + p) * 64);
     }
+  };
+  auto issue = [&](int sub, int buf) {
+#pragma unroll
+    for (int q = 0; q < T::PPW; ++q) issue_piece(sub, buf, q);
   };
 
   f32x4 acc[4][4];
@@ -328,8 +336,11 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
           fb[x][hf] = im[(T::GP + (4 * wc + x) * 2 + hf) * 64 + lane];
         }
       // sub-chunk s - 1's buffer is free: it receives sub-chunk s + kBufs - 1
-      if (s + kBufs - 1 < nsub) issue(s + kBufs - 1, (s + kBufs - 1) % kBufs);
+      const bool more = s + kBufs - 1 < nsub;
+      const int nx = s + kBufs - 1, nbuf = (s + kBufs - 1) % kBufs;
+      if (DPOS == 0 && more) issue(nx, nbuf);
       if (s > 0) mfmas();  // sub-chunk s - 1, while the reads above land
+      if (DPOS == 1 && more) issue(nx, nbuf);
       float ma = 0.f, mb = 0.f;
 #pragma unroll
       for (int x = 0; x < 4; ++x)
@@ -368,11 +379,18 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
         sbs = ldexpf(1.0f, eb);
         uns = ldexpf(1.0f, -(ea + eb));
       }
+      auto split_all = [&](auto D_) {
+        constexpr bool D = decltype(D_)::value;
 #pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        split8(fa[x][0], fa[x][1], sa, ah[x], al[x]);
-        split8(fb[x][0], fb[x][1], sbs, bh[x], bl[x]);
-      }
+        for (int x = 0; x < 4; ++x) {
+          split8(fa[x][0], fa[x][1], sa, ah[x], al[x]);
+          if constexpr (D) if (2 * x < T::PPW) issue_piece(nx, nbuf, 2 * x);
+          split8(fb[x][0], fb[x][1], sbs, bh[x], bl[x]);
+          if constexpr (D) if (2 * x + 1 < T::PPW) issue_piece(nx, nbuf, 2 * x + 1);
+        }
+      };
+      if (DPOS == 2 && more) split_all(std::true_type{});
+      else split_all(std::false_type{});
     }
     if (nsub > 0) mfmas();
   }
@@ -430,8 +448,16 @@ hipError_t launch_wgrad_x3(const WgradArgs& a, int tiles, hipStream_t s, int lay
   // (609-613 vs 561 us, profiles/r05_wgrad_x3_steps.json)
   const char* sp = getenv("DLADMM_WGRAD_X3_SPEC");
   const bool spec = b3 && sp && atoi(sp) == 1;
+  // LDS-DMA issue position: after the MFMAs (539-556 vs 558-582 us right after the fragment
+  // reads, 574-585 spread over the split; DLADMM_WGRAD_X3_DPOS=0 / 2, A/B)
+  const char* dp = getenv("DLADMM_WGRAD_X3_DPOS");
+  const int dpos = dp ? atoi(dp) : 1;
   if (spec) hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 3, true>), grid, bw, 0, s, a, xcd);
-  else if (b3) hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 3>), grid, bw, 0, s, a, xcd);
+  else if (b3 && dpos == 0)
+    hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 3, false, 0>), grid, bw, 0, s, a, xcd);
+  else if (b3 && dpos == 2)
+    hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 3, false, 2>), grid, bw, 0, s, a, xcd);
+  else if (b3) hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 3, false, 1>), grid, bw, 0, s, a, xcd);
   else if (wide && run) hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 2>), grid, bw, 0, s, a, xcd);
   else if (wide) hipLaunchKernelGGL((wgrad_x3_kernel<256, false, 2>), grid, bw, 0, s, a, xcd);
   else if (run) hipLaunchKernelGGL((wgrad_x3_kernel<128, true, 2>), grid, bn, 0, s, a, xcd);

@@ -357,12 +357,15 @@ def test_split_weight_gradient_per_layer_backward(dl, monkeypatch):
     ("f32_split", "DLADMM_WGRAD_X3_XCD", "0"),
     ("f32_split", "DLADMM_WGRAD_X3_BUFS", "2"),
     ("f32_split", "DLADMM_WGRAD_X3_SPEC", "1"),
+    ("f32_split", "DLADMM_WGRAD_X3_DPOS", "0"),
+    ("f32_split", "DLADMM_WGRAD_X3_DPOS", "2"),
     ("f32", "DLADMM_WGRAD_XCD", "0"),
 ])
 def test_weight_gradient_schedules_bit_identical(prec, var, val, dl, monkeypatch):
     """The weight-gradient schedule switches change only where and when the work runs, not its
     arithmetic: V-tile width (each wave keeps its 64 G x 64 V rows and their scales), workgroup
-    order over the XCDs, buffer count, the speculative split -- every gradient bitwise equal to
+    order over the XCDs, buffer count, the speculative split, where the LDS-DMA is issued --
+    every gradient bitwise equal to
     the default schedule's.  B = 65,536 with the magnitude ramp, so the running scales move."""
     from test_gpu_backward import make_train_net
     m, n, B, K = 256, 512, 65536, 2
