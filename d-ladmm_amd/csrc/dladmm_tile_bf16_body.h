@@ -9,6 +9,12 @@
 #include "dladmm_internal.h"
 #include "dladmm_layer_epi.h"
 
+#ifndef DLADMM_TILE_DPOS
+#define DLADMM_TILE_DPOS 2  // where a stage's LDS-DMA pieces issue (A/B, same results): 0 half
+                            // beside the second half's fragment reads, half between the MFMA
+                            // halves; 1 all between the halves; 2 one after each group of 4 MFMAs
+                            // (2: 7.04-7.08 vs 7.09-7.11 ms per config-5 forward, r05_tile_dpos.json)
+#endif
 #ifndef DLADMM_TILE_EXP
 #define DLADMM_TILE_EXP 0  // experiment bits (WRONG results): 1 no in-loop DMA, 2 no MFMA,
                            // 4 no epilogue
@@ -91,7 +97,7 @@ __device__ __forceinline__ void tile_body(const LayerArgs& a, f32x4* ring, int b
     for (int j = 0; j < kWaveCB; ++j) bfr[j] = st[(kTileBlocks + kWaveCB * wc + j) * 64 + lane];
 #pragma unroll
     for (int i = 0; i < 4; ++i) a0[i] = st[(kWaveRB * wr + i) * 64 + lane];
-    if (!(DLADMM_TILE_EXP & 1)) {
+    if (!(DLADMM_TILE_EXP & 1) && DLADMM_TILE_DPOS == 0) {
 #pragma unroll
       for (int q = 0; q < G::H1; ++q) issue(nkb, nslot, q);
     }
@@ -100,19 +106,36 @@ __device__ __forceinline__ void tile_body(const LayerArgs& a, f32x4* ring, int b
     if (DLADMM_TILE_EXP & 2) continue;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
 #pragma unroll
       for (int j = 0; j < kWaveCB; ++j) acc[i][j] = mfma_bf16(a0[i], bfr[j], acc[i][j]);
+      if constexpr (!(DLADMM_TILE_EXP & 1) && DLADMM_TILE_DPOS == 2) {
+        // pieces q = i, i + 4, ... after MFMA group i (FPW <= 8 pieces over 8 groups)
+        if (i < FPW) {
+          __builtin_amdgcn_sched_barrier(0);
+          issue(nkb, nslot, i);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
     __builtin_amdgcn_s_setprio(0);
-    if (!(DLADMM_TILE_EXP & 1)) {
+    if (!(DLADMM_TILE_EXP & 1) && DLADMM_TILE_DPOS < 2) {
 #pragma unroll
-      for (int q = G::H1; q < FPW; ++q) issue(nkb, nslot, q);
+      for (int q = DLADMM_TILE_DPOS == 0 ? G::H1 : 0; q < FPW; ++q) issue(nkb, nslot, q);
     }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
 #pragma unroll
       for (int j = 0; j < kWaveCB; ++j) acc[4 + i][j] = mfma_bf16(a1[i], bfr[j], acc[4 + i][j]);
+      if constexpr (!(DLADMM_TILE_EXP & 1) && DLADMM_TILE_DPOS == 2) {
+        if (4 + i < FPW) {
+          __builtin_amdgcn_sched_barrier(0);
+          issue(nkb, nslot, 4 + i);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
     __builtin_amdgcn_s_setprio(0);
     slot = slot + 1 == NST ? 0 : slot + 1;
     nslot = nslot + 1 == NST ? 0 : nslot + 1;
