@@ -491,6 +491,9 @@ constexpr int kWgStages = 4;
 // xcd set the tiles of one (chunk, layer) run on one XCD back to back, so its L2 serves the G and
 // V row blocks they share (each V block is read by every G tile, each G block by every V tile)
 // once from HBM.  Without it, consecutive ids spread a chunk's tiles over the XCDs.
+// DPOS: where iteration s issues the LDS-DMA of step s + 3: 0 right after the barrier (beside
+// the fragment reads), 1 after the first quarter of the MFMAs, 2 one piece after each quarter
+template <int DPOS>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a, int xcd) {
   __shared__ f32x4 ring[kWgStages * 16 * 64];
   const int lane = threadIdx.x & 63;
@@ -529,12 +532,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a, int xc
   src += b0;
   const uint32_t vl = (uint32_t)(((int64_t)r * a.ld + 4 * g) * 4);
   const uint32_t rs16 = (uint32_t)(16 * a.ld * 4);
-  auto issue = [&](int s, int stage) {
+  auto issue_f = [&](int s, int stage, int f) {
     uint64_t sb = (uint64_t)(src + 16 * (int64_t)s);
     asm volatile("" : "+s"(sb));
+    glds16((const float*)sb, vl + f * rs16, ring + (stage * 16 + 4 * w + f) * 64);
+  };
+  auto issue = [&](int s, int stage) {
 #pragma unroll
-    for (int f = 0; f < 4; ++f)
-      glds16((const float*)sb, vl + f * rs16, ring + (stage * 16 + 4 * w + f) * 64);
+    for (int f = 0; f < 4; ++f) issue_f(s, stage, f);
   };
 #pragma unroll
   for (int s = 0; s < kWgStages - 1; ++s)
@@ -545,7 +550,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a, int xc
     // every wave is done reading stage s - 1, which the issue below overwrites
     if (s + kWgStages - 2 < steps) ring_barrier_n<4 * (kWgStages - 2)>();
     else ring_barrier_n<0>();
-    if (s + kWgStages - 1 < steps) issue(s + kWgStages - 1, (s + kWgStages - 1) % kWgStages);
+    const bool more = s + kWgStages - 1 < steps;
+    const int ns = s + kWgStages - 1, nst = (s + kWgStages - 1) % kWgStages;
+    if (DPOS == 0 && more) issue(ns, nst);
     const f32x4* st = ring + (s % kWgStages) * 16 * 64;
     f32x4 ga[4], va[4];
 #pragma unroll
@@ -553,12 +560,25 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a, int xc
       ga[x] = st[(gf + x) * 64 + lane];
       va[x] = st[(vf + x) * 64 + lane];
     }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
+    auto quarter = [&](int q) {
 #pragma unroll
       for (int x = 0; x < 4; ++x)
 #pragma unroll
         for (int y = 0; y < 4; ++y) acc[x][y] = mfma4(ga[x][q], va[y][q], acc[x][y]);
+    };
+    if (DPOS == 0 || !more) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) quarter(q);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        quarter(q);
+        __builtin_amdgcn_sched_barrier(0);
+        if (DPOS == 1 && q == 0) issue(ns, nst);
+        if (DPOS == 2) issue_f(ns, nst, q);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA in flight when the LDS is released
   // C/D layout: lane holds column (l & 15) = V row j, rows 4g + r' = G rows
@@ -724,7 +744,12 @@ hipError_t launch_wgrad(const WgradArgs& a, int tiles, hipStream_t s, int layers
   const int groups = a.nchunks * layers;
   const int xcd = groups % 8 == 0 && !(x && atoi(x) == 0) ? 1 : 0;
   if (tiles != (a.NBp16 / 8) * (a.MBp16 / 8)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(wgrad_kernel, dim3(tiles * groups), dim3(256), 0, s, a, xcd);
+  // LDS-DMA issue position (DLADMM_WGRAD_DPOS, A/B)
+  const char* dp = getenv("DLADMM_WGRAD_DPOS");
+  const int dpos = dp ? atoi(dp) : 0;
+  if (dpos == 1) hipLaunchKernelGGL(wgrad_kernel<1>, dim3(tiles * groups), dim3(256), 0, s, a, xcd);
+  else if (dpos == 2) hipLaunchKernelGGL(wgrad_kernel<2>, dim3(tiles * groups), dim3(256), 0, s, a, xcd);
+  else hipLaunchKernelGGL(wgrad_kernel<0>, dim3(tiles * groups), dim3(256), 0, s, a, xcd);
   return hipGetLastError();
 }
 
