@@ -93,6 +93,10 @@ __device__ __forceinline__ void split8(const f32x4& p0, const f32x4& p1, float s
   lo = __builtin_bit_cast(h8, u32x4{L[0], L[1], L[2], L[3]});
 }
 
+#ifndef WX3_PRIO
+#define WX3_PRIO 0  // A/B build: raised wave priority around the MFMA phase (s_setprio)
+#endif
+
 constexpr int kSub = 32;   // batch columns per sub-chunk (one k-step of 32)
 
 // Tile geometry by V-tile width TJ: 128 G rows x TJ V rows, waves of 64 x 64 (2 wave rows x
@@ -339,7 +343,9 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
       const bool more = s + kBufs - 1 < nsub;
       const int nx = s + kBufs - 1, nbuf = (s + kBufs - 1) % kBufs;
       if (DPOS == 0 && more) issue(nx, nbuf);
+      if (WX3_PRIO) __builtin_amdgcn_s_setprio(1);
       if (s > 0) mfmas();  // sub-chunk s - 1, while the reads above land
+      if (WX3_PRIO) __builtin_amdgcn_s_setprio(0);
       if (DPOS == 1 && more) issue(nx, nbuf);
       float ma = 0.f, mb = 0.f;
 #pragma unroll
