@@ -61,6 +61,10 @@
 #ifndef X3_BAR2
 #define X3_BAR2 0  // one ring barrier per two chunks (each refills two slots)
 #endif
+#ifndef X3_DMA_LATE
+#define X3_DMA_LATE 0  // A/B build: a barrier step's DMA group issued after its MFMAs (the ring
+                       // windows then count one step less)
+#endif
 #ifndef X3_SDLY
 #define X3_SDLY 2  // deferred tile stores: steps between the read-back and the store
 #endif
@@ -260,7 +264,7 @@ struct Win {
   static constexpr int win() {
     const int ch = T / SPC;
     int n = group(ch + 2, G1) + group(ch + 3, G1);
-    for (int u = T - 3 * SPC; u < T; ++u) {
+    for (int u = T - 3 * SPC + (X3_DMA_LATE ? 1 : 0); u < T; ++u) {
       if (u >= 0) n += G1 ? ops1(u) : ops2(u);
       else if (ST + u >= 0) n += G1 ? ops2(ST + u) : ops1(ST + u);
     }
@@ -658,7 +662,7 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
           // slots of chunks ch-1 and ch are free: chunks ch+3, ch+4
           issue(G1_, std::integral_constant<int, ch + 3>{}, gi, slot_add(cur, kSlots - 1));
           issue(G1_, std::integral_constant<int, ch + 4>{}, gi, cur);
-        } else {
+        } else if constexpr (!X3_DMA_LATE) {
           issue(G1_, std::integral_constant<int, ch + kSlots>{}, gi, cur);
         }
       }
@@ -667,8 +671,13 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
       frl[tn % R] = frag(nx, 2 * (c + D - SPC) + 1);
     }
   };
-  auto step_tail = [&](auto T_) {
+  auto step_tail = [&](auto T_, auto G1_, int gi) {
     constexpr int t = decltype(T_)::value;
+    if constexpr (X3_DMA_LATE && !X3_BAR2 && t % SPC + D == SPC) {
+      // the barrier step's DMA group, after its MFMAs (the barrier in its head freed slot cur)
+      __builtin_amdgcn_sched_barrier(0);
+      issue(G1_, std::integral_constant<int, t / SPC + kSlots>{}, gi, cur);
+    }
 #if X3_SGB
     // MFMA, X3_SGB fillers, MFMA, X3_SGB fillers, MFMA, rest (filler classes: X3_SGM)
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -770,7 +779,7 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
           if constexpr (ZC::g1_block(t / SPC + 1, 0) >= 0) zread(zreg(slot_add(cur, 1), 0), zo[0]);
         }
         acc = mfma3(t % R, Vpk[s], acc);
-        step_tail(std::integral_constant<int, t>{});
+        step_tail(std::integral_constant<int, t>{}, std::true_type{}, gi);
       });
       qp = acc;
     });
@@ -833,7 +842,7 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
           }
         }
         acc = mfma3(t % R, Zpk[s], acc);
-        step_tail(std::integral_constant<int, t>{});
+        step_tail(std::integral_constant<int, t>{}, std::false_type{}, gi);
       });
       qp = acc;
     });
