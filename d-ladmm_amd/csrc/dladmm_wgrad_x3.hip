@@ -455,7 +455,8 @@ hipError_t launch_wgrad_x3(const WgradArgs& a, int tiles, hipStream_t s, int lay
   const char* sp = getenv("DLADMM_WGRAD_X3_SPEC");
   const bool spec = b3 && sp && atoi(sp) == 1;
   // LDS-DMA issue position: after the MFMAs (539-556 vs 558-582 us right after the fragment
-  // reads, 574-585 spread over the split; DLADMM_WGRAD_X3_DPOS=0 / 2, A/B)
+  // reads, 574-585 spread over the split; DLADMM_WGRAD_X3_DPOS=0 / 2, A/B).  The 128-row form
+  // (two workgroups per CU, two buffers) keeps the early issue: 418-421 vs 409 us at m = 64.
   const char* dp = getenv("DLADMM_WGRAD_X3_DPOS");
   const int dpos = dp ? atoi(dp) : 1;
   if (spec) hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 3, true>), grid, bw, 0, s, a, xcd);
