@@ -57,9 +57,10 @@ def parse():
     ap.add_argument("--m", type=int, default=256)
     ap.add_argument("--n", type=int, default=512)
     ap.add_argument("--layers", type=int, default=15)
-    ap.add_argument("--variant", default="v4", choices=["v4", "v6"],
+    ap.add_argument("--variant", default="v4", choices=["v4", "v6", "v1"],
                     help="v4 = main_syn_l1l1_scalar.py (configs 1-3); v6 = main_syn_lasso_scalar.py "
-                         "(config 4: --m 512 --n 2048 --layers 40)")
+                         "(config 4: --m 512 --n 2048 --layers 40); v1 = main_lena.py's "
+                         "DLADMMNet (per-sample betas, forward only)")
     ap.add_argument("--alpha", type=float, default=0.001)
     ap.add_argument("--lean", action="store_true", help="write only the last layer (not default)")
     ap.add_argument("--precision", default="f32", choices=["f32", "f32_split", "bf16"],
@@ -221,7 +222,7 @@ class Workload:
         gen_B = B_global if cols is not None else B_rank
         A, X, Z0, E0, L0 = synth(m, n, gen_B, seed, dev, cols)
         self.X = X
-        cls = {"v4": dl.DLADMMNetScalar, "v6": dl.DLADMMNetLasso}[a.variant]
+        cls = {"v4": dl.DLADMMNetScalar, "v6": dl.DLADMMNetLasso, "v1": dl.DLADMMNet}[a.variant]
         torch.manual_seed(1126)   # params seeded -> reproducible objective
         self.net = cls(m=m, n=0, d=n, batch_size=B_rank, A=A, Z0=Z0, E0=E0, L0=L0, layers=K)
         self.net.requires_grad_(False)
@@ -229,13 +230,16 @@ class Workload:
             with torch.no_grad():
                 for fc in self.net.fc:
                     fc.weight.mul_(wscale / 0.4)
-        self.lk = dl._lib.LOSS_L1L1 if a.variant == "v4" else dl._lib.LOSS_LASSO
+        # V4: the training loop's fused L1L1 objective; V6: LASSO; V1: the bare forward
+        # (main_lena.py's objective is a separate pass, dladmm_lena_f32)
+        self.lk = {"v4": dl._lib.LOSS_L1L1, "v6": dl._lib.LOSS_LASSO, "v1": 0}[a.variant]
         self.ddist = importlib.import_module("d-ladmm_amd.dist")
 
     def step(self, keep_all, evpair=None):
         r = self.net.run(self.X, keep_all=keep_all, loss_kind=self.lk, kernel_events=evpair)
         # one RCCL all-reduce of the [K, 2] objective sums over xGMI (no-op at N = 1)
-        obj = self.ddist.global_objectives(r.loss_sums, self.a.alpha, self.B_global)
+        obj = (self.ddist.global_objectives(r.loss_sums, self.a.alpha, self.B_global)
+               if r.loss_sums is not None else torch.zeros(1, dtype=torch.float64))
         self.path = r.path  # the kernel path the library chose (dladmm_fwd_path)
         return r, obj
 
@@ -309,8 +313,7 @@ def main():
     # the same workload with the fp32 GEMMs on the f16 matrix cores (split-f16, same fp32
     # tolerance tests; tests/test_gpu_split.py), timed the same way beside the headline
     split = None
-    if a.precision == "f32" and m <= 256 and n <= 512 and B % 4 == 0 and \
-            os.environ.get("DLADMM_PATH", "")[:1] != "l" and not a.no_split:
+    if a.precision == "f32" and m <= 256 and n <= 512 and B % 4 == 0 and not a.no_split:
         s_el, s_kern, _, s_obj = timed(w, "f32_split")
         assert w.path == 4, f"split leg ran on path {w.path}, not the split-f16 kernel"
         # untimed: per-layer norm-relative distance of the split path's Z/E/L/T from the fp32
@@ -379,6 +382,20 @@ def main():
                                shape=(m_, n_, K_, B_), var=var, prec=prec, wscale=wsc)
             del w_
             torch.cuda.empty_cache()
+    # the north_star's primary variant V1 (main_lena.py:16-102, DLADMMNet: per-sample (m, B)
+    # betas read by every layer) at the headline shape, forward with every layer's Z/E/L written
+    v1 = None
+    if world == 1 and not strong and not a.no_cfg3 and a.variant == "v4" and \
+            a.precision == "f32" and (m, n, K) == (256, 512, 15):
+        import copy
+        a1 = copy.copy(a)
+        a1.variant = "v1"
+        w1 = Workload(dl, a1, m, n, K, B, B, None, rank, dev, rank)
+        c_el, c_kern, _, _ = timed(w1, "f32")
+        v1 = dict(value=B * a.steps / c_el, ms_per_step=c_el / a.steps * 1e3, kern=c_kern,
+                  path=w1.path, B=B)
+        del w1
+        torch.cuda.empty_cache()
     torch.cuda.synchronize()
     # SURVEY row f1 at N = 1: the headline shape's training step (tools/bench_train.py: forward +
     # fused per-layer L1L1 objective + reverse-sweep backward + Adam), timed after everything above
@@ -389,15 +406,24 @@ def main():
         import bench_train
         ta = bench_train.parser().parse_args(["--variant", "v4", "--fused-loss", "--batch", str(B),
                                               "--steps", "10", "--warmup", "3"])
-        train = bench_train.run(ta)
+        # a failure here (e.g. out of memory after the legs above) is recorded, never allowed
+        # to cost the headline line
+        try:
+            train = bench_train.run(ta)
+        except Exception as e:  # noqa: BLE001
+            train = {"error": f"{type(e).__name__}: {e}"}
         torch.cuda.empty_cache()
-        if not a.no_split:  # the same step on the split-f16 kernels (forward + weight gradient)
+        if not a.no_split and "error" not in train:
+            # the same step on the split-f16 kernels (forward + weight gradient)
             ts = bench_train.parser().parse_args(["--variant", "v4", "--fused-loss", "--batch",
                                                   str(B), "--steps", "10", "--warmup", "3",
                                                   "--precision", "f32_split"])
-            train["split_f16"] = {k: v for k, v in bench_train.run(ts).items()
-                                  if k in ("step_ms", "samples_per_s", "forward_ms",
-                                           "backward_ms")}
+            try:
+                train["split_f16"] = {k: v for k, v in bench_train.run(ts).items()
+                                      if k in ("step_ms", "samples_per_s", "forward_ms",
+                                               "backward_ms")}
+            except Exception as e:  # noqa: BLE001
+                train["split_f16"] = {"error": f"{type(e).__name__}: {e}"}
             torch.cuda.empty_cache()
 
     if rank == 0:
@@ -415,11 +441,7 @@ def main():
         value = total / elapsed
         flop = (4 * K + 2) * m * n * B                      # per launch (rank 0's shard)
         achieved = flop / kern_avg  # noqa
-        # algorithmic HBM bytes per sample (SURVEY 8d, V4 API-parity): inputs X,Z0,E0,L0 +
-        # outputs Z,E,L (K layers) + T (K+1); weights (K+1)*m*n*4 per launch
-        bytes_io = 4 * ((m + n + 2 * m) + K * (n + 2 * m) + (K + 1) * m) if keep_all else \
-            4 * ((m + n + 2 * m) + (n + 3 * m))
-        bytes_launch = bytes_io * B + (K + 1) * m * n * 4
+        bytes_launch = alg_bytes(a.variant, m, n, K, B, keep_all)
         traffic = None
         if os.path.exists(a.traffic_json):
             try:
@@ -540,6 +562,25 @@ def main():
                 "roofline_peak": "bf16 dense MFMA" if c["prec"] == "bf16" else "fp32 MFMA",
                 "objective_last_layer": c["obj"],
             }
+        if v1 is not None:
+            f1 = (4 * K + 2) * m * n * v1["B"]
+            b1 = alg_bytes("v1", m, n, K, v1["B"], True)
+            res["v1"] = {
+                "workload": f"DLADMMNet (V1, main_lena.py:16-102) forward m={m} n={n} K={K}, "
+                            f"B={v1['B']}/GPU, per-sample (m, B) beta1/beta2 per layer, every "
+                            "layer's Z/E/L written (the reference's return lists); "
+                            "reference-init parameters (betas 1, W = A^T + 1e-3 N)",
+                "value": v1["value"], "unit": "samples/s", "ms_per_step": v1["ms_per_step"],
+                "path": {1: "fused", 2: "per-layer"}.get(v1["path"], v1["path"]),
+                "kernel": "dladmm::fused_kernel (one launch)",
+                "kernel_ms": v1["kern"] * 1e3,
+                "roofline_frac": f1 / v1["kern"] / PEAK_F32_MFMA,
+                "roofline_peak": "fp32 MFMA 157.3 TF/s",
+                "flop_per_launch": f1,
+                "algorithmic_bytes_per_launch": b1,
+                "bytes_per_sample": b1 / v1["B"],
+                "hbm_frac_algorithmic": b1 / v1["kern"] / PEAK_HBM,
+            }
         if cfg3 is not None:
             f3 = (4 * K + 2) * m * n * cfg3["B"]
             res["cfg3_strong"] = {
@@ -563,7 +604,7 @@ def main():
         if train is not None:
             res["train"] = {k: train[k] for k in (
                 "metric", "batch", "step_ms", "samples_per_s", "forward_ms", "backward_ms",
-                "backward_tflops", "backward_frac_fp32_mfma", "loss_path", "split_f16")
+                "backward_tflops", "backward_frac_fp32_mfma", "loss_path", "split_f16", "error")
                 if k in train}
             res["train"]["note"] = ("V4 m=256 n=512 K=15 training step (zero_grad, forward with "
                                     "saved A Z_k, fused L1L1 objective with decay, reverse-sweep "
@@ -578,7 +619,22 @@ def main():
 
 
 def w_net_name(dl, a):
-    return {"v4": dl.DLADMMNetScalar, "v6": dl.DLADMMNetLasso}[a.variant].NAME
+    return {"v4": dl.DLADMMNetScalar, "v6": dl.DLADMMNetLasso, "v1": dl.DLADMMNet}[a.variant].NAME
+
+
+def alg_bytes(variant, m, n, K, B, keep_all):
+    """Algorithmic HBM bytes of one forward launch: inputs X, Z0, E0, L0; outputs
+    Z, E, L of every layer (keep_all) or of the last; T_0..T_K for the variants that return it
+    (V4-V6; V1-V3 write none); V1's per-sample beta1 / beta2 of every layer (2 K m per sample);
+    the weights (K + 1) m n once per launch.  V4 keep_all: 83,072 B/sample + 8 MiB; V1: 97,408
+    at B = 65,536."""
+    with_t = variant not in ("v1", "v2", "v3")
+    io = (m + n + 2 * m) + (K if keep_all else 1) * (n + 2 * m)
+    if with_t:
+        io += (K + 1) * m if keep_all else m
+    if variant == "v1":
+        io += 2 * K * m
+    return 4 * io * B + (K + 1) * m * n * 4
 
 
 # ------------------------------------------------------------------------------------------------
@@ -628,35 +684,51 @@ def world_check(gpus, environ=None):
     return None
 
 
-def visible_gpu_count(environ=None, kfd="/sys/class/kfd/kfd/topology/nodes"):
+def visible_gpu_count(environ=None, kfd="/sys/class/kfd/kfd/topology/nodes", dri="/dev/dri"):
     """GPUs this process could use, counted WITHOUT any HIP or torch.cuda call (the launcher
     parent must not initialise the runtime: torch.cuda.device_count() falls back to
-    hipGetDeviceCount when amdsmi is not importable).  The KFD topology lists one node per agent;
-    GPU nodes have a non-zero simd_count.  A *_VISIBLE_DEVICES list narrows the count the way
-    the runtime applies it (ROCR first, then HIP / CUDA on top).  None when the topology is
-    unreadable (no KFD driver: the ranks' own start-up then decides)."""
+    hipGetDeviceCount when amdsmi is not importable).  The KFD topology lists one node per agent
+    of the HOST (a container sees all of them); a GPU node has a non-zero simd_count and counts
+    only if this process can open its render node, /dev/dri/renderD<drm_render_minor> -- what
+    the ROCm runtime itself needs.  A *_VISIBLE_DEVICES list narrows the count the way the
+    runtime applies it (ROCR first, then HIP / CUDA on top); a list that starts with an invalid
+    id ("-1" hides every device) leaves none.  None when the topology is unreadable (no KFD
+    driver: the ranks' own start-up then decides)."""
     environ = os.environ if environ is None else environ
     try:
         nodes = sorted(int(d) for d in os.listdir(kfd) if d.isdigit())
     except OSError:
         return None
-    gpus = 0
+    gpus = opened = 0
     for nd in nodes:
         try:
             props = open(os.path.join(kfd, str(nd), "properties")).read().split("\n")
         except OSError:
             continue
-        for ln in props:
-            kv = ln.split()
-            if len(kv) == 2 and kv[0] == "simd_count" and kv[1].isdigit() and int(kv[1]) > 0:
-                gpus += 1
-                break
+        kv = dict(ln.split() for ln in props if len(ln.split()) == 2)
+        simd, minor = kv.get("simd_count", "0"), kv.get("drm_render_minor")
+        if not (simd.isdigit() and int(simd) > 0):
+            continue
+        gpus += 1
+        if minor is not None and os.access(os.path.join(dri, f"renderD{minor}"),
+                                           os.R_OK | os.W_OK):
+            opened += 1
+    # no render node readable at all (no /dev/dri in this mount namespace): the check cannot
+    # tell, so the topology's count stands rather than refusing every launch
+    if opened:
+        gpus = opened
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
         v = environ.get(var)
         if not v:   # unset or empty: no narrowing (the ranks' own start-up decides)
             continue
-        ids = [x for x in v.split(",") if x.strip() != ""]
-        gpus = min(gpus, len(ids))
+        ids = [x.strip() for x in v.split(",") if x.strip() != ""]
+        # the runtime stops at the first id it cannot parse ("-1" and the like): none before it
+        valid = 0
+        for x in ids:
+            if not (x.isdigit() or x.startswith("GPU-")):
+                break
+            valid += 1
+        gpus = min(gpus, valid)
     return gpus
 
 
@@ -668,8 +740,10 @@ def self_launch(argv, n) -> int:
     # the self-test ranks touch no device, so without it they skip the count
     topo = os.environ.get("DLADMM_KFD_TOPOLOGY")
     if backend == "nccl" and ("--launch-selftest" not in argv or topo):
-        # from the KFD topology: no HIP call in this process
-        have = visible_gpu_count(kfd=topo) if topo else visible_gpu_count()
+        # from the KFD topology: no HIP call in this process (the CPU tests' fake tree carries
+        # its render nodes in a dri/ directory beside the node directories)
+        have = visible_gpu_count(kfd=topo, dri=os.path.join(topo, "dri")) \
+            if topo else visible_gpu_count()
         if have is not None and have < n:
             print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
             return 2

@@ -10,7 +10,8 @@ from .model import (DLADMMNet, DLADMMNetFull, DLADMMNetLasso, DLADMMNetLTheta,  
                     DLADMMNetScalarZ0, VARIANTS, load_checkpoint)
 from .model import DLADMMNetNewS, DLADMMNetPTiedNewS, DLADMMNetTiedNewS  # noqa: F401
 from .lskm import DLADMMNetLSKM  # noqa: F401
-from .ops import BackwardResult, ForwardResult, dladmm_backward, dladmm_forward  # noqa: F401
+from .ops import (BackwardResult, ForwardResult, dladmm_backward, dladmm_forward,  # noqa: F401
+                  plan_flags)
 
 __all__ = ["DLADMMNet", "DLADMMNetLTheta", "DLADMMNetFull", "DLADMMNetScalar",
            "DLADMMNetScalarSl2", "DLADMMNetScalarZ0",

@@ -12,11 +12,14 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DLADMM_LIB") or os.path.join(HERE, "lib", "libdladmm_hip.so")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 PREC_F32, PREC_BF16, PREC_F32_SPLIT = 0, 1, 2
 MAX_LAYERS = 65536
 NSCALAR = 8
 
+# enum dladmm_flags (dladmm_fwd_desc.flags): plan options, never arithmetic
+F_PER_LAYER, F_BF16_WIDE, F_BWD_PER_LAYER, F_BWD_UNFUSED, F_BWD_NO_ZMASK, F_WGRAD_F32 = \
+    1, 2, 4, 8, 16, 32
 # enum dladmm_variant
 V1_LENA, V2_LTHETA, V3_FULL, V4_SCALAR, V5_TIED, V6_LASSO = 1, 2, 3, 4, 5, 6
 # enum dladmm_loss_kind
@@ -59,7 +62,7 @@ class FwdDesc(ctypes.Structure):
         ("workspace", _fp), ("workspace_bytes", ctypes.c_size_t),
         ("ev_kernel_start", _fp), ("ev_kernel_stop", _fp),
         ("col_loss", _fp),
-        ("precision", _i32), ("pad1", _i32),
+        ("precision", _i32), ("flags", _i32),
         ("P", _fp),
     ]
 

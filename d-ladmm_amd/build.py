@@ -19,8 +19,7 @@ CSRC = os.path.join(HERE, "csrc")
 UNITS = ("dladmm_capi.hip", "dladmm_fused.hip", "dladmm_fused_savep.hip", "dladmm_fused_x3.hip",
          "dladmm_fused_x3_savep.hip",
          "dladmm_layered.hip", "dladmm_backward.hip", "dladmm_lskm.hip", "dladmm_eval.hip",
-         "dladmm_tile_bf16.hip", "dladmm_tile_bf16_pair.hip", "dladmm_tile_bf16_pipe.hip",
-         "dladmm_tile_bf16_queue.hip", "dladmm_wgrad_x3.hip",
+         "dladmm_tile_bf16.hip", "dladmm_wgrad_x3.hip",
          "dladmm_reverse.hip",
          "dladmm_lena.hip",
          # reverse-sweep instantiations: one unit per E-step form and shape group (minutes each)
@@ -38,8 +37,7 @@ FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", f"--offload-arch={AR
 # MFMAs (packed v_pk_* f32 ops issue slower there; MI355X_MICROARCH.md, price of one filler
 # beside MFMAs)
 UNIT_FLAGS = {u: ["-fno-slp-vectorize"] for u in UNITS
-              if u.startswith("dladmm_fused_x3") or u.startswith("dladmm_reverse") or
-              u == "dladmm_tile_bf16_pipe.hip"}
+              if u.startswith("dladmm_fused_x3") or u.startswith("dladmm_reverse")}
 # the split-f16 weight gradient unscales every MFMA result with VALU: MFMA results in VGPRs
 # (no v_accvgpr_read per element)
 UNIT_FLAGS["dladmm_wgrad_x3.hip"] = ["-mllvm", "-amdgpu-mfma-vgpr-form"]

@@ -491,9 +491,9 @@ constexpr int kWgStages = 4;
 // xcd set the tiles of one (chunk, layer) run on one XCD back to back, so its L2 serves the G and
 // V row blocks they share (each V block is read by every G tile, each G block by every V tile)
 // once from HBM.  Without it, consecutive ids spread a chunk's tiles over the XCDs.
-// DPOS: where iteration s issues the LDS-DMA of step s + 3: 0 right after the barrier (beside
-// the fragment reads), 1 after the first quarter of the MFMAs, 2 one piece after each quarter
-template <int DPOS>
+// Iteration s issues the LDS-DMA of step s + 3 right after the barrier, beside the fragment reads
+// (issued after the first quarter of the MFMAs, or one piece after each quarter, it measured no
+// faster: round-5 A/B)
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a, int xcd) {
   __shared__ f32x4 ring[kWgStages * 16 * 64];
   const int lane = threadIdx.x & 63;
@@ -552,7 +552,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a, int xc
     else ring_barrier_n<0>();
     const bool more = s + kWgStages - 1 < steps;
     const int ns = s + kWgStages - 1, nst = (s + kWgStages - 1) % kWgStages;
-    if (DPOS == 0 && more) issue(ns, nst);
+    if (more) issue(ns, nst);
     const f32x4* st = ring + (s % kWgStages) * 16 * 64;
     f32x4 ga[4], va[4];
 #pragma unroll
@@ -566,19 +566,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgradArgs a, int xc
 #pragma unroll
         for (int y = 0; y < 4; ++y) acc[x][y] = mfma4(ga[x][q], va[y][q], acc[x][y]);
     };
-    if (DPOS == 0 || !more) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) quarter(q);
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        quarter(q);
-        __builtin_amdgcn_sched_barrier(0);
-        if (DPOS == 1 && q == 0) issue(ns, nst);
-        if (DPOS == 2) issue_f(ns, nst, q);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
+    for (int q = 0; q < 4; ++q) quarter(q);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA in flight when the LDS is released
   // C/D layout: lane holds column (l & 15) = V row j, rows 4g + r' = G rows
@@ -738,18 +727,11 @@ hipError_t launch_bwd(int phase, int variant, const BwdArgs& a, dim3 grid, int s
 }
 
 hipError_t launch_wgrad(const WgradArgs& a, int tiles, hipStream_t s, int layers) {
-  // XCD-grouped tiles where the (chunk, layer) count is a multiple of 8 (DLADMM_WGRAD_XCD=0:
-  // consecutive ids, A/B)
-  const char* x = getenv("DLADMM_WGRAD_XCD");
+  // XCD-grouped tiles where the (chunk, layer) count is a multiple of 8
   const int groups = a.nchunks * layers;
-  const int xcd = groups % 8 == 0 && !(x && atoi(x) == 0) ? 1 : 0;
+  const int xcd = groups % 8 == 0 ? 1 : 0;
   if (tiles != (a.NBp16 / 8) * (a.MBp16 / 8)) return hipErrorInvalidValue;
-  // LDS-DMA issue position (DLADMM_WGRAD_DPOS, A/B)
-  const char* dp = getenv("DLADMM_WGRAD_DPOS");
-  const int dpos = dp ? atoi(dp) : 0;
-  if (dpos == 1) hipLaunchKernelGGL(wgrad_kernel<1>, dim3(tiles * groups), dim3(256), 0, s, a, xcd);
-  else if (dpos == 2) hipLaunchKernelGGL(wgrad_kernel<2>, dim3(tiles * groups), dim3(256), 0, s, a, xcd);
-  else hipLaunchKernelGGL(wgrad_kernel<0>, dim3(tiles * groups), dim3(256), 0, s, a, xcd);
+  hipLaunchKernelGGL(wgrad_kernel, dim3(tiles * groups), dim3(256), 0, s, a, xcd);
   return hipGetLastError();
 }
 

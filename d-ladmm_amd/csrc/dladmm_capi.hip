@@ -7,7 +7,6 @@
 #include <vector>
 
 #include "dladmm_common.h"
-#include "dladmm_queue.h"
 #include "dladmm_wgrad_x3.h"
 #include "dladmm_internal.h"
 
@@ -15,7 +14,6 @@ namespace dladmm {
 
 // ------------------------------------------------------------------------ weight packing
 constexpr int kPackBatch = 64;  // sources per pack launch (the struct is a kernel argument)
-constexpr bool kBf16NarrowDefault = true;  // bf16 tiles: 128 columns (2 % faster at config 5)
 
 struct PackArgs {
   const float* src[kPackBatch];
@@ -334,11 +332,7 @@ struct Plan {
   int nslots;  // loss partials per (layer, term): slices x ldl per-column entries
   int ldl;     // columns per slice
   int nbp;     // bf16 path: 16-column blocks of the packed state
-  bool narrow;  // bf16 path: 128-column tiles (two workgroups per CU)
-  bool pipe1;   // bf16 path: G1 on the persistent pipelined kernel (dladmm_tile_bf16_pipe.hip)
-  bool queue;   // bf16 path: the whole forward as one persistent queue launch (wide tiles)
-  int lags;     // queue: diagonal lag classes
-  size_t off_qtab, off_qcnt;  // queue: phase-argument table, ticket / completion counters
+  bool narrow;  // bf16 path: 128-column tiles (two workgroups per CU; DLADMM_F_BF16_WIDE: 256)
   size_t off_ap, off_wp, off_v, off_zb, off_zw, off_ew, off_lw, off_loss, total;
   size_t off_btab;            // path 1, V1: device tables of the per-layer beta pointers
   size_t off_wexp, off_umax;  // path 4
@@ -405,75 +399,17 @@ inline bool shared_weight(const dladmm_fwd_desc* d) {
   return true;
 }
 
-// bf16 tiles: two column halves one phase apart per launch (dladmm_tile_bf16_pair.hip) when
-// the batch has at least two narrow column tiles.  DLADMM_BF16_PAIR=0 runs one phase per launch
-// (A/B measurements; the results are bit-identical)
-inline bool bf16_paired(const Plan& p) {
-  // measured slower than one phase per launch (profiles/r05_pair_ab.json): opt-in only
-  const char* e = getenv("DLADMM_BF16_PAIR");
-  return p.narrow && p.gx >= 2 && e && e[0] == '1';
-}
-
-// bf16 tiles: G1 as the persistent software-pipelined kernel (dladmm_tile_bf16_pipe.hip) when the
-// contraction (m) is 32 k-blocks of 32 (m = 993 .. 1024, config 5's 1024) and its 32-bit buffer
-// offsets hold (the padded rows of Z_{k-1} / Z_k and the packed copy).  Measured slower than the
-// one-phase kernel at config 5 (322 vs 260 us per G1: the epilogue's loads and stores contend
-// with the main loop's operand DMA in each CU's vector-memory path; profiles/r05_pipe_ab.json,
-// profiles/r05_cfg5_pmc.json): opt-in only, DLADMM_BF16_PIPE=1 (bit-identical outputs)
-inline bool bf16_pipe_g1(const dladmm_fwd_desc* d, const Plan& p) {
-  const char* e = getenv("DLADMM_BF16_PIPE");
-  if (!p.narrow || p.KB1 != 32 || !(e && e[0] == '1')) return false;
-  // per-row thresholds (V2 / V3): the one-phase kernel
-  if (d->variant == DLADMM_V2_LTHETA || d->variant == DLADMM_V3_FULL) return false;
-  const int64_t lim = (int64_t)1 << 31, rows = (int64_t)16 * p.MBp1;
-  const int64_t B = d->batch;
-  const int64_t ldmax = d->ld_z0 > d->ld_out ? d->ld_z0 : (d->ld_out > B ? d->ld_out : B);
-  return rows * ldmax * 4 < lim && (int64_t)p.KB2 * p.nbp * 1024 < lim;
-}
-
-// bf16 tiles: the whole forward as one persistent launch pulling tile units from work queues in
-// dependency order (dladmm_tile_bf16_queue.hip, bit-identical outputs): DLADMM_BF16_QUEUE=1
-inline bool bf16_queue() {
-  const char* e = getenv("DLADMM_BF16_QUEUE");
-  return e && e[0] == '1';
-}
-
-// the split-f16 weight-gradient kernel: precision "f32_split", whole 64-column sub-chunks,
-// unless DLADMM_WGRAD_X3=0
-inline bool use_wgrad_x3(bool x3w, const WgradArgs& wa) {
-  const char* e = getenv("DLADMM_WGRAD_X3");
-  return x3w && wgrad_x3_fits(wa) && !(e && e[0] == '0');
-}
-
-// compute units of the current device (the persistent kernels' grid), cached per device
-inline int device_cus() {
-  // DLADMM_PIPE_GRID=<g>: at most g persistent workgroups (tests: many tiles per workgroup on a
-  // small problem)
-  if (const char* e = getenv("DLADMM_PIPE_GRID")) {
-    const int g = atoi(e);
-    if (g > 0) return g;
-  }
-  static int cache[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (!cache[dev]) {
-    int v = 0;
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        v <= 0)
-      v = 256;
-    cache[dev] = v;
-  }
-  return cache[dev];
-}
+// the split-f16 weight-gradient kernel: precision "f32_split" (make_bwd_plan rounds its chunks
+// to whole 32-column sub-chunks), unless fwd.flags holds DLADMM_F_WGRAD_F32
+inline bool use_wgrad_x3(bool x3w, const WgradArgs& wa) { return x3w && wgrad_x3_fits(wa); }
 
 inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
   *p = Plan{};
   const int s = pick_shape(d->m, d->n);
   const int K = d->layers;
   const int64_t B = d->batch;
-  // DLADMM_PATH=layered forces the per-layer kernels (tests / A-B measurements)
-  const char* force = getenv("DLADMM_PATH");
-  const bool force_layered = force && force[0] == 'l';
+  // DLADMM_F_PER_LAYER forces the per-layer kernels (tests / A-B measurements)
+  const bool force_layered = (d->flags & DLADMM_F_PER_LAYER) != 0;
   const bool bf16 = d->precision == DLADMM_PREC_BF16;
   // split-f16 fused kernel: register-resident shapes, scalar-parameter variants (V4-V6); other
   // cases run the fp32 kernels (same results up to fp32 GEMM rounding)
@@ -527,25 +463,14 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
   p->MBp2 = ceil_div(MB, p->SB2) * p->SB2;
   p->slices1 = p->MBp1 / p->SB1;
   p->slices2 = p->MBp2 / p->SB2;
-  // bf16 tile width: DLADMM_BF16_TILE=wide|narrow (A/B measurements), default below
-  const char* tw = getenv("DLADMM_BF16_TILE");
-  p->narrow = bf16 && (tw ? tw[0] == 'n' : kBf16NarrowDefault);
-  p->queue = bf16 && bf16_queue();
-  if (p->queue) {
-    p->narrow = false;  // the queue runs the wide tile body, one workgroup per CU
-    const char* le = getenv("DLADMM_BF16_QUEUE_LAGS");
-    const int lv = le ? atoi(le) : 2;
-    p->lags = lv < 1 ? 1 : (lv > 8 ? 8 : lv);
-  }
+  // bf16 tile width: 128 columns (2 % faster at config 5) unless DLADMM_F_BF16_WIDE
+  p->narrow = bf16 && !(d->flags & DLADMM_F_BF16_WIDE);
   const int cols = bf16 ? bf16_tile_cols(p->narrow) : kLayerCols;
   p->gx = ceil_div(d->batch, cols);
   p->ldl = p->gx * cols;
   p->nbp = p->ldl / 16;
-  p->pipe1 = bf16 && !p->queue && bf16_pipe_g1(d, *p);
-  // loss partial slots per column: one per slice (bf16 tiles: one per slice and wave row; the
-  // pipelined G1 kernel's waves cover 64 rows: 4 per slice)
-  p->nslots = p->ldl * (p->slices1 > p->slices2 ? p->slices1 : p->slices2) *
-              (bf16 ? (p->pipe1 ? 4 : 2) : 1);
+  // loss partial slots per column: one per slice (bf16 tiles: one per slice and wave row)
+  p->nslots = p->ldl * (p->slices1 > p->slices2 ? p->slices1 : p->slices2) * (bf16 ? 2 : 1);
   const size_t fb = (size_t)kFrag * sizeof(float);
   p->off_ap = 0;
   p->off_wp = align256(fb * p->KB2 * p->MBp2);
@@ -557,11 +482,7 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
   p->off_ew = p->off_zw + (lean ? align256((size_t)d->n * B * sizeof(float)) : 0);
   p->off_lw = p->off_ew + (lean ? align256((size_t)d->m * B * sizeof(float)) : 0);
   p->off_loss = p->off_lw + (lean ? align256((size_t)d->m * B * sizeof(float)) : 0);
-  p->off_qtab = p->off_loss + align256((size_t)2 * K * p->nslots * sizeof(float));
-  const int nph = 2 * K + 1;
-  p->off_qcnt = p->off_qtab + (p->queue ? align256((size_t)nph * sizeof(LayerArgs)) : 0);
-  p->total = p->off_qcnt +
-             (p->queue ? align256((size_t)queue_counter_words(nph, p->gx) * sizeof(int)) : 0);
+  p->total = p->off_loss + align256((size_t)2 * K * p->nslots * sizeof(float));
   return 0;
 }
 
@@ -588,21 +509,19 @@ inline hipError_t pack(const float* const* srcs, int T, int R, int C, int64_t ld
   return hipSuccess;
 }
 
-// Device address of the per-wave cycle-sum buffer of the diagnostic stamp builds
-// (DLADMM_DBG_PTR, set by tools/x3_stamp.py); read once.  Regular builds never write it.
+// Device address of the per-wave cycle-sum buffer of the diagnostic stamp builds (built with
+// -DX3_STAMP by tools/x3_stamp.py, which passes the address in DLADMM_DBG_PTR); product builds
+// compile no stamp code and read nothing
 inline unsigned long long* dbg_ptr() {
+#if defined(X3_STAMP) && X3_STAMP
   static unsigned long long* const p = [] {
     const char* e = getenv("DLADMM_DBG_PTR");
     return e ? (unsigned long long*)strtoull(e, nullptr, 0) : nullptr;
   }();
   return p;
-}
-
-// DLADMM_BWD_UNFUSED=1: after a saved-product forward, BK1 still runs as its own launch
-// (phase 4) instead of inside BK3's (phase 6) -- A/B timing and the equivalence test
-inline bool fwd_unfused_bwd() {
-  const char* e = getenv("DLADMM_BWD_UNFUSED");
-  return e && e[0] == '1';
+#else
+  return nullptr;
+#endif
 }
 
 inline int run_fused(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStream_t s) {
@@ -728,44 +647,6 @@ inline int run_fused_x3(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipSt
   return 0;
 }
 
-// Launch the collected phases ph[0 .. nph) (nph = 2K + 1: prologue, G1(0), G2(0), ...) as 2K + 2
-// launches: launch t runs phase t on column half 0 (tiles [0, gx0)) and phase t - 1 on half 1.
-inline int launch_paired(int variant, const Plan& p, const LayerArgs* ph, int nph, hipStream_t s) {
-  const int gx0 = (p.gx + 1) / 2, gx1 = p.gx - gx0;
-  // DLADMM_BF16_PAIR_F=<permille>: the G2-shaped tiles are spread over the first F of the blocks
-  const char* fe = getenv("DLADMM_BF16_PAIR_F");
-  const int fv = fe ? atoi(fe) : 1000;
-  const int fpm = fv < 1 ? 1 : (fv > 1000 ? 1000 : fv);
-  auto ptype = [](int q) { return q == 0 ? 2 : ((q & 1) ? 0 : 1); };  // 2 prologue, 0 G1, 1 G2
-  auto rows = [&](int q) { return ptype(q) == 0 ? p.slices1 : p.slices2; };
-  for (int t = 0; t <= nph; ++t) {
-    const int q0 = t < nph ? t : -1, q1 = t - 1;
-    TilePairArgs pa{};
-    int t0, t1;
-    if (q0 >= 0) {   // half 0 at phase t [, half 1 at t - 1]
-      pa.a[0] = ph[q0]; pa.gx[0] = gx0; pa.x0[0] = 0; pa.n[0] = gx0 * rows(q0);
-      t0 = ptype(q0);
-      if (q1 >= 0) {
-        pa.a[1] = ph[q1]; pa.gx[1] = gx1; pa.x0[1] = gx0; pa.n[1] = gx1 * rows(q1);
-        t1 = ptype(q1);
-      } else {
-        pa.a[1] = ph[q0]; pa.gx[1] = 1; pa.n[1] = 0;  // (2, 0): prologue alone
-        t1 = 0;
-      }
-    } else {         // the last launch: half 1's G2(K-1) alone, as half 0 of a (1, 0) launch
-      pa.a[0] = ph[q1]; pa.gx[0] = gx1; pa.x0[0] = gx0; pa.n[0] = gx1 * rows(q1);
-      pa.a[1] = ph[q1]; pa.gx[1] = 1; pa.n[1] = 0;
-      t0 = 1; t1 = 0;
-    }
-    const int LH = t0 != 0 ? 0 : 1;
-    const int total = pa.n[0] + pa.n[1];
-    const int F = (int)(((int64_t)total * fpm + 999) / 1000);
-    pa.F = F < pa.n[LH] ? pa.n[LH] : (F < 1 ? 1 : F);
-    if (hipError_t e = launch_tile_bf16_pair(t0, t1, variant, pa, s)) return (int)e;
-  }
-  return 0;
-}
-
 inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStream_t s) {
   const int K = d->layers, m = d->m, n = d->n;
   const int64_t B = d->batch;
@@ -781,11 +662,7 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
   const int sb1 = p.SB1, sb2 = p.SB2;
   char* Vb = ws + p.off_v;   // bf16: packed Var_k (B operand of G1)
   char* Zb = ws + p.off_zb;  // bf16: packed Z_k / Z0 (B operand of G2)
-  const bool pipe1 = bf && p.pipe1;
-  const int cus = pipe1 ? device_cus() : 0;
   auto launch = [&](int phase, const LayerArgs& la, dim3 grid, int sb) -> hipError_t {
-    if (pipe1 && phase == 0)
-      return launch_tile_bf16_pipe_g1(d->variant, la, p.gx, p.slices1, cus, s);
     return bf ? launch_tile_bf16(phase, d->variant, p.narrow, la, grid, s)
               : launch_layer(phase, d->variant, la, grid, sb, s);
   };
@@ -816,14 +693,7 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
   a.lossp = d->loss_kind ? lossp : nullptr;
   const dim3 g1(p.gx, p.slices1), g2(p.gx, p.slices2);
   const bool v1 = d->variant == DLADMM_V1_LENA;
-  // bf16 tiles, two column halves one phase apart per launch (dladmm_tile_bf16_pair.hip):
-  // the phases are collected first (prologue, G1(0), G2(0), ..., G2(K-1)) and launched in pairs
-  const bool paired = bf && bf16_paired(p);
-  const bool queue = bf && p.queue;
-  std::vector<LayerArgs> ph(paired || queue ? 2 * K + 1 : 0);
-  int nph = 0;
   auto run = [&](int phase, const LayerArgs& la, dim3 grid, int sb) -> hipError_t {
-    if (paired || queue) { ph[nph++] = la; return hipSuccess; }
     return launch(phase, la, grid, sb);
   };
   if (d->ev_kernel_start) {
@@ -882,26 +752,6 @@ inline int run_layered(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStr
     }
     if (hipError_t e = run(1, c, g2, sb2)) return (int)e;
   }
-  if (paired) {
-    if (const int e = launch_paired(d->variant, p, ph.data(), nph, s)) return e;
-  }
-  if (queue) {
-    LayerArgs* tab = (LayerArgs*)(ws + p.off_qtab);
-    int* cnt = (int*)(ws + p.off_qcnt);
-    if (hipError_t e = write_layer_table(ph.data(), nph, tab, s)) return (int)e;
-    if (hipError_t e = zero_async(cnt, (size_t)queue_counter_words(nph, p.gx) * sizeof(int), s))
-      return (int)e;
-    QueueArgs qa{};
-    qa.ph = tab; qa.nph = nph; qa.gx = p.gx;
-    qa.rows1 = p.slices1; qa.rows2 = p.slices2; qa.lags = p.lags;
-    qa.tickets = cnt; qa.done = cnt + 8 * 32;
-    qa.err = cnt + queue_counter_words(nph, p.gx) - 1;
-    if (hipError_t e = launch_tile_bf16_queue(d->variant, qa, device_cus(), s)) return (int)e;
-    float* z_last = lean ? d->Z : d->Z + (int64_t)(K - 1) * zl;
-    if (hipError_t e = launch_queue_check(qa, z_last, d->loss_kind ? lossp : nullptr, 2 * K,
-                                          p.nslots, s))
-      return (int)e;
-  }
   if (d->ev_kernel_stop) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_stop, s)) return (int)e;
   }
@@ -928,19 +778,8 @@ struct BwdPlan {
   size_t off_ratp, off_rmtp, off_gu, off_rvar, off_rpart, off_rptab, off_rrow;
 };
 
-// DLADMM_BWD_ZMASK=0: V2 / V3 form q = W_k Var_k in BK2 (PH 2) instead of reading the shrink
-// masks off the saved Z_k (PH 5)
-inline bool zmask_rows_enabled() {
-  const char* e = getenv("DLADMM_BWD_ZMASK");
-  return !(e && e[0] == '0');
-}
-
-// DLADMM_BWD_REV=0: the per-layer backward kernels even where the reverse-sweep kernel applies
-// (A/B timing and the equivalence tests)
-inline bool rev_enabled() {
-  const char* e = getenv("DLADMM_BWD_REV");
-  return !(e && e[0] == '0');
-}
+// plan options of the backward, from the forward descriptor it carries (enum dladmm_flags)
+inline bool bwd_flag(const dladmm_fwd_desc& f, int flag) { return (f.flags & flag) != 0; }
 
 inline int validate_bwd(const dladmm_bwd_desc* d) {
   if (!d) return DLADMM_E_NULL;
@@ -976,20 +815,18 @@ inline int validate_bwd(const dladmm_bwd_desc* d) {
 inline int64_t round_up(int64_t x, int64_t q) { return (x + q - 1) / q * q; }
 inline int64_t K_of(const dladmm_fwd_desc& f) { return f.layers; }
 
-// Largest workspace the reverse sweep may ask for: DLADMM_REV_WS_MAX_MB, else a quarter of the
-// device's memory (72 GB on an MI355X)
+// Largest workspace the reverse sweep may ask for: a quarter of the device's memory (72 GB on an
+// MI355X)
 inline size_t rev_ws_cap() {
-  static const size_t cap = [] {
-    const char* e = getenv("DLADMM_REV_WS_MAX_MB");
-    if (e && *e) return (size_t)strtoull(e, nullptr, 10) << 20;
-    int dev = 0;
+  static size_t cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return (size_t)64 << 30;
+  if (!cache[dev]) {
     size_t total = 0;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceTotalMem(&total, dev) == hipSuccess &&
-        total)
-      return total / 4;
-    return (size_t)64 << 30;
-  }();
-  return cap;
+    cache[dev] = hipDeviceTotalMem(&total, dev) == hipSuccess && total ? total / 4
+                                                                        : (size_t)64 << 30;
+  }
+  return cache[dev];
 }
 
 inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
@@ -1001,7 +838,7 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   dladmm_fwd_desc f32 = f;
   f32.precision = DLADMM_PREC_F32;
   if (int e = make_plan(&f32, &p->fwd)) return e;
-  p->x3w = f.precision == DLADMM_PREC_F32_SPLIT;
+  p->x3w = f.precision == DLADMM_PREC_F32_SPLIT && !bwd_flag(f, DLADMM_F_WGRAD_F32);
   // the forward stored A Z_k only on the fused paths, fp32 and split-f16 (fwd_desc.P)
   p->saved_p = f.P != nullptr && f.keep_all && (p->fwd.path == 1 || p->fwd.path == 4);
   const int m = f.m, n = f.n;
@@ -1033,8 +870,11 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   const bool cot_ok = !(d->gZ || d->gE || d->gL || d->gT) || d->ld_g == f.ld_out;
   const bool v1_ok = f.variant != DLADMM_V1_LENA || f.ld_beta == f.ld_out;
   if (p->saved_p && reverse_supports(f.variant) && cot_ok && v1_ok &&
-      f.ld_e0 == f.ld_out && f.ld_l0 == f.ld_out && rev_enabled()) {
+      f.ld_e0 == f.ld_out && f.ld_l0 == f.ld_out && !bwd_flag(f, DLADMM_F_BWD_PER_LAYER)) {
     const int MP = kShapeMP[p->fwd.shape], NP = kShapeNP[p->fwd.shape];
+    // the split-f16 weight gradient runs whole 32-column sub-chunks: pad its operand columns to
+    // 32 (the sweep writes zeros up to bpad; its tiles cover 64 columns) so every batch takes it
+    const int64_t bpad = p->x3w ? round_up(B, 32) : p->Bpad;
     p->Rn2 = round_up(NP, 128);
     p->Rm2 = round_up(MP, 128);
     const int64_t lim = (int64_t)1 << 31;
@@ -1043,12 +883,13 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
     // above rev_ws_cap() the per-layer phases run instead of a workspace that may not fit
     const bool rowv = f.variant == DLADMM_V2_LTHETA || f.variant == DLADMM_V3_FULL;
     const size_t rev_bytes = (size_t)(K_of(f) + 1) * MP * NP * 4 +
-                             (size_t)K_of(f) * (p->Rn2 + p->Rm2 + MP) * p->Bpad * 4 +
+                             (size_t)K_of(f) * (p->Rn2 + p->Rm2 + MP) * bpad * 4 +
                              (rowv ? (size_t)8 * K_of(f) * (MP > NP ? MP : NP) *
                                          ((B + 63) / 64 * 4) * 4 : 0);
-    if ((int64_t)NP * p->Bpad * 4 < lim && 2 * (p->Rm2 + MP) * p->Bpad * 4 < lim &&
+    if ((int64_t)NP * bpad * 4 < lim && 2 * (p->Rm2 + MP) * bpad * 4 < lim &&
         rev_bytes <= rev_ws_cap()) {
       p->rev = true;
+      p->Bpad = bpad;
       p->Rn = p->Rn2;  // the weight gradient reads the reverse kernel's row padding
       p->Rm = p->Rm2;
       p->rtiles = ceil_div(f.batch, kTileCols);
@@ -1056,11 +897,15 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
     }
   }
   p->wtiles = (int)((p->Rn / 128) * (p->Rm / 128));
-  const int64_t steps = p->Bpad / 16;
+  // split-K chunks: whole 16-column k-steps, or 32-column sub-chunks for the split-f16 kernel
+  // (the reverse sweep's Bpad is then a multiple of 32; the per-layer backward keeps 16 and its
+  // odd-16 chunks take the fp32 kernel)
+  const int q = p->x3w && p->rev ? 32 : 16;
+  const int64_t steps = p->Bpad / q;
   int64_t nch = (512 + p->wtiles - 1) / p->wtiles;
   if (nch > steps) nch = steps;
   if (nch < 1) nch = 1;
-  p->chunk = ceil_div((int)steps, (int)nch) * 16;
+  p->chunk = ceil_div((int)steps, (int)nch) * q;
   p->nchunks = (int)((p->Bpad + p->chunk - 1) / p->chunk);
   const size_t fb = (size_t)kFrag * sizeof(float);
   const size_t colb = (size_t)p->Bpad * sizeof(float);
@@ -1296,7 +1141,7 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
   // with the forward's saved products (p.saved_p) BK1 of layer k-1 runs inside BK3(k)'s launch
   // (phase 6); the parameter-slot partials of layer k then live in part buffer k & 1 (layer k's
   // BK1 slots are written one iteration before its BK2 / BK3 ones)
-  const bool fuse = p.saved_p && !fwd_unfused_bwd();
+  const bool fuse = p.saved_p && !bwd_flag(f, DLADMM_F_BWD_UNFUSED);
   float* part2 = (float*)(ws + p.off_part2);
   auto partk = [&](int k) { return (fuse && (k & 1)) ? part2 : part; };
   // phase 4: a wave covers 64 columns (one per lane), so its grid has a quarter of the tiles
@@ -1365,7 +1210,7 @@ inline int run_bwd(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hipStre
     // per-row theta_z (V2, V3): PH 5 when no row of the layer has theta_z < 0 (checked on the
     // device), PH 2 otherwise (DLADMM_BWD_ZMASK=0: the recomputing PH 2 for these too -- A/B
     // and equivalence tests)
-    const bool zrow = (v == DLADMM_V2_LTHETA || v == DLADMM_V3_FULL) && zmask_rows_enabled();
+    const bool zrow = (v == DLADMM_V2_LTHETA || v == DLADMM_V3_FULL) && !bwd_flag(f, DLADMM_F_BWD_NO_ZMASK);
     // mask variants: a PH 5 launch (32-block slices, one GEMM) does the layer when theta_z >= 0,
     // the PH 2 launch when theta_z < 0; the other exits at once (the sign is read on the device)
     // (per-row kinds: the PH 5 launch when every row's theta_z >= 0, else the PH 2 launch)

@@ -109,21 +109,6 @@ constexpr int kTileBlocks = 16;                 // row blocks per tile
 constexpr int bf16_tile_cols(bool narrow) { return narrow ? 128 : 256; }
 hipError_t launch_tile_bf16(int phase, int variant, bool narrow, const LayerArgs& a, dim3 grid,
                             hipStream_t s);
-// Two column halves one phase apart in one launch (dladmm_tile_bf16_pair.hip, narrow tiles):
-// half h runs layer product a[h] (phase ph0 / ph1: 0 = G1, 1 = G2, 2 = prologue) on column tiles
-// x0[h] .. x0[h] + gx[h] - 1, n[h] = gx[h] * its row tiles blocks; the G2-shaped half's blocks are
-// spread evenly over the first F blocks of the grid (F >= its n)
-struct TilePairArgs {
-  LayerArgs a[2];
-  int gx[2], x0[2], n[2];
-  int F;
-};
-hipError_t launch_tile_bf16_pair(int ph0, int ph1, int variant, const TilePairArgs& pa,
-                                 hipStream_t s);
-// G1 of the bf16 path as a persistent software-pipelined tile loop (dladmm_tile_bf16_pipe.hip):
-// narrow tile geometry, grid min(gx * slices, cus), contraction of at most 32 k-blocks
-hipError_t launch_tile_bf16_pipe_g1(int variant, const LayerArgs& a, int gx, int slices, int cus,
-                                    hipStream_t s);
 // Z0 [rows][ld] fp32 -> packed bf16 B operand [KB][nbp] (RNE, zero padding)
 hipError_t pack_state_bf16(const float* S, int64_t ld, int rows, int64_t cols, int KB, int nbp,
                            void* out, hipStream_t s);

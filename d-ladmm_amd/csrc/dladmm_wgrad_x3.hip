@@ -17,8 +17,14 @@
 // unscale at the end.  The dropped lo lo term is 2^-22 of a product; elements more than 2^-29
 // below the running largest go subnormal in f16, i.e. contribute below 2^-29 of that largest
 // product.  Fixed order throughout: the result is deterministic.  Not bit-equal to wgrad_kernel
-// (a different rounding sequence of the same sum).  DLADMM_WGRAD_X3_RUN=0: one scale per
-// sub-chunk and an unscale-add per sub-chunk (the first form, A/B).
+// (a different rounding sequence of the same sum).
+//
+// Dynamic range.  The scales are per wave, not per row: a G (or V) row more than ~2^17 below
+// the largest magnitude its wave has seen in the chunk keeps fewer than 22 significant bits in
+// hi + lo, and one ~2^29 below it contributes nothing.  The error of every output element is
+// therefore bounded relative to the largest product in its wave's 64 x 64 block (the bound of
+// an fp32 GEMM relative to |G| |V|^T), not to that element's own rows
+// (tests/test_gpu_split.py::test_split_weight_gradient_row_range measures it).
 //
 // Geometry.  Partial layout of wgrad_kernel, a 1-D grid over (tile, chunk, layer).  A workgroup
 // covers 128 G rows x TJ V rows (TJ = 256 where the padded V rows allow: 8 waves of 64 x 64, one
@@ -93,10 +99,6 @@ __device__ __forceinline__ void split8(const f32x4& p0, const f32x4& p1, float s
   lo = __builtin_bit_cast(h8, u32x4{L[0], L[1], L[2], L[3]});
 }
 
-#ifndef WX3_PRIO
-#define WX3_PRIO 0  // A/B build: raised wave priority around the MFMA phase (s_setprio)
-#endif
-
 constexpr int kSub = 32;   // batch columns per sub-chunk (one k-step of 32)
 
 // Tile geometry by V-tile width TJ: 128 G rows x TJ V rows, waves of 64 x 64 (2 wave rows x
@@ -111,16 +113,13 @@ struct WgX3 {
   static_assert(PIECES % NW == 0, "even DMA share per wave");
 };
 
-// RUN: one running scale per operand over the chunk (below) instead of one per sub-chunk.
-// NBUF sub-chunk buffers: NBUF - 1 sub-chunks stream in while one is read.  SPEC (with RUN):
-// split each sub-chunk speculatively at the running scales in the same straight-line block as the
-// previous sub-chunk's MFMAs (two operand register sets), re-splitting in the rare case a
-// magnitude reached them.
-// DPOS: where the LDS-DMA of sub-chunk s + NBUF - 1 is issued in iteration s (non-SPEC loop):
-// 0 right after the fragment reads, 1 after the MFMAs of s - 1, 2 one piece per operand split
-// (an LDS-DMA instruction costs its wave ~60 cycles among MFMAs / VALU but 100-185 beside
-// ds_reads, MI355X_MICROARCH.md)
-template <int TJ, bool RUN, int NBUF, bool SPEC = false, int DPOS = 0>
+// One running scale per operand over the chunk (below).  NBUF sub-chunk buffers: NBUF - 1
+// sub-chunks stream in while one is read.  DPOS: where the LDS-DMA of sub-chunk s + NBUF - 1 is
+// issued in iteration s: 0 right after the fragment reads, 1 after the MFMAs of s - 1 (an
+// LDS-DMA instruction costs its wave ~60 cycles among MFMAs / VALU but 100-185 beside ds_reads,
+// MI355X_MICROARCH.md).  Round 5 also measured a per-sub-chunk scale, a speculative split beside
+// the MFMAs and the DMA spread over the split: all slower (profiles/r05_wgrad_x3_steps.json).
+template <int TJ, int NBUF, int DPOS>
 __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_kernel(
     const WgradArgs a, int xcd) {
   using T = WgX3<TJ>;
@@ -194,8 +193,7 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
   // Software-pipelined: iteration s reads and splits sub-chunk s, then runs the MFMAs of s - 1
   // (split in the previous iteration) while the LDS reads of s land.
   h8 ah[4], al[4], bh[4], bl[4];
-  float uns = 0.f;
-  // RUN: the accumulators hold the sum at scale 2^(ea + eb), where 2^ea / 2^eb put the largest
+  // The accumulators hold the sum at scale 2^(ea + eb), where 2^ea / 2^eb put the largest
   // G / V magnitude of this wave's rows SO FAR in the chunk in [2^14, 2^15); a sub-chunk that
   // exceeds it (any lane at or above lim) lowers the exponent and rescales the accumulators by
   // the exact power of two, so the MFMAs accumulate straight into them and the per-sub-chunk
@@ -203,33 +201,19 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
   int ea = 127, eb = 127;
   float sa = ldexpf(1.0f, 127), sbs = sa, lima = ldexpf(1.0f, -112), limb = lima;
   auto mfmas = [&]() {
-    if constexpr (RUN) {
-      // three passes over the 16 independent accumulators (no back-to-back dependent MFMAs)
+    // three passes over the 16 independent accumulators (no back-to-back dependent MFMAs)
 #pragma unroll
-      for (int x = 0; x < 4; ++x)
+    for (int x = 0; x < 4; ++x)
 #pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] = mfma_h(ah[x], bh[y], acc[x][y]);
+      for (int y = 0; y < 4; ++y) acc[x][y] = mfma_h(ah[x], bh[y], acc[x][y]);
 #pragma unroll
-      for (int x = 0; x < 4; ++x)
+    for (int x = 0; x < 4; ++x)
 #pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] = mfma_h(ah[x], bl[y], acc[x][y]);
+      for (int y = 0; y < 4; ++y) acc[x][y] = mfma_h(ah[x], bl[y], acc[x][y]);
 #pragma unroll
-      for (int x = 0; x < 4; ++x)
+    for (int x = 0; x < 4; ++x)
 #pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] = mfma_h(al[x], bh[y], acc[x][y]);
-    } else {
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y) {
-          f32x4 c = {0.f, 0.f, 0.f, 0.f};
-          c = mfma_h(ah[x], bh[y], c);
-          c = mfma_h(ah[x], bl[y], c);
-          c = mfma_h(al[x], bh[y], c);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) acc[x][y][q] = __builtin_fmaf(c[q], uns, acc[x][y][q]);
-        }
-    }
+      for (int y = 0; y < 4; ++y) acc[x][y] = mfma_h(al[x], bh[y], acc[x][y]);
   };
   auto wait_bar = [&](int s) {
     // sub-chunk s landed for every wave (three buffers: this wave's PPW DMAs of s + 1 may stay
@@ -239,95 +223,7 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
     else
       asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   };
-  if constexpr (RUN && SPEC) {
-    struct Ops { h8 ah[4], al[4], bh[4], bl[4]; };
-    Ops P, Q;
-    // sub-chunk s split at the current scales into o; ma / mb: this lane's magnitudes; true when
-    // one reached its scale's limit somewhere in the wave (o then holds overflowed halves)
-    auto split_sub = [&](int s, Ops& o, float& ma, float& mb) -> bool {
-      const f32x4* im = img + (s % kBufs) * T::PIECES * 64;
-      ma = 0.f;
-      mb = 0.f;
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const f32x4 p0 = im[((4 * wr + x) * 2) * 64 + lane], p1 = im[((4 * wr + x) * 2 + 1) * 64 + lane];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) ma = fmaxf(ma, fmaxf(fabsf(p0[q]), fabsf(p1[q])));
-        split8(p0, p1, sa, o.ah[x], o.al[x]);
-      }
-#pragma unroll
-      for (int y = 0; y < 4; ++y) {
-        const f32x4 p0 = im[(T::GP + (4 * wc + y) * 2) * 64 + lane];
-        const f32x4 p1 = im[(T::GP + (4 * wc + y) * 2 + 1) * 64 + lane];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) mb = fmaxf(mb, fmaxf(fabsf(p0[q]), fabsf(p1[q])));
-        split8(p0, p1, sbs, o.bh[y], o.bl[y]);
-      }
-      return (__builtin_amdgcn_ballot_w64(ma >= lima) | __builtin_amdgcn_ballot_w64(mb >= limb)) != 0;
-    };
-    // rare: lower the scales, rescale the accumulators (every MFMA at the old scales precedes
-    // this in program order) and split sub-chunk s again
-    auto grow = [&](int s, Ops& o, float ma, float mb) {
-      const bool ga = __builtin_amdgcn_ballot_w64(ma >= lima) != 0;
-      const bool gb = __builtin_amdgcn_ballot_w64(mb >= limb) != 0;
-      const int na = ga ? split_exp(wave_max(ma)) : ea;
-      const int nb = gb ? split_exp(wave_max(mb)) : eb;
-      const float fa2 = ldexpf(1.0f, na - ea), fb2 = ldexpf(1.0f, nb - eb);
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) acc[x][y][q] = acc[x][y][q] * fa2 * fb2;
-      ea = na;
-      eb = nb;
-      sa = ldexpf(1.0f, ea);
-      sbs = ldexpf(1.0f, eb);
-      lima = ldexpf(1.0f, 15 - ea);
-      limb = ldexpf(1.0f, 15 - eb);
-      float m2a, m2b;
-      (void)split_sub(s, o, m2a, m2b);
-    };
-    auto mf = [&](const Ops& o) {
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] = mfma_h(o.ah[x], o.bh[y], acc[x][y]);
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] = mfma_h(o.ah[x], o.bl[y], acc[x][y]);
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] = mfma_h(o.al[x], o.bh[y], acc[x][y]);
-    };
-    // iteration s: MFMAs of s - 1 (cur) and the split of s (nxt) in one block
-    auto step = [&](int s, Ops& cur, Ops& nxt) {
-      wait_bar(s);
-      if (s + kBufs - 1 < nsub) issue(s + kBufs - 1, (s + kBufs - 1) % kBufs);
-      mf(cur);
-      float ma, mb;
-      if (split_sub(s, nxt, ma, mb)) grow(s, nxt, ma, mb);
-    };
-    if (nsub > 0) {
-      wait_bar(0);
-      if (kBufs - 1 < nsub) issue(kBufs - 1, (kBufs - 1) % kBufs);
-      float ma, mb;
-      if (split_sub(0, P, ma, mb)) grow(0, P, ma, mb);
-      int s = 1;
-      for (; s + 1 < nsub; s += 2) {
-        step(s, P, Q);
-        step(s + 1, Q, P);
-      }
-      if (s < nsub) {
-        step(s, P, Q);
-        mf(Q);
-      } else {
-        mf(P);
-      }
-    }
-  } else {
+  {
     for (int s = 0; s < nsub; ++s) {
       wait_bar(s);
       const f32x4* im = img + (s % kBufs) * T::PIECES * 64;
@@ -343,9 +239,7 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
       const bool more = s + kBufs - 1 < nsub;
       const int nx = s + kBufs - 1, nbuf = (s + kBufs - 1) % kBufs;
       if (DPOS == 0 && more) issue(nx, nbuf);
-      if (WX3_PRIO) __builtin_amdgcn_s_setprio(1);
       if (s > 0) mfmas();  // sub-chunk s - 1, while the reads above land
-      if (WX3_PRIO) __builtin_amdgcn_s_setprio(0);
       if (DPOS == 1 && more) issue(nx, nbuf);
       float ma = 0.f, mb = 0.f;
 #pragma unroll
@@ -357,7 +251,7 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
             ma = fmaxf(ma, fabsf(fa[x][hf][q]));
             mb = fmaxf(mb, fabsf(fb[x][hf][q]));
           }
-      if constexpr (RUN) {
+      {
         // (after the MFMAs of s - 1, which used the old scales)
         const bool ga = __builtin_amdgcn_ballot_w64(ma >= lima) != 0;
         const bool gb = __builtin_amdgcn_ballot_w64(mb >= limb) != 0;
@@ -378,29 +272,16 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
           lima = ldexpf(1.0f, 15 - ea);
           limb = ldexpf(1.0f, 15 - eb);
         }
-      } else {
-        ea = split_exp(wave_max(ma));
-        eb = split_exp(wave_max(mb));
-        sa = ldexpf(1.0f, ea);
-        sbs = ldexpf(1.0f, eb);
-        uns = ldexpf(1.0f, -(ea + eb));
       }
-      auto split_all = [&](auto D_) {
-        constexpr bool D = decltype(D_)::value;
 #pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          split8(fa[x][0], fa[x][1], sa, ah[x], al[x]);
-          if constexpr (D) if (2 * x < T::PPW) issue_piece(nx, nbuf, 2 * x);
-          split8(fb[x][0], fb[x][1], sbs, bh[x], bl[x]);
-          if constexpr (D) if (2 * x + 1 < T::PPW) issue_piece(nx, nbuf, 2 * x + 1);
-        }
-      };
-      if (DPOS == 2 && more) split_all(std::true_type{});
-      else split_all(std::false_type{});
+      for (int x = 0; x < 4; ++x) {
+        split8(fa[x][0], fa[x][1], sa, ah[x], al[x]);
+        split8(fb[x][0], fb[x][1], sbs, bh[x], bl[x]);
+      }
     }
     if (nsub > 0) mfmas();
   }
-  if constexpr (RUN) {
+  {
     // one exact unscale (two factors: 2^-(ea + eb) alone could leave the float range)
     const float ua = ldexpf(1.0f, -ea), ub = ldexpf(1.0f, -eb);
 #pragma unroll
@@ -431,44 +312,21 @@ __global__ __launch_bounds__(WgX3<TJ>::NW * 64, WgX3<TJ>::OCC) void wgrad_x3_ker
 hipError_t launch_wgrad_x3(const WgradArgs& a, int tiles, hipStream_t s, int layers) {
   // tiles: the caller's 128 x 128 count (the launch re-tiles at the V-tile width chosen here)
   if (!wgrad_x3_fits(a) || tiles != (a.NBp16 / 8) * (a.MBp16 / 8)) return hipErrorInvalidValue;
-  // 256-row V tiles where the padded V rows allow (DLADMM_WGRAD_X3_TJ=128 forces the narrow
-  // form: A/B)
-  const char* e = getenv("DLADMM_WGRAD_X3_TJ");
-  const bool wide = a.MBp16 % 16 == 0 && !(e && atoi(e) == 128);
+  // 256-row V tiles where the padded V rows allow: three sub-chunk buffers (144 KiB: two
+  // sub-chunks in flight), the LDS-DMA issued after the MFMAs (539-556 vs 558-582 us right after
+  // the fragment reads).  Else 128-row tiles, two workgroups per CU, two buffers, the early issue
+  // (409 vs 418-421 us at m = 64).  XCD-grouped tiles where the (chunk, layer) count is a
+  // multiple of 8.
+  const bool wide = a.MBp16 % 16 == 0;
   const int ti = a.NBp16 / 8;
-  // running scales over the chunk (DLADMM_WGRAD_X3_RUN=0: one scale per sub-chunk, A/B);
-  // XCD-grouped tiles where the (chunk, layer) count is a multiple of 8 (DLADMM_WGRAD_X3_XCD=0:
-  // consecutive ids, A/B)
-  const char* r = getenv("DLADMM_WGRAD_X3_RUN");
-  const bool run = !(r && atoi(r) == 0);
-  const char* x = getenv("DLADMM_WGRAD_X3_XCD");
   const int groups = a.nchunks * layers;
-  const int xcd = groups % 8 == 0 && !(x && atoi(x) == 0) ? 1 : 0;
+  const int xcd = groups % 8 == 0 ? 1 : 0;
   const int nt = ti * (wide ? a.MBp16 / 16 : a.MBp16 / 8);
-  // three sub-chunk buffers at the 256 width (144 KiB: two sub-chunks in flight;
-  // DLADMM_WGRAD_X3_BUFS=2: one, A/B)
-  const char* b = getenv("DLADMM_WGRAD_X3_BUFS");
-  const bool b3 = wide && run && !(b && atoi(b) == 2);
-  const dim3 grid(nt * groups), bw(WgX3<256>::NW * 64), bn(WgX3<128>::NW * 64);
-  // speculative split beside the MFMAs: opt-in (DLADMM_WGRAD_X3_SPEC=1), measured slower
-  // (609-613 vs 561 us, profiles/r05_wgrad_x3_steps.json)
-  const char* sp = getenv("DLADMM_WGRAD_X3_SPEC");
-  const bool spec = b3 && sp && atoi(sp) == 1;
-  // LDS-DMA issue position: after the MFMAs (539-556 vs 558-582 us right after the fragment
-  // reads, 574-585 spread over the split; DLADMM_WGRAD_X3_DPOS=0 / 2, A/B).  The 128-row form
-  // (two workgroups per CU, two buffers) keeps the early issue: 418-421 vs 409 us at m = 64.
-  const char* dp = getenv("DLADMM_WGRAD_X3_DPOS");
-  const int dpos = dp ? atoi(dp) : 1;
-  if (spec) hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 3, true>), grid, bw, 0, s, a, xcd);
-  else if (b3 && dpos == 0)
-    hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 3, false, 0>), grid, bw, 0, s, a, xcd);
-  else if (b3 && dpos == 2)
-    hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 3, false, 2>), grid, bw, 0, s, a, xcd);
-  else if (b3) hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 3, false, 1>), grid, bw, 0, s, a, xcd);
-  else if (wide && run) hipLaunchKernelGGL((wgrad_x3_kernel<256, true, 2>), grid, bw, 0, s, a, xcd);
-  else if (wide) hipLaunchKernelGGL((wgrad_x3_kernel<256, false, 2>), grid, bw, 0, s, a, xcd);
-  else if (run) hipLaunchKernelGGL((wgrad_x3_kernel<128, true, 2>), grid, bn, 0, s, a, xcd);
-  else hipLaunchKernelGGL((wgrad_x3_kernel<128, false, 2>), grid, bn, 0, s, a, xcd);
+  const dim3 grid(nt * groups);
+  if (wide)
+    hipLaunchKernelGGL((wgrad_x3_kernel<256, 3, 1>), grid, dim3(WgX3<256>::NW * 64), 0, s, a, xcd);
+  else
+    hipLaunchKernelGGL((wgrad_x3_kernel<128, 2, 0>), grid, dim3(WgX3<128>::NW * 64), 0, s, a, xcd);
   return hipGetLastError();
 }
 

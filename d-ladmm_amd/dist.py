@@ -36,6 +36,19 @@ def global_objectives(local_sums: torch.Tensor, alpha: float, total_batch: int,
     return torch.add(s[:, 1], s[:, 0], alpha=alpha).div_(total_batch)
 
 
+def rank_local_params(module: torch.nn.Module) -> set:
+    """ids of the rank-local parameters of `module` and its children: the per-sample betas
+    (main_lena.py:35-36) of every submodule that is a batch shard (its `batch_shard` set by the
+    batch_shard= constructor keyword or shard_batch_), found from the module structure itself --
+    so a deep copy, or parameters re-registered by later code, are still recognised."""
+    ids = set()
+    for mod in module.modules():
+        if getattr(mod, "batch_shard", None) is not None and hasattr(mod, "_elem_param_lists"):
+            for pl in mod._elem_param_lists():
+                ids.update(id(p) for p in pl)
+    return ids
+
+
 def allreduce_grads(module: torch.nn.Module, group: Optional[dist.ProcessGroup] = None,
                     average: bool = False) -> None:
     """Data-parallel training over batch shards: ONE all-reduce of every parameter gradient,
@@ -44,13 +57,13 @@ def allreduce_grads(module: torch.nn.Module, group: Optional[dist.ProcessGroup] 
     each rank's gradient is its shard's share of the global-batch objective, so SUM (the default)
     gives the full-batch gradient; `average=True` divides by the world size instead (losses
     normalised by the local batch).
-    Rank-local parameters -- V1's per-sample betas of a module made a batch shard by
-    `shard_batch_` (main_lena.py:35-36: one column per sample) -- are not in the bucket: their
+    Rank-local parameters -- V1's per-sample betas of a module that is a batch shard
+    (main_lena.py:35-36: one column per sample; rank_local_params) -- are not in the bucket: their
     gradient is already complete on the rank that holds those columns."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return
-    ps = [p for p in module.parameters()
-          if p.grad is not None and not getattr(p, "_dladmm_rank_local", False)]
+    local = rank_local_params(module)
+    ps = [p for p in module.parameters() if p.grad is not None and id(p) not in local]
     if not ps:
         return
     flat = torch.cat([p.grad.reshape(-1) for p in ps])
@@ -75,7 +88,12 @@ def gather_state_dict(module: torch.nn.Module, group: Optional[dist.ProcessGroup
     if shard is None:
         return sd
     c0, c1, B = shard
-    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    up = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size(group) if up else 1
+    rank = dist.get_rank(group) if up else 0
+    if tuple(getattr(module, "world", (rank, world))) != (rank, world):
+        raise RuntimeError(f"dladmm: the module is shard {module.world} (rank, world) but the "
+                           f"process group is rank {rank} of {world}")
     local = {f"{nm}.{k}" for nm in module._elem_names() for k in range(module.layers)}
     if world == 1:
         if c1 - c0 != B:

@@ -50,20 +50,39 @@ class _DLADMMBase(nn.Module):
     WSCALE = 1.0     # fc init scale: main_lena.py:49 (1.0) / main_syn_l1l1_scalar.py:72 (0.4)
     NAME = "DLADMMNet"
 
-    def __init__(self, m, n, d, batch_size, A, Z0, E0, L0, layers):
+    def __init__(self, m, n, d, batch_size, A, Z0, E0, L0, layers, *, batch_shard=None):
+        """The reference constructor (main_lena.py:17-49), plus the keyword `batch_shard=(rank,
+        world)`: build rank `rank`'s share of a data-parallel run directly -- Z0 / E0 / L0 given
+        with batch_size columns are sliced to the rank's span (on their own device, before the
+        move to the GPU; already-sliced ones are taken as they are) and V1's per-sample betas
+        are registered at (m, c1 - c0) from the start, so no rank ever holds the global
+        2 K m batch_size betas (main_lena.py:35-36).  Same parameters, names and initial values
+        as the replicated module followed by shard_batch_(rank, world)."""
         super().__init__()
         self.m = m
         self.n = n
         self.d = d
         self.batch_size = batch_size
+        self.layers = layers
+        self.batch_shard = None   # (c0, c1, batch_size) of a data-parallel shard
+        cols = None
+        if batch_shard is not None:
+            from .dist import shard_columns
+            rank, world = (int(x) for x in batch_shard)
+            cols = shard_columns(batch_size, rank, world)
+            Z0, E0, L0 = (_shard_cols(t, batch_size, cols, nm)
+                          for t, nm in ((Z0, "Z0"), (E0, "E0"), (L0, "L0")))
         self.A = _dev(A)
         self.Z0 = _dev(Z0)
         self.E0 = _dev(E0)
         self.L0 = _dev(L0)
-        self.layers = layers
-        self.batch_shard = None   # (c0, c1, batch_size) after shard_batch_ (data parallel)
+        # columns of the per-sample parameters this module holds (V1's betas)
+        self._pcols = batch_size if cols is None else cols[1] - cols[0]
         self._register_params()
         self._init_fc()
+        if cols is not None:
+            self.batch_shard = (cols[0], cols[1], batch_size)
+            self.world = (rank, world)
         # the reference follows construction with model.cuda() (main_lena.py:191); do it here
         self.to(self.A.device)
 
@@ -103,7 +122,7 @@ class _DLADMMBase(nn.Module):
         place): it keeps only its contiguous column span c0:c1 = dist.shard_columns(batch_size,
         rank, world) of everything that is per sample -- Z0, E0, L0 and V1's per-sample betas
         (main_lena.py:35-36), which become (m, c1 - c0) Parameters holding their current values'
-        columns and are marked rank-local.  Then:
+        columns (rank-local: dist.rank_local_params finds them from the module).  Then:
           * forward / training_loss take the rank's (m, c1 - c0) shard of X; training_loss's
             mean runs over the global batch_size by default, so the ranks' gradients SUM to the
             whole batch's;
@@ -111,7 +130,8 @@ class _DLADMMBase(nn.Module):
             per-row ones): a per-sample beta's gradient is rank-local;
           * load_state_dict slices a global checkpoint's (m, batch_size) betas to the span, and
             dist.gather_state_dict assembles the reference layout again for saving.
-        Per rank, V1's betas then cost 2 K m (B / world) floats instead of 2 K m B.  Returns
+        Per rank, V1's betas then cost 2 K m (B / world) floats instead of 2 K m B (the global
+        betas exist until this call; the constructor's batch_shard= never makes them).  Returns
         self."""
         from .dist import shard_columns
         if self.batch_shard is not None:
@@ -126,10 +146,9 @@ class _DLADMMBase(nn.Module):
         self.L0 = self.L0[:, c0:c1].contiguous()
         for pl in self._elem_param_lists():
             for i in range(len(pl)):
-                p = nn.Parameter(pl[i].detach()[:, c0:c1].contiguous(),
-                                 requires_grad=pl[i].requires_grad)
-                p._dladmm_rank_local = True
-                pl[i] = p
+                pl[i] = nn.Parameter(pl[i].detach()[:, c0:c1].contiguous(),
+                                     requires_grad=pl[i].requires_grad)
+        self._pcols = c1 - c0
         self.batch_shard = (c0, c1, B)
         self.world = (rank, world)
         return self
@@ -400,6 +419,18 @@ class _DLADMMBase(nn.Module):
 
     def _shared_weight(self) -> bool:
         return isinstance(self.fc, nn.Linear)
+
+
+def _shard_cols(t: torch.Tensor, batch: int, cols, name: str) -> torch.Tensor:
+    """Rank's columns c0:c1 of a (rows, batch) initial-state tensor; a tensor that already has
+    c1 - c0 columns is the caller's shard and is taken as it is."""
+    c0, c1 = cols
+    if t.dim() == 2 and t.shape[1] == batch and c1 - c0 != batch:
+        return t[:, c0:c1].contiguous()
+    if t.dim() == 2 and t.shape[1] == c1 - c0:
+        return t
+    raise ValueError(f"dladmm: {name} of shape {tuple(t.shape)} is neither the global batch "
+                     f"({batch} columns) nor the shard's {c1 - c0}")
 
 
 def _slice_tables(tables: dict, nl: int) -> dict:
@@ -705,8 +736,9 @@ class DLADMMNet(_DLADMMBase):
         self.beta2 = nn.ParameterList()
         self.fc = nn.ModuleList()
         for _ in range(self.layers):
-            self.beta1.append(nn.Parameter(torch.ones(self.m, self.batch_size, dtype=torch.float32)))
-            self.beta2.append(nn.Parameter(torch.ones(self.m, self.batch_size, dtype=torch.float32)))
+            # (m, batch_size); a batch shard holds its own columns only (batch_shard=)
+            self.beta1.append(nn.Parameter(torch.ones(self.m, self._pcols, dtype=torch.float32)))
+            self.beta2.append(nn.Parameter(torch.ones(self.m, self._pcols, dtype=torch.float32)))
             self.fc.append(nn.Linear(self.m, self.d, bias=False))
         self.active_para = _dev(torch.tensor(0.025, dtype=torch.float32))
         self.active_para1 = _dev(torch.tensor(0.06, dtype=torch.float32))
@@ -782,8 +814,8 @@ class DLADMMNetScalar(_DLADMMBase):
                   "active_para": ("scalar", (_lib.P_THETA_Z,)),
                   "active_para1": ("scalar", (_lib.P_THETA_E,))}
 
-    def __init__(self, m, n, d, batch_size, A, Z0, E0, L0, layers):
-        super().__init__(m, n, d, batch_size, A, Z0, E0, L0, layers)
+    def __init__(self, m, n, d, batch_size, A, Z0, E0, L0, layers, **kw):
+        super().__init__(m, n, d, batch_size, A, Z0, E0, L0, layers, **kw)
         # main_syn_l1l1_scalar.py:41-48 attributes used by the (un-learned) KM iteration
         self.At = self.A.t()
         A_np = A.detach().cpu().numpy()
@@ -915,9 +947,9 @@ class DLADMMNetPTiedNewS(DLADMMNetTiedNewS):
     Constructor adds `interval` (:36)."""
     NAME = "DLADMMNet_scalar_ptied_newS_layerwise"
 
-    def __init__(self, m, n, d, batch_size, A, Z0, E0, L0, layers, interval):
+    def __init__(self, m, n, d, batch_size, A, Z0, E0, L0, layers, interval, **kw):
         self.interval = interval
-        super().__init__(m, n, d, batch_size, A, Z0, E0, L0, layers)
+        super().__init__(m, n, d, batch_size, A, Z0, E0, L0, layers, **kw)
 
     def _register_params(self):
         # :51-71: fc (layers // interval Linears) is registered after the ParameterLists

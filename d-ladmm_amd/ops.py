@@ -7,6 +7,8 @@ CPU tensors or a missing library raise.
 """
 from __future__ import annotations
 
+import contextlib
+import contextvars
 import ctypes
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
@@ -27,6 +29,31 @@ class ForwardResult:
     P: Optional[torch.Tensor] = None  # [K, m, B] A Z_k per layer (want_P: training forwards)
     path: int = 0  # dladmm_fwd_path: the kernel path that ran (1 fused, 2 per-layer, 3 bf16
                    # tiles, 4 fused split-f16; 0 = nothing launched)
+
+
+_PLAN_FLAGS = contextvars.ContextVar("dladmm_plan_flags", default=0)
+_FLAG_NAMES = {"per_layer": _lib.F_PER_LAYER, "bf16_wide": _lib.F_BF16_WIDE,
+               "bwd_per_layer": _lib.F_BWD_PER_LAYER, "bwd_unfused": _lib.F_BWD_UNFUSED,
+               "bwd_no_zmask": _lib.F_BWD_NO_ZMASK, "wgrad_f32": _lib.F_WGRAD_F32}
+
+
+@contextlib.contextmanager
+def plan_flags(**opts):
+    """Plan options (include/dladmm.h enum dladmm_flags) for every forward / backward call made
+    inside the block, e.g. `with plan_flags(per_layer=True): net(X)` runs the per-layer kernels
+    where the fused kernel would fit.  They select kernels, never arithmetic; the C ABI receives
+    them in dladmm_fwd_desc.flags (the library reads no environment).  Nested blocks add to the
+    enclosing block's flags; a False value clears that flag."""
+    flags = _PLAN_FLAGS.get()
+    for k, v in opts.items():
+        if k not in _FLAG_NAMES:
+            raise ValueError(f"dladmm: unknown plan flag {k!r} (one of {sorted(_FLAG_NAMES)})")
+        flags = (flags | _FLAG_NAMES[k]) if v else (flags & ~_FLAG_NAMES[k])
+    tok = _PLAN_FLAGS.set(flags)
+    try:
+        yield flags
+    finally:
+        _PLAN_FLAGS.reset(tok)
 
 
 def _f32_dev(t: torch.Tensor, name: str) -> torch.Tensor:
@@ -68,6 +95,7 @@ def _fill_fwd_desc(d, variant, X, A, W, Z0, E0, L0, scalar_params, row_params, b
             raise RuntimeError(f"dladmm: fc[{k}].weight must be ({n}, {m}) with a common stride")
     dev = X.device
     d.abi_version = _lib.ABI_VERSION
+    d.flags = _PLAN_FLAGS.get()
     d.variant, d.m, d.n, d.batch, d.layers = variant, m, n, B, K
     d.keep_all, d.loss_kind = int(bool(keep_all)), int(loss_kind)
     d.X, d.ld_x = X.data_ptr(), X.stride(0)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DLADMM_ABI_VERSION 5
+#define DLADMM_ABI_VERSION 6
 #define DLADMM_MAX_LAYERS 65536   /* K limit, every variant (e.g. the K=2000 KM ground-truth run) */
 
 /* Reference variants (class DLADMMNet of the named reference script). */
@@ -152,7 +152,10 @@ typedef struct dladmm_fwd_desc {
          for the MFMAs, fp32 accumulation, every elementwise update -- shrinks, E, dual L, T -- in
          fp32).  bf16 runs on the per-layer kernels (path 3). */
   int32_t precision;
-  int32_t pad1;
+  /* plan options, a bitwise OR of enum dladmm_flags (0 = the default plan).  They change which
+     kernels run -- never the arithmetic a kernel performs -- and the descriptor is the whole
+     input of the plan: the library reads no environment variable. */
+  int32_t flags;
 
   /* optional (training): P [K][m][ld_out] receives A Z_k of every layer, exactly the product the
      E/L/T updates consumed (main_syn_l1l1_scalar.py:114-117).  Written only on path 1 (fused
@@ -162,6 +165,21 @@ typedef struct dladmm_fwd_desc {
 } dladmm_fwd_desc;
 
 enum dladmm_precision { DLADMM_PREC_F32 = 0, DLADMM_PREC_BF16 = 1, DLADMM_PREC_F32_SPLIT = 2 };
+
+/* dladmm_fwd_desc.flags (also read from dladmm_bwd_desc.fwd.flags by the backward). */
+enum dladmm_flags {
+  DLADMM_F_PER_LAYER = 1,      /* forward: the per-layer kernel pair (path 2) even where the fused
+                                  kernel fits (equivalence tests, A/B timing)                      */
+  DLADMM_F_BF16_WIDE = 2,      /* bf16 tiles: 256-column tiles, one workgroup per CU (default: 128
+                                  columns, two per CU -- 2 % faster at BASELINE config 5)          */
+  DLADMM_F_BWD_PER_LAYER = 4,  /* backward: the per-layer kernels even where the reverse sweep
+                                  applies (dladmm_bwd_path 0)                                      */
+  DLADMM_F_BWD_UNFUSED = 8,    /* per-layer backward after a saved-product forward: BK1 as its own
+                                  launch instead of inside BK3's (bit-identical)                   */
+  DLADMM_F_BWD_NO_ZMASK = 16,  /* per-layer backward, V2 / V3: form q = W_k Var_k in BK2 instead of
+                                  reading the shrink masks off the saved Z_k                       */
+  DLADMM_F_WGRAD_F32 = 32      /* split-f16 backward: the weight gradient on the fp32-MFMA kernel  */
+};
 
 /* ABI version the library was built with. */
 int dladmm_abi_version(void);
@@ -196,10 +214,15 @@ int dladmm_fwd_f32(const dladmm_fwd_desc* d, void* stream);
  */
 typedef struct dladmm_bwd_desc {
   /* the forward's descriptor (keep_all, T, and P where it was saved).  fwd.precision:
-     DLADMM_PREC_F32, or DLADMM_PREC_F32_SPLIT after a split-f16 training forward -- then, with
-     whole 32-column chunks, the weight-gradient GEMM (gU_k Var_k^T over the batch) also runs on
-     the f16 matrix cores with exactly split operands (fp32 GEMM accuracy), on the reverse sweep
-     and on the per-layer backward alike; every other backward kernel is fp32 either way */
+     DLADMM_PREC_F32, or DLADMM_PREC_F32_SPLIT after a split-f16 training forward -- then the
+     weight-gradient GEMM (gU_k Var_k^T over the batch) also runs on the f16 matrix cores with
+     exactly split operands (any batch on the reverse sweep, whose operand columns are padded to
+     32; whole 32-column chunks on the per-layer backward, else the fp32 kernel), unless
+     fwd.flags holds DLADMM_F_WGRAD_F32; every other backward kernel is fp32 either way.
+     Accuracy: fp32-GEMM error relative to the largest product in each 64 x 64 block of gW --
+     the split scales are per wave, so a row of gU_k or Var_k more than ~2^17 below the largest
+     row of its 64-row block keeps fewer bits (measured within 1e-5 of the fp32 kernel per row
+     at a 2^20 spread; rows ~2^29 below contribute nothing) */
   dladmm_fwd_desc fwd;
 
   /* upstream cotangents: HOST arrays of device pointers, one per layer (gT: K+1), each a
@@ -249,8 +272,8 @@ size_t dladmm_bwd_workspace_bytes(const dladmm_bwd_desc* d);
        (layers + 1) * MP * NP * 4 + layers * (Rn + 2 * MP) * Bpad * 4 bytes (MP, NP: the
        instantiation's padded m, n; Rn = NP rounded up to 128; Bpad = batch rounded up to 16;
        V2 / V3 add 8 * layers * max(MP, NP) * (batch / 16, rounded up to 4) * 4 bytes of per-row
-       partials), stays under a quarter of the device memory (DLADMM_REV_WS_MAX_MB overrides);
-     - DLADMM_BWD_REV is not "0".
+       partials), stays under a quarter of the device memory;
+     - fwd.flags does not hold DLADMM_F_BWD_PER_LAYER.
    dladmm_bwd_workspace_bytes() reports the size of whichever path this returns. */
 int dladmm_bwd_path(const dladmm_bwd_desc* d);
 

@@ -57,6 +57,38 @@ def problems():
     return P
 
 
+class _PlanFlags:
+    """Plan options (include/dladmm.h dladmm_flags) for the rest of a test, the way
+    monkeypatch.setenv sets a variable: `flags.set(per_layer=True)` ... `flags.set(per_layer=False)`;
+    everything is undone at teardown (d-ladmm_amd.ops.plan_flags' context variable)."""
+
+    def __init__(self):
+        self.ops = importlib.import_module("d-ladmm_amd.ops")
+        self.first = None
+
+    def set(self, **opts):
+        var = self.ops._PLAN_FLAGS
+        cur = var.get()
+        for k, v in opts.items():
+            f = self.ops._FLAG_NAMES[k]
+            cur = (cur | f) if v else (cur & ~f)
+        tok = var.set(cur)
+        if self.first is None:
+            self.first = tok
+
+    def undo(self):
+        if self.first is not None:
+            self.ops._PLAN_FLAGS.reset(self.first)
+            self.first = None
+
+
+@pytest.fixture
+def flags():
+    f = _PlanFlags()
+    yield f
+    f.undo()
+
+
 def load_golden(name):
     g = np.load(os.path.join(GOLDEN, name + ".npz"))
     meta = json.loads(str(g["meta"]))

@@ -67,25 +67,37 @@ def test_self_launch_spawns_n_gloo_ranks():
     assert r["n_gpus"] == 3 and r["rank_sum"] == 3.0 and r["ranks"] == [0, 1, 2]
 
 
-def _fake_topology(root, gpus, cpus=1):
-    """A KFD topology tree: `cpus` CPU agents (simd_count 0), then `gpus` GPU agents."""
-    for i in range(cpus + gpus):
+def _fake_topology(root, gpus, cpus=1, hidden=0):
+    """A KFD topology tree: `cpus` CPU agents (simd_count 0), then `gpus` GPU agents whose render
+    nodes exist under root/dri, then `hidden` GPU agents of the host whose render nodes this
+    process cannot open (a container's view of the other GPUs)."""
+    (root / "dri").mkdir(parents=True)
+    for i in range(cpus + gpus + hidden):
         d = root / str(i)
         d.mkdir(parents=True)
         simd = 0 if i < cpus else 1024
-        (d / "properties").write_text(f"cpu_cores_count 8\nsimd_count {simd}\nmax_waves_per_simd 8\n")
+        minor = 128 + i
+        (d / "properties").write_text(f"cpu_cores_count 8\nsimd_count {simd}\n"
+                                      f"max_waves_per_simd 8\ndrm_render_minor {minor}\n")
+        if cpus <= i < cpus + gpus:
+            (root / "dri" / f"renderD{minor}").write_text("")
     return str(root)
 
 
 def test_visible_gpu_count_from_topology(tmp_path):
     b = _bench()
-    topo = _fake_topology(tmp_path / "nodes", gpus=8, cpus=2)
-    assert b.visible_gpu_count({}, kfd=topo) == 8
-    assert b.visible_gpu_count({"HIP_VISIBLE_DEVICES": "0,1,2"}, kfd=topo) == 3
+    topo = _fake_topology(tmp_path / "nodes", gpus=8, cpus=2, hidden=3)
+    dri = os.path.join(topo, "dri")
+    # the 3 host GPUs without an openable render node are not counted
+    assert b.visible_gpu_count({}, kfd=topo, dri=dri) == 8
+    assert b.visible_gpu_count({"HIP_VISIBLE_DEVICES": "0,1,2"}, kfd=topo, dri=dri) == 3
     assert b.visible_gpu_count({"ROCR_VISIBLE_DEVICES": "4", "HIP_VISIBLE_DEVICES": "0"},
-                               kfd=topo) == 1
-    assert b.visible_gpu_count({"CUDA_VISIBLE_DEVICES": ""}, kfd=topo) == 8
-    assert b.visible_gpu_count({}, kfd=str(tmp_path / "absent")) is None
+                               kfd=topo, dri=dri) == 1
+    assert b.visible_gpu_count({"CUDA_VISIBLE_DEVICES": ""}, kfd=topo, dri=dri) == 8
+    # "-1" hides every device; ids after an invalid one are ignored by the runtime
+    assert b.visible_gpu_count({"HIP_VISIBLE_DEVICES": "-1"}, kfd=topo, dri=dri) == 0
+    assert b.visible_gpu_count({"CUDA_VISIBLE_DEVICES": "0,-1,2"}, kfd=topo, dri=dri) == 1
+    assert b.visible_gpu_count({}, kfd=str(tmp_path / "absent"), dri=dri) is None
 
 
 # the launcher parent under test: every way torch could reach hipGetDeviceCount raises, so a

@@ -270,3 +270,112 @@ def test_gloo_world2_v1_beta_shard():
         assert gb == rank + 1.0      # not all-reduced: rank-local
         assert gw == 3.0             # all-reduced: 1 + 2
         assert same                  # gathered state_dict == the global checkpoint
+
+
+def _v1_ctor_shard_worker(rank, world, port, q):
+    """A V1 shard built by the constructor (batch_shard=(rank, world)): the betas never exist
+    at the global width; a DEEP COPY of the shard still keeps its betas out of the all-reduce
+    (rank-local parameters are found from the module, not from a Parameter attribute); the
+    gathered state_dict is the global checkpoint; gathering with a (rank, world) that does not
+    match the process group raises."""
+    import copy
+    import importlib
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    dl = importlib.import_module("d-ladmm_amd")
+    ddist = importlib.import_module("d-ladmm_amd.dist")
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m, n, B, K = 8, 16, 11, 3
+    g = torch.Generator().manual_seed(5)
+    A = torch.randn(m, n, generator=g)
+    Z0 = torch.rand(n, B, generator=g)
+    sd_full = None
+    torch.manual_seed(7)
+    net = dl.DLADMMNet(m=m, n=0, d=n, batch_size=B, A=A, Z0=Z0, E0=torch.zeros(m, B),
+                       L0=torch.zeros(m, B), layers=K, batch_shard=(rank, world))
+    c0, c1, Bg = net.batch_shard
+    shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+    z0_ok = torch.equal(net.Z0, Z0[:, c0:c1])
+    g2 = torch.Generator().manual_seed(11)
+    sd_full = {k: torch.randn((m, B) if k.startswith("beta") else v.shape, generator=g2)
+               for k, v in net.state_dict().items()}
+    net.load_state_dict(sd_full)            # the global checkpoint, sliced on load
+    dup = copy.deepcopy(net)
+    for p in dup.parameters():
+        p.grad = torch.full_like(p, float(rank + 1))
+    ddist.allreduce_grads(dup)              # uneven spans (6 and 5 columns): must not mix betas
+    gb = float(dup.beta1[0].grad.mean())
+    gw = float(dup.fc[0].weight.grad.mean())
+    same = all(torch.equal(v, sd_full[k]) for k, v in ddist.gather_state_dict(dup).items())
+    bad = copy.deepcopy(net)
+    bad.world = ((rank + 1) % world, world)
+    try:
+        ddist.gather_state_dict(bad)
+        raised = False
+    except RuntimeError:
+        raised = True
+    q.put((rank, (c0, c1, Bg), shapes, z0_ok, gb, gw, same, raised))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_v1_ctor_shard_and_deepcopy():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_v1_ctor_shard_worker, args=(r, world, port, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    m, n, K = 8, 16, 3
+    assert [r[1] for r in res] == [(0, 6, 11), (6, 11, 11)]
+    for rank, (c0, c1, _), shapes, z0_ok, gb, gw, same, raised in res:
+        for k in range(K):
+            assert shapes[f"beta1.{k}"] == (m, c1 - c0) == shapes[f"beta2.{k}"]
+        assert z0_ok
+        assert gb == rank + 1.0      # the deep copy's betas stayed rank-local
+        assert gw == 3.0             # replicated weights all-reduced: 1 + 2
+        assert same
+        assert raised
+
+
+def test_v1_ctor_shard_equals_shard_batch():
+    """batch_shard=(rank, world) builds exactly what the replicated constructor followed by
+    shard_batch_(rank, world) holds -- same keys, shapes, values (same RNG draws for W) -- and
+    accepts already-sliced Z0 / E0 / L0; a Z0 of neither width raises."""
+    import importlib
+    dl = importlib.import_module("d-ladmm_amd")
+    m, n, B, K = 8, 16, 11, 3
+    g = torch.Generator().manual_seed(3)
+    A, Z0 = torch.randn(m, n, generator=g), torch.rand(n, B, generator=g)
+    E0, L0 = torch.randn(m, B, generator=g), torch.randn(m, B, generator=g)
+    for rank in range(3):
+        torch.manual_seed(9)
+        a = dl.DLADMMNet(m=m, n=0, d=n, batch_size=B, A=A, Z0=Z0, E0=E0, L0=L0, layers=K)
+        a.shard_batch_(rank, 3)
+        torch.manual_seed(9)
+        b = dl.DLADMMNet(m=m, n=0, d=n, batch_size=B, A=A, Z0=Z0, E0=E0, L0=L0, layers=K,
+                         batch_shard=(rank, 3))
+        assert a.batch_shard == b.batch_shard and b.world == (rank, 3)
+        sa, sb = a.state_dict(), b.state_dict()
+        assert list(sa) == list(sb)
+        for k in sa:
+            assert torch.equal(sa[k], sb[k]), k
+        for t in ("Z0", "E0", "L0"):
+            assert torch.equal(getattr(a, t), getattr(b, t)), t
+        c0, c1, _ = b.batch_shard
+        torch.manual_seed(9)
+        c = dl.DLADMMNet(m=m, n=0, d=n, batch_size=B, A=A, Z0=Z0[:, c0:c1], E0=E0[:, c0:c1],
+                         L0=L0[:, c0:c1], layers=K, batch_shard=(rank, 3))
+        assert torch.equal(c.Z0, b.Z0)
+    with pytest.raises(ValueError):
+        dl.DLADMMNet(m=m, n=0, d=n, batch_size=B, A=A, Z0=Z0[:, :2], E0=E0, L0=L0, layers=K,
+                     batch_shard=(0, 3))

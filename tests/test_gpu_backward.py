@@ -5,20 +5,29 @@ reference's own autograd gradients and with the backward oracle.
   `total_loss.backward()` with the training loss of main_syn_l1l1_scalar.py:283-298 /
   main_syn_lasso_scalar.py:270-285 plus seeded linear terms on every output -- every variant;
   the loss is built here with torch ops on the GPU outputs, exactly as the reference loops do;
-* the same through the per-layer kernel path (DLADMM_PATH=layered);
+* the same through the per-layer kernel path (flags per_layer);
 * the oracle (oracle/dladmm_oracle_grad.py, pinned by those fixtures) at a larger ragged batch;
 * determinism (bitwise) and one full Adam training step.
+
+The golden-gradient and fused-objective tests run at both training precisions: "f32" (fp32 MFMA)
+and "f32_split" (the split-f16 forward that saves A Z_k, then the reverse sweep with the
+split-f16 weight gradient -- the bench's train.split_f16 leg), each against the reference
+autograd fixtures at the same GTOL.  Every checked error is logged (tests/parity.py) so a
+DLADMM_PARITY_JSON run records the margins.
 
 Tolerance: norm-relative per parameter <= max(GTOL, 3 x the reference's fp32-vs-fp64 gap of that
 gradient).  GTOL = 1e-4: the GPU forward sums its GEMMs in another order than CPU BLAS, and a
 shrink mask that flips on a near-threshold element moves a gradient by more than fp32 rounding
 (the reference's own fp64 twin shows the same effect: its gap column).
 """
+from importlib import import_module
+
 import numpy as np
 import pytest
 import torch
 
 from conftest import load_golden
+import parity
 import problems as P
 
 pytestmark = pytest.mark.gpu
@@ -33,7 +42,13 @@ def nrel(a, b):
     return float(np.linalg.norm(a - b) / nb) if nb > 0 else float(np.linalg.norm(a))
 
 
-def make_train_net(dl, variant, inp, sd, K, **extra):
+# variants whose fused forward has a split-f16 form (csrc/dladmm_fused_x3.hip: V4-V6 and the
+# newS schedules built on them); the others train f32 under "f32_split"
+SPLIT_VARIANTS = ("v4", "v5", "v6", "v7", "v7t", "v7p")
+PRECISIONS = ("f32", "f32_split")
+
+
+def make_train_net(dl, variant, inp, sd, K, precision="f32", **extra):
     m, n = inp["A"].shape
     B = inp["X"].shape[1]
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
@@ -41,7 +56,37 @@ def make_train_net(dl, variant, inp, sd, K, **extra):
                                E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K, **extra)
     net.load_state_dict({k: t(v) for k, v in sd.items()}, strict=True)
     net.requires_grad_(True)
+    net.precision = precision
     return net
+
+
+def split_expected(d) -> bool:
+    """Whether a "f32_split" training forward of problem d runs the split-f16 kernel (path 4):
+    split variants at the register-resident shapes with a batch that is a multiple of 4."""
+    return d["variant"] in SPLIT_VARIANTS and d["m"] <= 256 and d["n"] <= 512 and d["B"] % 4 == 0
+
+
+def record_paths(monkeypatch):
+    """The kernel path of every forward the model runs (ForwardResult.path), in call order."""
+    mod = import_module("d-ladmm_amd.model")
+    orig, paths = mod.dladmm_forward, []
+
+    def wrap(*a, **k):
+        r = orig(*a, **k)
+        paths.append(r.path)
+        return r
+    monkeypatch.setattr(mod, "dladmm_forward", wrap)
+    return paths
+
+
+def grad_cases(names):
+    """(fixture, precision) pairs: every fixture at f32, the split-f16 ones also at f32_split."""
+    out = []
+    for nm in names:
+        out.append((nm, "f32"))
+        if P.grad_defn(P.GRAD_FIXTURES[nm])["variant"] in SPLIT_VARIANTS:
+            out.append((nm, "f32_split"))
+    return out
 
 
 def total_loss(out, X, A, up, kind, K):
@@ -68,12 +113,13 @@ def total_loss(out, X, A, up, kind, K):
     return tot
 
 
-def run_grads(dl, name):
+def run_grads(dl, name, precision="f32"):
     g, meta = load_golden(name)
     d = meta["defn"]
     inp, sd = P.build_problem(d)
     up = P.make_upstream(d, P.VARIANT_SPECS[d["variant"]]["ret_t"])
-    net = make_train_net(dl, d["variant"], inp, sd, d["K"], **P.ctor_extra(d))
+    net = make_train_net(dl, d["variant"], inp, sd, d["K"], precision=precision,
+                         **P.ctor_extra(d))
     X = torch.from_numpy(inp["X"]).cuda()
     A = torch.from_numpy(inp["A"]).cuda()
     out = net(X)
@@ -94,7 +140,7 @@ def none_keys(name, which):
         return set(json.load(f)[name][which])
 
 
-def check_against_golden(g, meta, net):
+def check_against_golden(g, meta, net, path="f32"):
     got = {k: p.grad for k, p in net.named_parameters()}
     worst = {}
     none = none_keys(meta["name"], "fixture_loss")
@@ -104,24 +150,32 @@ def check_against_golden(g, meta, net):
             continue
         ref = g["g:" + key]
         e = nrel(got[key].detach().cpu().numpy(), ref)
-        tol = max(GTOL, 3.0 * float(g["gap:" + key]))
+        gap = float(g["gap:" + key])
+        tol = max(GTOL, 3.0 * gap)
         worst[key] = e
-        assert e <= tol, (key, e, tol)
+        parity.check(meta["name"] + " grad vs reference autograd", path, key, e, tol, gap)
     return worst
 
 
-@pytest.mark.parametrize("name", sorted(P.GRAD_FIXTURES))
-def test_grads_match_reference_autograd(name, dl):
-    g, meta, net, loss = run_grads(dl, name)
+@pytest.mark.parametrize("name,precision", grad_cases(sorted(P.GRAD_FIXTURES)))
+def test_grads_match_reference_autograd(name, precision, dl, monkeypatch):
+    """The reference's own autograd gradients (golden fixtures) at both training precisions;
+    under "f32_split" the forward must have run the split-f16 kernel wherever it applies (and
+    then the backward's weight gradient runs split-f16 too)."""
+    paths = record_paths(monkeypatch)
+    g, meta, net, loss = run_grads(dl, name, precision)
+    assert paths, "no forward ran"
+    if precision == "f32_split":
+        assert paths[0] == (4 if split_expected(meta["defn"]) else 1), paths
     np.testing.assert_allclose(loss, g["loss"][0], rtol=1e-4)
-    check_against_golden(g, meta, net)
+    check_against_golden(g, meta, net, path=precision)
 
 
 @pytest.mark.parametrize("name", ["grad_v4_med", "grad_v6_med", "grad_v1_med", "grad_v3_med",
                                   "grad_v5_small", "grad_v2_ragged"])
-def test_grads_layered_path(name, dl, monkeypatch):
+def test_grads_layered_path(name, dl, flags):
     """Forward and backward both on the per-layer kernels (the path of m > 256 / n > 512)."""
-    monkeypatch.setenv("DLADMM_PATH", "layered")
+    flags.set(per_layer=True)
     g, meta, net, _ = run_grads(dl, name)
     check_against_golden(g, meta, net)
 
@@ -191,12 +245,14 @@ def test_adam_training_step(dl):
                                    rtol=0, atol=1e-6, err_msg=k)
 
 
-@pytest.mark.parametrize("name", ["grad_v4_med", "grad_v6_med", "grad_v1_small", "grad_v2_ragged",
-                                  "grad_v5_small", "grad_v3_small"])
-def test_fused_training_loss(name, dl):
+@pytest.mark.parametrize("name,precision", grad_cases(
+    ["grad_v4_med", "grad_v6_med", "grad_v1_small", "grad_v2_ragged", "grad_v5_small",
+     "grad_v3_small"]))
+def test_fused_training_loss(name, precision, dl, monkeypatch):
     """net.training_loss (objective reduced in the forward kernel, its gradient injected in the
     backward kernels) == the reference loss built from the outputs with torch ops: same value,
-    same gradients (against the oracle's reverse sweep of the same loss)."""
+    same gradients (against the oracle's reverse sweep of the same loss and against reference
+    autograd through the module's outputs), at both training precisions."""
     from oracle import dladmm_oracle as fwd
     from oracle import dladmm_oracle_grad as og
     g, meta = load_golden(name)
@@ -207,9 +263,12 @@ def test_fused_training_loss(name, dl):
     X = torch.from_numpy(inp["X"]).cuda()
     A = torch.from_numpy(inp["A"]).cuda()
     coeffs = P.loss_coeffs(K)
-    net = make_train_net(dl, d["variant"], inp, sd, K, **P.ctor_extra(d))
+    paths = record_paths(monkeypatch)
+    net = make_train_net(dl, d["variant"], inp, sd, K, precision=precision, **P.ctor_extra(d))
     total, per_layer = net.training_loss(X, P.GRAD_ALPHA, coeffs, kind)
     total.backward()
+    if precision == "f32_split":
+        assert paths[0] == (4 if split_expected(d) else 1), paths
     net2 = make_train_net(dl, d["variant"], inp, sd, K, **P.ctor_extra(d))
     ref_total = total_loss(net2(X), X, A, {"Gz": np.zeros((K, 1, 1), np.float32),
                                           "Ge": np.zeros((K, 1, 1), np.float32),
@@ -236,17 +295,19 @@ def test_fused_training_loss(name, dl):
             continue
         gap = nrel(res[np.float32][key], res[np.float64][key])
         e = nrel(p.grad.cpu().numpy(), res[np.float64][key])
-        assert e <= max(GTOL, 3.0 * gap), (key, e, gap)
+        parity.check(name + " fused objective grad vs oracle64", precision, key, e,
+                     max(GTOL, 3.0 * gap), gap)
         e2 = nrel(p.grad.cpu().numpy(), p2[key].grad.cpu().numpy())
-        assert e2 <= max(GTOL, 3.0 * gap), (key, e2, gap)
+        parity.check(name + " fused objective grad vs torch-op loss", precision, key, e2,
+                     max(GTOL, 3.0 * gap), gap)
 
 
 @pytest.mark.parametrize("variant", ["v4", "v1", "v2", "v3", "v5", "v6"])
 @pytest.mark.parametrize("lossy", [False, True])
-def test_saved_product_backward(variant, lossy, dl, monkeypatch):
+def test_saved_product_backward(variant, lossy, dl, flags):
     """A training forward on the fused kernel keeps P_k = A Z_k (fwd_desc.P) and BK1 reads it
     instead of recomputing the product, inside BK3's launch (phase 6).
-      (a) phase 6 == BK1 as its own launch (DLADMM_BWD_UNFUSED=1): every elementwise adjoint,
+      (a) phase 6 == BK1 as its own launch (flags bwd_unfused): every elementwise adjoint,
           the weight and the per-sample gradients bit for bit, the parameter-slot sums to their
           fp32 partials' rounding (the partials group the terms by wave differently);
       (b) the saved P is A Z_k of the returned Z_k, and storing it changes no other output;
@@ -286,9 +347,9 @@ def test_saved_product_backward(variant, lossy, dl, monkeypatch):
     if lossy:
         kw.update(loss_kind=lk, loss_coef=torch.tensor([[1e-3, 1.0]] * K, device="cuda"))
     fused = ops.dladmm_backward(*args, r1, gz, ge, gl, gt, **kw)
-    monkeypatch.setenv("DLADMM_BWD_UNFUSED", "1")
+    flags.set(bwd_unfused=True)
     unfused = ops.dladmm_backward(*args, r1, gz, ge, gl, gt, **kw)
-    monkeypatch.delenv("DLADMM_BWD_UNFUSED")
+    flags.set(bwd_unfused=False)
     recomp = ops.dladmm_backward(*args, r0, gz, ge, gl, gt, **kw)
     for other, exact in ((unfused, True), (recomp, False)):
         for f in ("gW", "g_scalar", "g_row"):

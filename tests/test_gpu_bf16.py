@@ -27,10 +27,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True, params=["wide", "narrow"])
-def tile(request, monkeypatch):
+def tile(request, flags):
     """Every test runs on both tile widths (256 columns / 8 waves, 128 columns / 4 waves with
-    two workgroups per CU; DLADMM_BF16_TILE is read by the C ABI at every call)."""
-    monkeypatch.setenv("DLADMM_BF16_TILE", request.param)
+    two workgroups per CU; plan flag bf16_wide, i.e. DLADMM_F_BF16_WIDE in the descriptor)."""
+    flags.set(bf16_wide=request.param == "wide")
     return request.param
 
 
@@ -151,7 +151,7 @@ def test_bf16_loss_lean_and_determinism(dl):
         assert abs(ls[k, 1] - np.abs(res).sum()) <= 1e-4 * np.abs(res).sum(), k
 
 
-def test_bf16_tile_widths_bit_identical(dl, monkeypatch):
+def test_bf16_tile_widths_bit_identical(dl, flags):
     """Both tile widths compute every output element as the same chain (k-blocks in order, same
     packed operands, same epilogue code): the outputs and fused sums are bitwise equal."""
     m, n, B, K = 300, 530, 600, 3
@@ -167,7 +167,7 @@ def test_bf16_tile_widths_bit_identical(dl, monkeypatch):
     X = t(inp["X"]).cuda()
     res = {}
     for wd in ("wide", "narrow"):
-        monkeypatch.setenv("DLADMM_BF16_TILE", wd)
+        flags.set(bf16_wide=wd == "wide")
         with torch.no_grad():
             res[wd] = net.run(X, keep_all=True, loss_kind=1)
     a, b = res["wide"], res["narrow"]
@@ -175,123 +175,6 @@ def test_bf16_tile_widths_bit_identical(dl, monkeypatch):
         assert torch.equal(x, y)
     # the per-column partials are summed in a fixed order per slot; the slot layout is the same
     np.testing.assert_allclose(a.loss_sums.cpu().numpy(), b.loss_sums.cpu().numpy(), rtol=1e-6)
-
-
-@pytest.mark.parametrize("variant", ["v1", "v2", "v3", "v4", "v5", "v6"])
-def test_bf16_paired_halves_bit_identical(variant, dl, monkeypatch):
-    """Two column halves one phase apart per launch (dladmm_tile_bf16_pair.hip) compute every tile
-    with the one-phase kernel's code: outputs, lean outputs and fused sums are bitwise those of
-    one phase per launch (DLADMM_BF16_PAIR=0), for an even interleave and for the long tiles
-    front-loaded (DLADMM_BF16_PAIR_F), at a ragged batch of 5 narrow column tiles (halves of
-    3 and 2) and at 2."""
-    monkeypatch.setenv("DLADMM_BF16_TILE", "narrow")
-    m, n, K = 300, 530, 3
-    for B in (600, 200):
-        inp = P.make_inputs(m, n, B, 9311)
-        sd = P.make_state_dict(variant, m, n, B, K, inp["A"], 9311, perturb=0.1,
-                               wscale=P.VARIANT_SPECS[variant]["wscale"])
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
-        net = dl.VARIANTS[variant](m=m, n=0, d=n, batch_size=B, A=t(inp["A"]),
-                                   Z0=t(inp["Z0"]), E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K)
-        net.load_state_dict({k: t(v) for k, v in sd.items()})
-        net.requires_grad_(False)
-        net.cuda()
-        net.precision = "bf16"
-        X = t(inp["X"]).cuda()
-        res = {}
-        for mode, f in (("0", "1000"), ("1", "1000"), ("1", "400")):
-            monkeypatch.setenv("DLADMM_BF16_PAIR", mode)
-            monkeypatch.setenv("DLADMM_BF16_PAIR_F", f)
-            with torch.no_grad():
-                full = net.run(X, keep_all=True, loss_kind=1)
-                lean = net.run(X, keep_all=False, loss_kind=1)
-            res[(mode, f)] = (full, lean)
-        ref = res[("0", "1000")]
-        for key in (("1", "1000"), ("1", "400")):
-            for r0, r1 in zip(ref, res[key]):
-                for x, y in ((r0.Z, r1.Z), (r0.E, r1.E), (r0.L, r1.L), (r0.T, r1.T)):
-                    if x is not None:
-                        assert torch.equal(x, y), (variant, B, key)
-                assert torch.equal(r0.loss_sums, r1.loss_sums), (variant, B, key)
-
-
-@pytest.mark.parametrize("variant,grid", [("v4", "0"), ("v4", "3"), ("v1", "5"), ("v2", "2"),
-                                          ("v3", "4"), ("v5", "3"), ("v6", "3")])
-def test_bf16_pipelined_g1_bit_identical(variant, grid, dl, monkeypatch):
-    """G1 on the persistent pipelined kernel (dladmm_tile_bf16_pipe.hip: m = 993 .. 1024, the
-    epilogue of tile i - 1 inside the main loop of tile i) computes every element with the
-    one-phase kernel's expressions: Z/E/L/T (full and lean) bitwise equal to DLADMM_BF16_PIPE=0;
-    the fused objective sums within fp32 rounding (the pipelined waves sum 64 rows per partial,
-    the one-phase ones 128).  DLADMM_PIPE_GRID caps the persistent grid so each workgroup runs
-    several tiles (the pipelined path proper) on a small problem: a ragged batch (7 column
-    tiles, the last partial) and n = 530 (3 row tiles, the last partial)."""
-    monkeypatch.setenv("DLADMM_BF16_TILE", "narrow")
-    if grid != "0":
-        monkeypatch.setenv("DLADMM_PIPE_GRID", grid)
-    m, n, B, K = 1000, 530, 850, 3
-    inp = P.make_inputs(m, n, B, 9321)
-    sd = P.make_state_dict(variant, m, n, B, K, inp["A"], 9321, perturb=0.1,
-                           wscale=P.VARIANT_SPECS[variant]["wscale"])
-    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
-    net = dl.VARIANTS[variant](m=m, n=0, d=n, batch_size=B, A=t(inp["A"]), Z0=t(inp["Z0"]),
-                               E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K)
-    net.load_state_dict({k: t(v) for k, v in sd.items()})
-    net.requires_grad_(False)
-    net.cuda()
-    net.precision = "bf16"
-    X = t(inp["X"]).cuda()
-    res = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("DLADMM_BF16_PIPE", mode)
-        with torch.no_grad():
-            res[mode] = (net.run(X, keep_all=True, loss_kind=1),
-                         net.run(X, keep_all=False, loss_kind=1))
-    for r0, r1 in zip(res["0"], res["1"]):
-        for x, y in ((r0.Z, r1.Z), (r0.E, r1.E), (r0.L, r1.L), (r0.T, r1.T)):
-            if x is not None:
-                assert torch.equal(x, y), variant
-        np.testing.assert_allclose(r1.loss_sums.cpu().numpy(), r0.loss_sums.cpu().numpy(),
-                                   rtol=1e-6)
-
-
-@pytest.mark.parametrize("variant,grid,lags", [("v4", "0", "2"), ("v4", "3", "1"), ("v4", "5", "3"),
-                                               ("v1", "7", "2"), ("v2", "4", "2"), ("v3", "0", "2"),
-                                               ("v5", "9", "2"), ("v6", "2", "2")])
-def test_bf16_queue_bit_identical(variant, grid, lags, dl, monkeypatch):
-    """The whole bf16 forward as one persistent launch pulling tile units from per-XCD queues
-    in dependency order (dladmm_tile_bf16_queue.hip, DLADMM_BF16_QUEUE=1): every unit is the
-    wide one-phase tile body, so Z/E/L/T (full and lean) and the fused sums are bitwise those of
-    one launch per product.  DLADMM_PIPE_GRID caps the persistent grid (workgroups serve other
-    XCDs' queues and run many units each); lags 1..3 order the tickets along different diagonals;
-    ragged batches of 4 and 11 column tiles."""
-    if grid != "0":
-        monkeypatch.setenv("DLADMM_PIPE_GRID", grid)
-    monkeypatch.setenv("DLADMM_BF16_QUEUE_LAGS", lags)
-    m, n, K = 300, 530, 3
-    for B in (850, 2600):
-        inp = P.make_inputs(m, n, B, 9331)
-        sd = P.make_state_dict(variant, m, n, B, K, inp["A"], 9331, perturb=0.1,
-                               wscale=P.VARIANT_SPECS[variant]["wscale"])
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
-        net = dl.VARIANTS[variant](m=m, n=0, d=n, batch_size=B, A=t(inp["A"]), Z0=t(inp["Z0"]),
-                                   E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K)
-        net.load_state_dict({k: t(v) for k, v in sd.items()})
-        net.requires_grad_(False)
-        net.cuda()
-        net.precision = "bf16"
-        X = t(inp["X"]).cuda()
-        res = {}
-        for mode in ("0", "1"):
-            monkeypatch.setenv("DLADMM_BF16_QUEUE", mode)
-            with torch.no_grad():
-                res[mode] = (net.run(X, keep_all=True, loss_kind=1),
-                             net.run(X, keep_all=False, loss_kind=1))
-            torch.cuda.synchronize()
-        for r0, r1 in zip(res["0"], res["1"]):
-            for x, y in ((r0.Z, r1.Z), (r0.E, r1.E), (r0.L, r1.L), (r0.T, r1.T)):
-                if x is not None:
-                    assert torch.equal(x, y), (variant, B)
-            assert torch.equal(r0.loss_sums, r1.loss_sums), (variant, B)
 
 
 @pytest.mark.parametrize("name", sorted(P.BF16_FIXTURES))

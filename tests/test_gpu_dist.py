@@ -122,3 +122,54 @@ def test_two_ranks_gloo_forward_and_training(dl):
     for key in res[0][2]:
         if res[0][2][key] is not None:
             np.testing.assert_array_equal(res[0][2][key], res[1][2][key])
+
+
+def test_v1_ctor_shard_device_memory(dl):
+    """SURVEY 8(e) at BASELINE config 3's scale: a V1 model (main_lena.py:16-49) over
+    B = 262,144 columns, K = 15, built as rank 0 of 8 with batch_shard=(0, 8), holds 1/8 of the
+    replicated module's per-sample betas on the device -- the global 2 K m B betas (8 GB) never
+    reach the GPU -- and its forward equals the replicated module's on the same columns."""
+    m, n, Bg, Kd, world = 256, 512, 262144, 15, 8
+    g = torch.Generator().manual_seed(17)
+    A = torch.randn(m, n, generator=g)
+    A = A / A.pow(2).sum(0, keepdim=True).sqrt()
+    Z0 = torch.rand(n, Bg, generator=g) / n
+    E0, L0 = torch.zeros(m, Bg), torch.zeros(m, Bg)
+    peaks = {}
+    for mode in ("replicated", "shard"):
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        base = torch.cuda.memory_allocated()
+        torch.cuda.reset_peak_memory_stats()
+        torch.manual_seed(5)
+        kw = {} if mode == "replicated" else {"batch_shard": (0, world)}
+        net = dl.DLADMMNet(m=m, n=0, d=n, batch_size=Bg, A=A, Z0=Z0, E0=E0, L0=L0, layers=Kd,
+                           **kw)
+        torch.cuda.synchronize()
+        peaks[mode] = torch.cuda.max_memory_allocated() - base
+        if mode == "replicated":
+            net.requires_grad_(False)
+            c0, c1 = dl.dist.shard_columns(Bg, 0, world)
+            Xs = torch.randn(m, c1 - c0, generator=g).cuda()
+            sub = {k: v[:, c0:c1].contiguous() if k.startswith("beta") else v
+                   for k, v in net.state_dict().items()}
+            del net
+        else:
+            net.requires_grad_(False)
+            shard_net = net
+    betas = 2 * Kd * m * Bg * 4
+    assert peaks["replicated"] >= betas
+    # the shard: its betas and initial state (1/8), the replicated weights (K n m) and A
+    small = (Kd + 1) * m * n * 4
+    assert peaks["shard"] <= peaks["replicated"] / world + small + (1 << 20), peaks
+    # same forward as the replicated parameters restricted to the shard's columns
+    torch.manual_seed(5)
+    c0, c1, _ = shard_net.batch_shard
+    one = dl.DLADMMNet(m=m, n=0, d=n, batch_size=c1 - c0, A=A, Z0=Z0[:, c0:c1].contiguous(),
+                       E0=E0[:, c0:c1].contiguous(), L0=L0[:, c0:c1].contiguous(), layers=Kd)
+    one.load_state_dict(sub)
+    one.requires_grad_(False)
+    with torch.no_grad():
+        a = shard_net.run(Xs, keep_all=False, loss_kind=1)
+        b = one.run(Xs, keep_all=False, loss_kind=1)
+    assert torch.equal(a.Z, b.Z) and torch.equal(a.L, b.L)

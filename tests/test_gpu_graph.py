@@ -29,13 +29,13 @@ def capture(net, x_static, **run_kw):
 
 
 @pytest.mark.parametrize("path", ["fused", "layered", "f32_split", "bf16"])
-def test_graph_replay_equals_eager(path, dl, monkeypatch):
+def test_graph_replay_equals_eager(path, dl, flags):
     m, n, B, K = 256, 512, 640, 6
     inp = P.make_inputs(m, n, B, 7101)
     inp2 = P.make_inputs(m, n, B, 7102)
     sd = P.make_state_dict("v4", m, n, B, K, inp["A"], 7101, perturb=0.1)
     if path == "layered":
-        monkeypatch.setenv("DLADMM_PATH", "layered")
+        flags.set(per_layer=True)
     net = make_net(dl, "v4", inp, sd, K).cuda()
     if path in ("f32_split", "bf16"):
         net.precision = path
@@ -96,10 +96,10 @@ def test_graph_replay_v1_beta_tables(K, dl):
             assert torch.equal(a, b), f"V1 K={K}: {nm} of the replayed graph differs from eager"
 
 
-def test_graph_replay_launch_heavy_path(dl, monkeypatch):
+def test_graph_replay_launch_heavy_path(dl, flags):
     """The per-layer path at a launch-heavy depth (V6, K = 40: 81 launches) replays from a graph
     with the eager results (timing is not asserted: on a shared box it is noise-bound)."""
-    monkeypatch.setenv("DLADMM_PATH", "layered")
+    flags.set(per_layer=True)
     m, n, B, K = 64, 256, 64, 40
     inp = P.make_inputs(m, n, B, 7201)
     sd = P.make_state_dict("v6", m, n, B, K, inp["A"], 7201, perturb=0.1)

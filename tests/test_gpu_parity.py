@@ -56,15 +56,15 @@ def test_matches_reference_golden(name, dl):
 
 
 @pytest.mark.parametrize("name", sorted(P.FIXTURES))
-def test_per_layer_path_matches_reference_golden(name, dl, monkeypatch):
-    """The same fixtures through the per-layer kernel pairs (DLADMM_PATH=layered: the path of
+def test_per_layer_path_matches_reference_golden(name, dl, flags):
+    """The same fixtures through the per-layer kernel pairs (flags per_layer: the path of
     every shape beyond the fused kernel's, e.g. BASELINE config 4)."""
     g, meta = load_golden(name)
     d = meta["defn"]
     inp, sd = P.build_problem(d)
     net = make_net(dl, d["variant"], inp, sd, d["K"], **P.ctor_extra(d))
     X = torch.from_numpy(inp["X"]).cuda()
-    monkeypatch.setenv("DLADMM_PATH", "layered")
+    flags.set(per_layer=True)
     with torch.no_grad():
         out = net(X)
     check_golden(name, g, meta, net, X, out, path="layered")
@@ -286,8 +286,8 @@ def test_per_layer_path_vs_oracle(variant, dl, oracle):
 
 
 @pytest.mark.parametrize("variant", ["v4", "v1", "v6"])
-def test_forced_per_layer_path_matches_fused(variant, dl, monkeypatch):
-    """The same problem through both paths (DLADMM_PATH=layered forces path 2): outputs agree
+def test_forced_per_layer_path_matches_fused(variant, dl, flags):
+    """The same problem through both paths (flags per_layer forces path 2): outputs agree
     to fp32 summation-order noise, the lean mode and the fused objective too."""
     m, n, B, K = 256, 512, 333, 5
     inp = P.make_inputs(m, n, B, 9100)
@@ -296,10 +296,10 @@ def test_forced_per_layer_path_matches_fused(variant, dl, monkeypatch):
     X = torch.from_numpy(inp["X"]).cuda()
     with torch.no_grad():
         rf, of = net.layer_objectives(X, 0.001, "l1l1")
-        monkeypatch.setenv("DLADMM_PATH", "layered")
+        flags.set(per_layer=True)
         rl, ol = net.layer_objectives(X, 0.001, "l1l1")
         lean = net.run(X, keep_all=False)
-        monkeypatch.delenv("DLADMM_PATH")
+        flags.set(per_layer=False)
     for a, b in ((rf.Z, rl.Z), (rf.E, rl.E), (rf.L, rl.L)):
         for k in range(K):
             assert nrel(b[k].cpu().numpy(), a[k].cpu().numpy()) <= 2e-6
@@ -386,14 +386,14 @@ def test_empty_batch(variant, dl, oracle):
 
 
 @pytest.mark.parametrize("layered", [False, True])
-def test_v1_deeper_than_64_layers(layered, dl, oracle, monkeypatch):
+def test_v1_deeper_than_64_layers(layered, dl, oracle, flags):
     """The reference V1 ctor has no depth limit (main_lena.py:30-41): the fused kernel reads the
     per-layer beta pointers from a device table, so K = 80 runs (both paths)."""
     m, n, B, K = 16, 32, 24, 80
     inp, sd, ref = _oracle_case(oracle, "v1", m, n, B, K, seed=9400, wscale=0.4)
     net = make_net(dl, "v1", inp, sd, K)
     if layered:
-        monkeypatch.setenv("DLADMM_PATH", "layered")
+        flags.set(per_layer=True)
     with torch.no_grad():
         out = net(torch.from_numpy(inp["X"]).cuda())
     assert len(out[0]) == K

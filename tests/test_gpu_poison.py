@@ -21,13 +21,13 @@ def poison(shapes, ws_bytes):
 
 
 @pytest.mark.parametrize("path", ["fused", "layered", "f32_split", "bf16"])
-def test_outputs_from_poisoned_memory(path, dl, monkeypatch):
+def test_outputs_from_poisoned_memory(path, dl, flags):
     m, n, B, K = 256, 512, 640, 6
     inp = P.make_inputs(m, n, B, 7301)
     inp2 = P.make_inputs(m, n, B, 7302)
     sd = P.make_state_dict("v4", m, n, B, K, inp["A"], 7301, perturb=0.1)
     if path == "layered":
-        monkeypatch.setenv("DLADMM_PATH", "layered")
+        flags.set(per_layer=True)
     net = make_net(dl, "v4", inp, sd, K).cuda()
     if path in ("f32_split", "bf16"):
         net.precision = path

@@ -1,5 +1,5 @@
 """The backward as one reverse-sweep kernel (csrc/dladmm_reverse.hip, dladmm_bwd_path() == 1)
-against the per-layer backward kernels (DLADMM_BWD_REV=0), on the same saved forward.
+against the per-layer backward kernels (flags bwd_per_layer), on the same saved forward.
 
 The reverse kernel forms every product as the per-layer kernels do (one fma chain per output
 block, k in the same order) and every elementwise adjoint with the same expressions, so
@@ -42,7 +42,7 @@ def saved_forward(dl, variant, m, n, B, K, seed, negtheta=False, lk=0):
     return ops, args, r, tables
 
 
-def both(dl, variant, m, n, B, K, seed, kind, monkeypatch, negtheta=False):
+def both(dl, variant, m, n, B, K, seed, kind, flags, negtheta=False):
     lk = dl._lib.LOSS_LASSO if kind == "lasso" else dl._lib.LOSS_L1L1
     ops, args, r, tables = saved_forward(dl, variant, m, n, B, K, seed, negtheta, lk)
     g = torch.Generator(device="cuda").manual_seed(seed)
@@ -50,9 +50,9 @@ def both(dl, variant, m, n, B, K, seed, kind, monkeypatch, negtheta=False):
                                                                            device="cuda")).contiguous()
     kw = dict(loss_kind=lk, loss_coef=coef, **tables)
     rev = ops.dladmm_backward(*args, r, **kw)
-    monkeypatch.setenv("DLADMM_BWD_REV", "0")
+    flags.set(bwd_per_layer=True)
     per = ops.dladmm_backward(*args, r, **kw)
-    monkeypatch.delenv("DLADMM_BWD_REV")
+    flags.set(bwd_per_layer=False)
     return rev, per
 
 
@@ -74,24 +74,24 @@ def check_equal(rev, per, K):
 @pytest.mark.parametrize("variant,kind", [("v4", "l1l1"), ("v4", "lasso"), ("v6", "lasso")])
 @pytest.mark.parametrize("shape", [(20, 30, 70, 3), (64, 200, 333, 2), (250, 500, 200, 4),
                                    (256, 512, 64, 1)])
-def test_reverse_matches_per_layer(variant, kind, shape, dl, monkeypatch):
+def test_reverse_matches_per_layer(variant, kind, shape, dl, flags):
     m, n, B, K = shape
-    rev, per = both(dl, variant, m, n, B, K, 9700 + m, kind, monkeypatch)
+    rev, per = both(dl, variant, m, n, B, K, 9700 + m, kind, flags)
     check_equal(rev, per, K)
 
 
 @pytest.mark.parametrize("variant", ["v4", "v6"])
-def test_reverse_negative_thresholds(variant, dl, monkeypatch):
+def test_reverse_negative_thresholds(variant, dl, flags):
     """theta_z, theta_e < 0 on every other layer: both relus open where |U| < |theta|; the
     reverse kernel reads S'(U) off the saved Z_k (|Z| < 2|theta| there), the per-layer kernels
     recompute U = Z_{k-1} - W_k Var_k (phase 2)."""
-    rev, per = both(dl, variant, 96, 200, 150, 4, 9800, "l1l1", monkeypatch, negtheta=True)
+    rev, per = both(dl, variant, 96, 200, 150, 4, 9800, "l1l1", flags, negtheta=True)
     check_equal(rev, per, 4)
 
 
-def test_reverse_headline_shape_columns(dl, monkeypatch):
+def test_reverse_headline_shape_columns(dl, flags):
     """The training bench's shape (V4, m=256, n=512, K=15) at 4,096 columns (64 workgroups)."""
-    rev, per = both(dl, "v4", 256, 512, 4096, 15, 9900, "l1l1", monkeypatch)
+    rev, per = both(dl, "v4", 256, 512, 4096, 15, 9900, "l1l1", flags)
     check_equal(rev, per, 15)
 
 
@@ -105,7 +105,7 @@ def test_reverse_deterministic(dl):
     assert torch.equal(a.gW, b.gW) and torch.equal(a.g_scalar, b.g_scalar)
 
 
-def test_z_cotangents_on_the_reverse_sweep(dl, monkeypatch):
+def test_z_cotangents_on_the_reverse_sweep(dl, flags):
     """A torch-op loss over the returned Z_k (the reference's own training loop) hands the
     backward per-layer Z cotangents only: the reverse sweep adds them where the per-layer BK2
     does ((adjoint + gZ_k) + A^T gP), so both paths agree bit for bit on the weight gradients;
@@ -117,9 +117,9 @@ def test_z_cotangents_on_the_reverse_sweep(dl, monkeypatch):
     coef = torch.tensor([[1e-3, 1.0]] * 3, device="cuda")
     kw = dict(loss_kind=dl._lib.LOSS_L1L1, loss_coef=coef, **tables)
     rev = ops.dladmm_backward(*args, r, gz, **kw)
-    monkeypatch.setenv("DLADMM_BWD_REV", "0")
+    flags.set(bwd_per_layer=True)
     per = ops.dladmm_backward(*args, r, gz, **kw)
-    monkeypatch.delenv("DLADMM_BWD_REV")
+    flags.set(bwd_per_layer=False)
     check_equal(rev, per, 3)
 
 
@@ -139,7 +139,7 @@ def _cotangents(m, n, B, K, seed, which):
     return out
 
 
-def both_cot(dl, variant, m, n, B, K, seed, monkeypatch, which, fused_loss):
+def both_cot(dl, variant, m, n, B, K, seed, flags, which, fused_loss):
     lk = dl._lib.LOSS_L1L1 if fused_loss else 0
     ops, args, r, tables = saved_forward(dl, variant, m, n, B, K, seed, lk=lk)
     c = _cotangents(m, n, B, K, seed + 1, which)
@@ -150,21 +150,21 @@ def both_cot(dl, variant, m, n, B, K, seed, monkeypatch, which, fused_loss):
                                            torch.tensor([1e-2, 1.0], device="cuda")).contiguous())
     cots = (c["Z"], c["E"], c["L"], c["T"])
     rev = ops.dladmm_backward(*args, r, *cots, **kw)
-    monkeypatch.setenv("DLADMM_BWD_REV", "0")
+    flags.set(bwd_per_layer=True)
     per = ops.dladmm_backward(*args, r, *cots, **kw)
-    monkeypatch.delenv("DLADMM_BWD_REV")
+    flags.set(bwd_per_layer=False)
     return rev, per
 
 
 @pytest.mark.parametrize("variant", ["v4", "v6"])
 @pytest.mark.parametrize("shape", [(20, 30, 70, 3), (250, 500, 200, 4)])
-def test_elt_cotangents_on_the_reverse_sweep(variant, shape, dl, monkeypatch):
+def test_elt_cotangents_on_the_reverse_sweep(variant, shape, dl, flags):
     """Cotangents of E_k, L_k and T_k (a loss over every returned list) join the sweep in round
     4: added to the incoming adjoints of BK1 where the per-layer kernels add them, so the two
     paths agree bit for bit on the weight gradients (with the fused objective too)."""
     m, n, B, K = shape
     for which, fused in (("ZELT", False), ("ELT", True), ("L", False)):
-        rev, per = both_cot(dl, variant, m, n, B, K, 9970 + m, monkeypatch, which, fused)
+        rev, per = both_cot(dl, variant, m, n, B, K, 9970 + m, flags, which, fused)
         check_equal(rev, per, K)
 
 
@@ -180,7 +180,7 @@ def check_equal_v1(rev, per, K):
 @pytest.mark.parametrize("shape", [(20, 30, 70, 3), (64, 200, 333, 2), (250, 500, 200, 4),
                                    (256, 512, 64, 1)])
 @pytest.mark.parametrize("loss", ["lena", "fused", "zonly"])
-def test_reverse_v1_matches_per_layer(shape, loss, dl, monkeypatch):
+def test_reverse_v1_matches_per_layer(shape, loss, dl, flags):
     """V1 (main_lena.py:57-98, per-sample betas) on the reverse sweep: its betas and their
     gradients are per-element operands of the G2' rows; beta1's gradient sums BK1's term (one
     pass) and BK3's (the next) in the per-layer sweep's order.  Losses: main_lena.py:221-228's
@@ -188,19 +188,19 @@ def test_reverse_v1_matches_per_layer(shape, loss, dl, monkeypatch):
     beta gradients equal the per-layer path's bit for bit."""
     m, n, B, K = shape
     which, fused = {"lena": ("ZEL", False), "fused": ("", True), "zonly": ("Z", False)}[loss]
-    rev, per = both_cot(dl, "v1", m, n, B, K, 9990 + m, monkeypatch, which, fused)
+    rev, per = both_cot(dl, "v1", m, n, B, K, 9990 + m, flags, which, fused)
     check_equal_v1(rev, per, K)
 
 
-def test_reverse_v1_headline_shape(dl, monkeypatch):
+def test_reverse_v1_headline_shape(dl, flags):
     """V1 at m=256, n=512, K=15 on 4,096 columns with the main_lena.py loss's cotangents."""
-    rev, per = both_cot(dl, "v1", 256, 512, 4096, 15, 9995, monkeypatch, "ZEL", False)
+    rev, per = both_cot(dl, "v1", 256, 512, 4096, 15, 9995, flags, "ZEL", False)
     check_equal_v1(rev, per, 15)
 
 
-def _zmask_ab(dl, variant, m, n, B, K, seed, monkeypatch, mixed=False):
+def _zmask_ab(dl, variant, m, n, B, K, seed, flags, mixed=False):
     """The per-row-theta variants' BK2 with masks read off the saved Z_k (PH 5) against the
-    recomputing BK2 (PH 2, DLADMM_BWD_ZMASK=0).  mixed: theta_z of every other ROW negative in
+    recomputing BK2 (PH 2, flags bwd_no_zmask).  mixed: theta_z of every other ROW negative in
     every layer (each row takes its own branch of the mask)."""
     ops = import_module("d-ladmm_amd.ops")
     d = dict(variant=variant, m=m, n=n, B=B, K=K, seed=seed, perturb=0.1, negtheta=not mixed)
@@ -224,9 +224,9 @@ def _zmask_ab(dl, variant, m, n, B, K, seed, monkeypatch, mixed=False):
     coef = torch.tensor([[1e-2, 1.0]] * K, device="cuda")
     kw = dict(loss_kind=lk, loss_coef=coef, **tables)
     a = ops.dladmm_backward(*args, r, **kw)
-    monkeypatch.setenv("DLADMM_BWD_ZMASK", "0")
+    flags.set(bwd_no_zmask=True)
     b = ops.dladmm_backward(*args, r, **kw)
-    monkeypatch.delenv("DLADMM_BWD_ZMASK")
+    flags.set(bwd_no_zmask=False)
     assert nrel(a.gW.cpu().numpy(), b.gW.cpu().numpy()) <= 1e-6
     ga, gb = a.g_row.cpu().numpy(), b.g_row.cpu().numpy()
     for k in range(K):
@@ -235,13 +235,13 @@ def _zmask_ab(dl, variant, m, n, B, K, seed, monkeypatch, mixed=False):
 
 @pytest.mark.parametrize("variant", ["v2", "v3"])
 @pytest.mark.parametrize("mixed", [False, True])
-def test_per_row_theta_zmask_matches_recomputing(variant, mixed, dl, monkeypatch):
+def test_per_row_theta_zmask_matches_recomputing(variant, mixed, dl, flags):
     """negtheta (mixed=False): theta < 0 on every other layer; mixed: on every other row."""
-    _zmask_ab(dl, variant, 96, 200, 150, 4, 9870, monkeypatch, mixed)
+    _zmask_ab(dl, variant, 96, 200, 150, 4, 9870, flags, mixed)
 
 
 @pytest.mark.parametrize("tied", [False, True])
-def test_reverse_v5_tied_step(tied, dl, monkeypatch):
+def test_reverse_v5_tied_step(tied, dl, flags):
     """V5 (one shared weight, a trainable step ss1_k on W Var_k) on the reverse sweep: ss1_k's
     gradient -<W, gU_k Var_k^T> from the weight gradient's sums in both paths; the per-layer
     path's BK2 reads the masks off Z_k too.  gW summed over the layers (tied) or per layer."""
@@ -249,9 +249,9 @@ def test_reverse_v5_tied_step(tied, dl, monkeypatch):
     coef = torch.tensor([[1e-2, 1.0]] * 4, device="cuda")
     kw = dict(loss_kind=dl._lib.LOSS_L1L1, loss_coef=coef, tied=tied, **tables)
     rev = ops.dladmm_backward(*args, r, **kw)
-    monkeypatch.setenv("DLADMM_BWD_REV", "0")
+    flags.set(bwd_per_layer=True)
     per = ops.dladmm_backward(*args, r, **kw)
-    monkeypatch.delenv("DLADMM_BWD_REV")
+    flags.set(bwd_per_layer=False)
     assert rev.path == 1 and per.path == 0
     assert torch.equal(rev.gW, per.gW)
     gs_r, gs_p = rev.g_scalar.cpu().numpy(), per.g_scalar.cpu().numpy()
@@ -278,19 +278,19 @@ def check_equal_row(rev, per, K):
 @pytest.mark.parametrize("shape", [(20, 30, 70, 3), (64, 200, 333, 2), (250, 500, 200, 4),
                                    (256, 512, 64, 1)])
 @pytest.mark.parametrize("loss", ["fused", "zel"])
-def test_reverse_per_row_params(variant, shape, loss, dl, monkeypatch):
+def test_reverse_per_row_params(variant, shape, loss, dl, flags):
     """V2 (main_syn_l1l1_ltheta.py) and V3 (main_syn_l1l1_full.py) on the reverse sweep (round
     4): per-row parameters as row-table operands, per-row gradient partials per (layer, slot,
     row, 16-column wave) as the per-layer kernels form them."""
     m, n, B, K = shape
     which, fused = {"fused": ("", True), "zel": ("ZEL", False)}[loss]
-    rev, per = both_cot(dl, variant, m, n, B, K, 9870 + m, monkeypatch, which, fused)
+    rev, per = both_cot(dl, variant, m, n, B, K, 9870 + m, flags, which, fused)
     check_equal_row(rev, per, K)
 
 
 @pytest.mark.parametrize("variant", ["v2", "v3"])
-def test_reverse_per_row_headline_shape(variant, dl, monkeypatch):
-    rev, per = both_cot(dl, variant, 256, 512, 4096, 15, 9880, monkeypatch, "", True)
+def test_reverse_per_row_headline_shape(variant, dl, flags):
+    rev, per = both_cot(dl, variant, 256, 512, 4096, 15, 9880, flags, "", True)
     check_equal_row(rev, per, 15)
 
 

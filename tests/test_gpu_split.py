@@ -246,11 +246,11 @@ def test_split_training_saves_product_and_matches_fp32(variant, dl):
 
 
 @pytest.mark.parametrize("variant", ["v4", "v5", "v6"])
-def test_split_weight_gradient_on_f16_cores(variant, dl, monkeypatch):
+def test_split_weight_gradient_on_f16_cores(variant, dl, flags):
     """Under precision "f32_split" the backward's weight-gradient GEMM (gU_k Var_k^T over the
     batch) also runs on the f16 matrix cores with exactly split operands
-    (csrc/dladmm_wgrad_x3.hip): its gradients equal the fp32-MFMA kernel's (DLADMM_WGRAD_X3=0)
-    within fp32 GEMM accuracy, every other gradient is unchanged bitwise, and it is
+    (csrc/dladmm_wgrad_x3.hip): its gradients equal the fp32-MFMA kernel's (plan flag
+    wgrad_f32) within fp32 GEMM accuracy, every other gradient is unchanged bitwise, and it is
     deterministic.  B = 4,096: whole 32-column sub-chunks of the split-K chunks."""
     from test_gpu_backward import make_train_net
     m, n, B, K = 256, 512, 4096, 3
@@ -261,7 +261,7 @@ def test_split_weight_gradient_on_f16_cores(variant, dl, monkeypatch):
     coeffs = [0.6] * (K - 1) + [1.0]
     grads = {}
     for mode in ("0", "1", "1b"):
-        monkeypatch.setenv("DLADMM_WGRAD_X3", mode[0])
+        flags.set(wgrad_f32=mode == "0")
         net = make_train_net(dl, variant, inp, sd, K)
         net.precision = "f32_split"
         tot, _ = net.training_loss(X, 1e-3, coeffs, kind)
@@ -284,27 +284,52 @@ def test_split_weight_gradient_on_f16_cores(variant, dl, monkeypatch):
             assert torch.equal(grads["1"][k], grads["0"][k]), k
 
 
-@pytest.mark.parametrize("tj,run,ramp", [("256", "1", False), ("128", "1", False),
-                                         ("256", "1", True), ("256", "0", True)])
-def test_split_weight_gradient_full_batch(tj, run, ramp, dl, monkeypatch):
-    """The split-f16 weight gradient at the bench's batch (B = 65,536: 32 sub-chunks per split-K
-    chunk, multi-GiB operand buffers whose addresses cross bit 31) in both V-tile widths
-    (DLADMM_WGRAD_X3_TJ) and both scale policies (DLADMM_WGRAD_X3_RUN: running per-chunk scales,
-    or one per sub-chunk): the fc* gradients stay within 1e-5 of the fp32-MFMA kernel's.  ramp:
-    X's columns grow by 2^12 across every 1,024-column chunk, so the running scales drop many
-    times inside a chunk (each an exact power-of-two rescale of the accumulators)."""
+@pytest.mark.parametrize("B", [20, 100, 300])
+def test_split_weight_gradient_any_batch(B, dl, flags):
+    """Every batch takes the split-f16 weight gradient on the reverse sweep (its operand columns
+    are padded to 32 and its chunks rounded to whole 32-column sub-chunks), including the
+    reference's batch_size = 20 (main_lena.py:155): fc* gradients within 1e-5 of the fp32-MFMA
+    kernel's and not bitwise equal to them (the f16 kernel ran)."""
     from test_gpu_backward import make_train_net
-    m, n, B, K = 256, 512, 65536, 2
+    m, n, K = 256, 512, 3
+    inp = P.make_inputs(m, n, B, 7715)
+    sd = P.make_state_dict("v4", m, n, B, K, inp["A"], 7715, perturb=0.1)
+    X = torch.from_numpy(inp["X"]).cuda()
+    grads = {}
+    for mode in ("0", "1"):
+        flags.set(wgrad_f32=mode == "0")
+        net = make_train_net(dl, "v4", inp, sd, K)
+        net.precision = "f32_split"
+        tot, _ = net.training_loss(X, 1e-3, [0.6, 0.6, 1.0], "l1l1")
+        tot.backward()
+        grads[mode] = {k: p.grad.detach().clone() for k, p in net.named_parameters()
+                       if p.grad is not None and k.startswith("fc")}
+    for k, b in grads["0"].items():
+        a = grads["1"][k]
+        assert not torch.equal(a, b), k
+        assert float((a.double() - b.double()).norm() / b.double().norm()) <= 1e-5, k
+
+
+@pytest.mark.parametrize("m,n,ramp", [(256, 512, False), (64, 256, False), (256, 512, True),
+                                      (64, 256, True)])
+def test_split_weight_gradient_full_batch(m, n, ramp, dl, flags):
+    """The split-f16 weight gradient at the bench's batch (B = 65,536: 32 sub-chunks per split-K
+    chunk, multi-GiB operand buffers whose addresses cross bit 31) in both V-tile widths (m = 256:
+    256-row tiles, three buffers; m = 64 (rows padded to 128): 128-row tiles, two workgroups per
+    CU): the fc*
+    gradients stay within 1e-5 of the fp32-MFMA kernel's.  ramp: X's columns grow by 2^12 across
+    every 1,024-column chunk, so the running scales drop many times inside a chunk (each an exact
+    power-of-two rescale of the accumulators)."""
+    from test_gpu_backward import make_train_net
+    B, K = 65536, 2
     inp = P.make_inputs(m, n, B, 7717)
     sd = P.make_state_dict("v4", m, n, B, K, inp["A"], 7717, perturb=0.1)
     X = torch.from_numpy(inp["X"]).cuda()
     if ramp:
         X = X * torch.exp2(12.0 * (torch.arange(B, device=X.device) % 1024) / 1024 - 6.0)
-    monkeypatch.setenv("DLADMM_WGRAD_X3_TJ", tj)
-    monkeypatch.setenv("DLADMM_WGRAD_X3_RUN", run)
     grads = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("DLADMM_WGRAD_X3", mode)
+        flags.set(wgrad_f32=mode == "0")
         net = make_train_net(dl, "v4", inp, sd, K)
         net.precision = "f32_split"
         tot, _ = net.training_loss(X, 1e-3, [0.6, 1.0], "l1l1")
@@ -320,20 +345,20 @@ def test_split_weight_gradient_full_batch(tj, run, ramp, dl, monkeypatch):
         assert float((a - b.double()).norm() / b.double().norm()) <= 1e-5, k
 
 
-def test_split_weight_gradient_per_layer_backward(dl, monkeypatch):
-    """The per-layer backward (DLADMM_BWD_REV=0: the fallback when the reverse sweep's workspace
-    does not fit) also runs the weight-gradient GEMM split-f16 after a split-f16 forward: fc*
-    gradients within 1e-5 of the fp32-MFMA kernel's and not bitwise equal to them; every other
-    gradient bitwise equal."""
+def test_split_weight_gradient_per_layer_backward(dl, flags):
+    """The per-layer backward (plan flag bwd_per_layer: the fallback when the reverse sweep's
+    workspace does not fit) also runs the weight-gradient GEMM split-f16 after a split-f16
+    forward: fc* gradients within 1e-5 of the fp32-MFMA kernel's and not bitwise equal to them;
+    every other gradient bitwise equal."""
     from test_gpu_backward import make_train_net
     m, n, B, K = 256, 512, 4096, 3
     inp = P.make_inputs(m, n, B, 7719)
     sd = P.make_state_dict("v4", m, n, B, K, inp["A"], 7719, perturb=0.1)
     X = torch.from_numpy(inp["X"]).cuda()
-    monkeypatch.setenv("DLADMM_BWD_REV", "0")
+    flags.set(bwd_per_layer=True)
     grads = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("DLADMM_WGRAD_X3", mode)
+        flags.set(wgrad_f32=mode == "0")
         net = make_train_net(dl, "v4", inp, sd, K)
         net.precision = "f32_split"
         tot, _ = net.training_loss(X, 1e-3, [0.6, 0.6, 1.0], "l1l1")
@@ -352,38 +377,47 @@ def test_split_weight_gradient_per_layer_backward(dl, monkeypatch):
             assert torch.equal(grads["1"][k], grads["0"][k]), k
 
 
-@pytest.mark.parametrize("prec,var,val", [
-    ("f32_split", "DLADMM_WGRAD_X3_TJ", "128"),
-    ("f32_split", "DLADMM_WGRAD_X3_XCD", "0"),
-    ("f32_split", "DLADMM_WGRAD_X3_BUFS", "2"),
-    ("f32_split", "DLADMM_WGRAD_X3_SPEC", "1"),
-    ("f32_split", "DLADMM_WGRAD_X3_DPOS", "0"),
-    ("f32_split", "DLADMM_WGRAD_X3_DPOS", "2"),
-    ("f32", "DLADMM_WGRAD_XCD", "0"),
-])
-def test_weight_gradient_schedules_bit_identical(prec, var, val, dl, monkeypatch):
-    """The weight-gradient schedule switches change only where and when the work runs, not its
-    arithmetic: V-tile width (each wave keeps its 64 G x 64 V rows and their scales), workgroup
-    order over the XCDs, buffer count, the speculative split, where the LDS-DMA is issued --
-    every gradient bitwise equal to
-    the default schedule's.  B = 65,536 with the magnitude ramp, so the running scales move."""
+@pytest.mark.parametrize("side", ["G", "V"])
+def test_split_weight_gradient_row_range(side, dl, flags):
+    """Per-row accuracy of the split-f16 weight gradient (csrc/dladmm_wgrad_x3.hip "Dynamic
+    range"): its power-of-two scales are per wave (64 G rows x 64 V rows), so rows far below the
+    wave's largest lose low-order bits.  Here every other row of one operand is 2^20 below its
+    neighbours (G = gU_0: rows of the cotangent of Z_0; V = Var_0: rows of E0, with X = Z0 = L0
+    = 0 so Var_0 = beta1 E0), and EVERY row of gW (G side) / column (V side) must match the
+    fp32-MFMA kernel within 1e-5 of that row's own norm -- the documented per-wave range."""
+    from importlib import import_module
+    ops = import_module("d-ladmm_amd.ops")
     from test_gpu_backward import make_train_net
-    m, n, B, K = 256, 512, 65536, 2
-    inp = P.make_inputs(m, n, B, 7723)
-    sd = P.make_state_dict("v4", m, n, B, K, inp["A"], 7723, perturb=0.1)
+    m, n, B, K = 256, 512, 4096, 1
+    rng = np.random.default_rng(7731)
+    A = P.make_inputs(m, n, 4, 7731)["A"]
+    E0 = rng.standard_normal((m, B)).astype(np.float32)
+    gz = rng.standard_normal((n, B)).astype(np.float32)
+    if side == "G":
+        gz[1::2] *= 2.0 ** -20
+    else:
+        E0[1::2] *= 2.0 ** -20
+    z = np.zeros
+    inp = dict(A=A, X=z((m, B), np.float32), Z0=z((n, B), np.float32), E0=E0,
+               L0=z((m, B), np.float32))
+    sd = P.make_state_dict("v4", m, n, B, K, A, 7731, perturb=0.1)
+    sd["active_para.0"][:] = 0.0   # every element of Z_0 passes the shrink: gU_0 = gZ_0
+    net = make_train_net(dl, "v4", inp, sd, K)
     X = torch.from_numpy(inp["X"]).cuda()
-    X = X * torch.exp2(12.0 * (torch.arange(B, device=X.device) % 1024) / 1024 - 6.0)
-    grads = {}
-    for mode in ("default", "switched"):
-        if mode == "switched":
-            monkeypatch.setenv(var, val)
-        net = make_train_net(dl, "v4", inp, sd, K)
-        net.precision = prec
-        tot, _ = net.training_loss(X, 1e-3, [0.6, 1.0], "l1l1")
-        tot.backward()
-        torch.cuda.synchronize()
-        grads[mode] = {k: p.grad.detach().clone() for k, p in net.named_parameters()
-                       if p.grad is not None}
-        del net, tot
-    for k in grads["default"]:
-        assert torch.equal(grads["default"][k], grads["switched"][k]), k
+    W = [w.detach() for w in net._weights()]
+    tabs = net._tables(net.A.device)
+    with torch.no_grad():
+        r = ops.dladmm_forward(net.VARIANT, X, net.A, W, net.Z0, net.E0, net.L0, keep_all=True,
+                               want_T=True, want_P=True, precision="f32_split", **tabs)
+    assert r.path == 4
+    gZ = [torch.from_numpy(gz).cuda()]
+    res = {}
+    for f32 in (True, False):
+        flags.set(wgrad_f32=f32)
+        res[f32] = ops.dladmm_backward(net.VARIANT, X, net.A, W, net.Z0, net.E0, net.L0, r,
+                                       gZ=gZ, **tabs).gW[0].double()
+    a, b = res[False], res[True]
+    assert not torch.equal(a, b)
+    dim = 1 if side == "G" else 0          # gW is (n, m): G rows are its rows, V rows its columns
+    err = ((a - b).norm(dim=dim) / b.norm(dim=dim)).cpu().numpy()
+    assert np.all(err <= 1e-5), (side, float(err.max()), int(err.argmax()))

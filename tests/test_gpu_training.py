@@ -180,6 +180,8 @@ def test_v1_beta_shard_matches_whole_batch(world, kind, dl):
         full.requires_grad_(False)
         Zf, Ef, Lf = full(X)
         full.requires_grad_(True)
+    from importlib import import_module
+    ddist = import_module("d-ladmm_amd.dist")
     gsum, tot = {}, 0.0
     m = inp["A"].shape[0]
     for r in range(world):
@@ -195,7 +197,7 @@ def test_v1_beta_shard_matches_whole_batch(world, kind, dl):
             if p.grad is None or gf is None:   # unreached (the last layer's E step under l1l1)
                 assert p.grad is None and gf is None, key
                 continue
-            if getattr(p, "_dladmm_rank_local", False):
+            if id(p) in ddist.rank_local_params(net):
                 e = nrel(p.grad.cpu().numpy(), gf[:, c0:c1].cpu().numpy())
                 assert e <= 1e-5, (r, key, e)
             elif p.grad is not None:

@@ -5,7 +5,7 @@ events on the current stream.
 
     python tools/bench_bwd.py --libs main,d-ladmm_amd/lib/abl/x/libdladmm_hip.so [--reps 10]
 
-`main` is the in-tree library; DLADMM_BWD_REV=0 in the environment selects the per-layer
+`main` is the in-tree library; --per-layer (plan flag bwd_per_layer) selects the per-layer
 kernels for every library.  Prints one JSON line: median / min ms per library.
 """
 from __future__ import annotations
@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--layers", type=int, default=15)
+    ap.add_argument("--per-layer", action="store_true",
+                    help="plan flag bwd_per_layer: the per-layer backward kernels")
     a = ap.parse_args()
     dl = importlib.import_module("d-ladmm_amd")
     ops = importlib.import_module("d-ladmm_amd.ops")
@@ -62,7 +64,8 @@ def main():
             L._LIB = h
             torch.cuda.synchronize()
             ev0.record()
-            res = ops.dladmm_backward(*args, r, **kw)
+            with ops.plan_flags(bwd_per_layer=a.per_layer):
+                res = ops.dladmm_backward(*args, r, **kw)
             ev1.record()
             torch.cuda.synchronize()
             if rep:  # the first round warms every library's kernels and workspace
@@ -70,8 +73,7 @@ def main():
             del res
     out = {s: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))}
            for s, t in times.items()}
-    out["config"] = dict(m=m, n=n, K=K, B=B, reps=a.reps,
-                         rev=os.environ.get("DLADMM_BWD_REV", "1") != "0")
+    out["config"] = dict(m=m, n=n, K=K, B=B, reps=a.reps, rev=not a.per_layer)
     print(json.dumps(out))
 
 
