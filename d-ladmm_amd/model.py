@@ -468,6 +468,7 @@ class _DLADMMFunction(torch.autograd.Function):
         ctx.tables = tables
         ctx.W = W
         ctx.fpath = r.path  # the forward's kernel path (4: split-f16, see dladmm_backward)
+        ctx.fflags = r.flags  # its plan options: the backward runs on an autograd thread
         ctx.save_for_backward(x, r.Z, r.E, r.L, r.T, r.P)
         ctx.set_materialize_grads(False)
         K = nl
@@ -482,7 +483,7 @@ class _DLADMMFunction(torch.autograd.Function):
         x, Z, E, L, T, P = ctx.saved_tensors
         mod = ctx.mod
         K = ctx.nl
-        saved = ForwardResult(Z, E, L, T, None, P=P, path=ctx.fpath)
+        saved = ForwardResult(Z, E, L, T, None, P=P, path=ctx.fpath, flags=ctx.fflags)
         res = dladmm_backward(mod.VARIANT, x, mod.A, ctx.W, mod.Z0, mod.E0, mod.L0, saved,
                               g[:K], g[K:2 * K], g[2 * K:3 * K],
                               g[3 * K:] if mod.RETURNS_T else None,
@@ -534,6 +535,7 @@ class _DLADMMLossFunction(torch.autograd.Function):
         # (cz_k, cf_k) per unit upstream gradient
         ctx.base = torch.stack([c * alpha / denom, c / denom], 1).to(torch.float32)
         ctx.fpath = r.path  # the forward's kernel path (4: split-f16, see dladmm_backward)
+        ctx.fflags = r.flags  # its plan options: the backward runs on an autograd thread
         ctx.save_for_backward(x, r.Z, r.E, r.L, r.T, r.P)
         per_layer = per_layer.to(torch.float32)
         ctx.mark_non_differentiable(per_layer)
@@ -547,7 +549,8 @@ class _DLADMMLossFunction(torch.autograd.Function):
         coef = (ctx.base * g_total).contiguous()  # device-side scale, no host sync
         Z0, E0, L0 = mod._init_state(ctx.cols)
         res = dladmm_backward(mod.VARIANT, x, mod.A, ctx.W, Z0, E0, L0,
-                              ForwardResult(Z, E, L, T, None, P=P, path=ctx.fpath),
+                              ForwardResult(Z, E, L, T, None, P=P, path=ctx.fpath,
+                                            flags=ctx.fflags),
                               loss_kind=ctx.lk,
                               loss_coef=coef,
                               tied=mod._shared_weight(), **ctx.tables)
@@ -601,6 +604,7 @@ class _DLADMMLenaLossFunction(torch.autograd.Function):
         ctx.c = c32
         ctx.gEL = (gE, gL)
         ctx.fpath = r.path  # the forward's kernel path (4: split-f16, see dladmm_backward)
+        ctx.fflags = r.flags  # its plan options: the backward runs on an autograd thread
         ctx.save_for_backward(x, r.Z, r.E, r.L, r.T, r.P)
         per_layer = per_layer.to(torch.float32)
         ctx.mark_non_differentiable(per_layer)
@@ -628,7 +632,8 @@ class _DLADMMLenaLossFunction(torch.autograd.Function):
                            1).contiguous()
         Z0, E0, L0 = mod._init_state(ctx.cols)
         res = dladmm_backward(mod.VARIANT, x, mod.A, ctx.W, Z0, E0, L0,
-                              ForwardResult(Z, E, L, T, None, P=P, path=ctx.fpath),
+                              ForwardResult(Z, E, L, T, None, P=P, path=ctx.fpath,
+                                            flags=ctx.fflags),
                               gE=[gE[k] for k in range(K)], gL=[gL[k] for k in range(K)],
                               loss_kind=_lib.LOSS_L1L1, loss_coef=coef,
                               tied=mod._shared_weight(), **ctx.tables)

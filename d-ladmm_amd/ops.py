@@ -29,6 +29,7 @@ class ForwardResult:
     P: Optional[torch.Tensor] = None  # [K, m, B] A Z_k per layer (want_P: training forwards)
     path: int = 0  # dladmm_fwd_path: the kernel path that ran (1 fused, 2 per-layer, 3 bf16
                    # tiles, 4 fused split-f16; 0 = nothing launched)
+    flags: int = 0  # the plan options (dladmm_flags) the forward ran with; its backward keeps them
 
 
 _PLAN_FLAGS = contextvars.ContextVar("dladmm_plan_flags", default=0)
@@ -43,7 +44,9 @@ def plan_flags(**opts):
     inside the block, e.g. `with plan_flags(per_layer=True): net(X)` runs the per-layer kernels
     where the fused kernel would fit.  They select kernels, never arithmetic; the C ABI receives
     them in dladmm_fwd_desc.flags (the library reads no environment).  Nested blocks add to the
-    enclosing block's flags; a False value clears that flag."""
+    enclosing block's flags; a False value clears that flag.  A backward keeps the options its
+    forward ran with (ForwardResult.flags; autograd runs backwards on worker threads, outside
+    the block) and adds those of a block around the backward call itself."""
     flags = _PLAN_FLAGS.get()
     for k, v in opts.items():
         if k not in _FLAG_NAMES:
@@ -70,7 +73,7 @@ def _f32_dev(t: torch.Tensor, name: str) -> torch.Tensor:
 
 
 def _fill_fwd_desc(d, variant, X, A, W, Z0, E0, L0, scalar_params, row_params, beta1_elem,
-                   beta2_elem, keep_all, loss_kind, out):
+                   beta2_elem, keep_all, loss_kind, out, flags=None):
     """Validate the forward's tensors and fill the C descriptor `d` (a FwdDesc, possibly embedded
     in a BwdDesc).  Returns the ctypes arrays that must outlive the call."""
     X = _f32_dev(X, "X")
@@ -95,7 +98,7 @@ def _fill_fwd_desc(d, variant, X, A, W, Z0, E0, L0, scalar_params, row_params, b
             raise RuntimeError(f"dladmm: fc[{k}].weight must be ({n}, {m}) with a common stride")
     dev = X.device
     d.abi_version = _lib.ABI_VERSION
-    d.flags = _PLAN_FLAGS.get()
+    d.flags = _PLAN_FLAGS.get() if flags is None else int(flags)
     d.variant, d.m, d.n, d.batch, d.layers = variant, m, n, B, K
     d.keep_all, d.loss_kind = int(bool(keep_all)), int(loss_kind)
     d.X, d.ld_x = X.data_ptr(), X.stride(0)
@@ -158,7 +161,7 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
                    out: Optional[ForwardResult] = None,
                    kernel_events: Optional[tuple] = None,
                    want_col_loss: bool = False, precision: str = "f32",
-                   want_P: bool = False) -> ForwardResult:
+                   want_P: bool = False, flags: Optional[int] = None) -> ForwardResult:
     """Run the whole K-layer forward of `variant` (dladmm_variant) on X's device.
 
     X: (m, B); A: (m, n); W: K tensors (n, m) (fc[k].weight; V5 passes the shared one K times);
@@ -168,6 +171,8 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
     want_P (training): also keep P_k = A Z_k of every layer (result.P) when the call runs on the
     fused fp32 kernel, so the backward reads the product instead of recomputing it; on every
     other path result.P stays None and the backward recomputes it.
+    flags: plan options (include/dladmm.h dladmm_flags); None = those of the enclosing
+    plan_flags block.
     """
     L = _lib.lib()
     _f32_dev(X, "X")
@@ -185,12 +190,13 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
               if want_T else None)
         ls = torch.empty((K, 2), device=dev, dtype=torch.float64) if loss_kind else None
         out = ForwardResult(Zo, Eo, Lo, To, ls)
+    out.flags = _PLAN_FLAGS.get() if flags is None else int(flags)
 
     if B == 0:
         # an empty batch: the reference's ops return empty (rows, 0) tensors and zero sums; no
         # kernel runs (shapes are still checked)
         _fill_fwd_desc(_lib.FwdDesc(), variant, X, A, W, Z0, E0, L0, scalar_params, row_params,
-                       beta1_elem, beta2_elem, keep_all, loss_kind, out)
+                       beta1_elem, beta2_elem, keep_all, loss_kind, out, out.flags)
         if out.loss_sums is not None:
             out.loss_sums.zero_()
         if want_col_loss:
@@ -200,7 +206,7 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
         return out
     d = _lib.FwdDesc()
     keep = _fill_fwd_desc(d, variant, X, A, W, Z0, E0, L0, scalar_params, row_params, beta1_elem,
-                          beta2_elem, keep_all, loss_kind, out)
+                          beta2_elem, keep_all, loss_kind, out, out.flags)
     if precision not in _PRECISIONS:
         raise ValueError(f"dladmm: precision must be one of {sorted(_PRECISIONS)}, "
                          f"got {precision!r}")
@@ -250,14 +256,15 @@ def dladmm_backward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[
                     row_params: Optional[torch.Tensor] = None,
                     beta1_elem: Sequence[torch.Tensor] = (),
                     beta2_elem: Sequence[torch.Tensor] = (),
-                    tied: bool = False) -> BackwardResult:
+                    tied: bool = False, flags: Optional[int] = None) -> BackwardResult:
     """Gradients of sum_k <gZ_k,Z_k> + <gE_k,E_k> + <gL_k,L_k> + sum_j <gT_j,T_j> (+ the fused
     training objective sum_k cz_k sum|Z_k| + cf_k fit_k when loss_kind, loss_coef = device
     (K, 2) fp32 (cz_k, cf_k)) w.r.t. the parameters of the forward that produced `saved` (a
     keep_all ForwardResult with T), via `dladmm_bwd_f32` (include/dladmm.h).  Cotangents are
     per-layer sequences of (rows, B) tensors (None entries / None = zero).  This is the backward
     of the reference's `total_loss.backward()` through DLADMMNet.forward
-    (main_syn_l1l1_scalar.py:298)."""
+    (main_syn_l1l1_scalar.py:298).  flags: plan options; None = the forward's (saved.flags)
+    plus those of an enclosing plan_flags block."""
     L = _lib.lib()
     if saved.T is None or saved.Z.shape[0] != len(W):
         raise ValueError("dladmm: backward needs the keep_all forward outputs including T")
@@ -275,8 +282,10 @@ def dladmm_backward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[
         return BackwardResult(torch.zeros((1 if tied else K, n, m), device=dev), gs, gr, gb,
                               [t.clone() for t in gb])
     d = _lib.BwdDesc()
+    if flags is None:
+        flags = int(getattr(saved, "flags", 0)) | _PLAN_FLAGS.get()
     keep = _fill_fwd_desc(d.fwd, variant, X, A, W, Z0, E0, L0, scalar_params, row_params,
-                          beta1_elem, beta2_elem, True, 0, saved)
+                          beta1_elem, beta2_elem, True, 0, saved, flags)
     # a split-f16 training forward (path 4) also runs the weight-gradient GEMM on the f16
     # matrix cores (csrc/dladmm_wgrad_x3.hip); every other backward kernel is the fp32 one
     d.fwd.precision = _PRECISIONS["f32_split"] if saved.path == 4 else _PRECISIONS["f32"]
