@@ -109,3 +109,55 @@ def test_backward_workspace_and_validation(dl):
     bb.fwd.keep_all = 1
     bb.fwd.T = None
     assert L.dladmm_bwd_f32(ctypes.byref(bb), None) == -7
+
+
+def test_plan_flags_select_kernels(dl):
+    """dladmm_fwd_desc.flags (enum dladmm_flags) is the whole plan-option input: per_layer moves
+    a fused-shape forward to the per-layer pair; bwd_per_layer moves a saved-product backward
+    off the reverse sweep; unknown bits change nothing."""
+    L = dl._lib.lib()
+    d, _keep = _desc(dl)
+    assert L.dladmm_fwd_path(ctypes.byref(d)) == 1
+    d.flags = dl._lib.F_PER_LAYER
+    assert L.dladmm_fwd_path(ctypes.byref(d)) == 2
+    d.flags = 1 << 20
+    assert L.dladmm_fwd_path(ctypes.byref(d)) == 1
+    d.precision = dl._lib.PREC_BF16
+    for f in (0, dl._lib.F_BF16_WIDE):
+        d.flags = f
+        assert L.dladmm_fwd_path(ctypes.byref(d)) == 3
+    b, _k = _bdesc(dl)
+    b.fwd.P = 1 << 40   # a saved-product forward
+    assert L.dladmm_bwd_path(ctypes.byref(b)) == 1
+    b.fwd.flags = dl._lib.F_BWD_PER_LAYER
+    assert L.dladmm_bwd_path(ctypes.byref(b)) == 0
+    assert L.dladmm_bwd_workspace_bytes(ctypes.byref(b)) > 0
+
+
+def test_library_reads_no_environment(dl):
+    """The product library imports no getenv: plan choices come from the descriptor only (the
+    cycle-stamp diagnostic build, -DX3_STAMP, is the one exception and is never shipped)."""
+    import shutil
+    import subprocess
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    if not os.path.exists(nm) and not shutil.which(nm):
+        pytest.skip("no nm")
+    out = subprocess.run([nm, "-D", "--undefined-only", dl._lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    assert "getenv" not in out
+
+
+def test_plan_flags_context():
+    import importlib
+    ops = importlib.import_module("d-ladmm_amd.ops")
+    lib = importlib.import_module("d-ladmm_amd._lib")
+    assert ops._PLAN_FLAGS.get() == 0
+    with ops.plan_flags(per_layer=True) as f1:
+        assert f1 == lib.F_PER_LAYER
+        with ops.plan_flags(bwd_unfused=True, per_layer=False) as f2:
+            assert f2 == lib.F_BWD_UNFUSED
+        assert ops._PLAN_FLAGS.get() == lib.F_PER_LAYER
+    assert ops._PLAN_FLAGS.get() == 0
+    with pytest.raises(ValueError):
+        with ops.plan_flags(no_such_flag=True):
+            pass
