@@ -1,8 +1,8 @@
 """A/B of the fused forward kernel with and without the saved product (want_P: the training
 forward also stores A Z_k for the backward), V4 m=256 n=512 K=15 B=65,536, interleaved in one
 process, HIP-event kernel times (median of 10).  Prints one JSON line."""
-import sys, importlib, json, torch
-sys.path.insert(0, "."); import bench
+import os, sys, importlib, json, torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__)))); import bench
 dl = importlib.import_module("d-ladmm_amd"); ops = importlib.import_module("d-ladmm_amd.ops")
 dev = torch.device("cuda", 0); m, n, K, B = 256, 512, 15, 65536
 A, X, Z0, E0, L0 = bench.synth(m, n, B, 0, dev)
