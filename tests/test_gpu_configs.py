@@ -268,3 +268,36 @@ def test_batch_beyond_32bit_row_offsets(dl, oracle):
     cols = pick_columns(B, 32, 10802)
     subset_vs_oracle(oracle, "v4", d, sd, K, r, cols, "v4 B=2^20+64", "layered")
     objective_vs_reduction(d, r, 1.0, "l1l1", "v4 B=2^20+64", "layered")
+
+
+@pytest.mark.parametrize("init", ["w04_betas_perturbed", "reference_default"])
+def test_v1_northstar_b65536(init, dl, oracle):
+    """The north_star's primary variant at its own shape -- bench.py's `v1` line: main_lena.py's
+    DLADMMNet, m=256 n=512 K=15 B=65,536, per-sample (m, B) betas read by every layer, every
+    layer's Z/E/L written.  A column subset (with the ragged-free last tile) against the oracle
+    at the fp32 bar.  reference_default: the module's own init (betas 1, W = A^T + 1e-3 N,
+    main_lena.py:35-49), the ill-conditioned case whose bar is the gap clause; w04: W scaled by
+    0.4 and every beta element perturbed by up to 10 %, so the per-element loads carry distinct
+    values and the 1e-5 clause applies."""
+    m, n, K, B = 256, 512, 15, 65536
+    d = device_problem(m, n, B, 10601)
+    torch.manual_seed(10601)
+    net = dl.DLADMMNet(m=m, n=0, d=n, batch_size=B, A=d["A"], Z0=d["Z0"], E0=d["E0"],
+                       L0=d["L0"], layers=K)
+    net.requires_grad_(False)
+    if init == "w04_betas_perturbed":
+        g = torch.Generator(device="cuda").manual_seed(10602)
+        with torch.no_grad():
+            for fc in net.fc:
+                fc.weight.mul_(0.4)
+            for pl in (net.beta1, net.beta2):
+                for p in pl:
+                    p.mul_(1.0 + 0.1 * (torch.rand(p.shape, generator=g, device="cuda") - 0.5))
+    with torch.no_grad():
+        r = net.run(d["X"], keep_all=True)
+    assert r.path == 1 and r.T is None
+    cols = pick_columns(B, 48, 10603)
+    cidx = torch.from_numpy(cols).cuda()
+    sd = {k: (v.index_select(1, cidx) if k.startswith("beta") else v).cpu().numpy()
+          for k, v in net.state_dict().items()}
+    subset_vs_oracle(oracle, "v1", d, sd, K, r, cols, f"v1 north_star B=65536 {init}", "f32")
