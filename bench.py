@@ -394,6 +394,9 @@ def main():
         c_el, c_kern, _, _ = timed(w1, "f32")
         v1 = dict(value=B * a.steps / c_el, ms_per_step=c_el / a.steps * 1e3, kern=c_kern,
                   path=w1.path, B=B)
+        if not a.no_split:   # V1 on the split-f16 kernel (round 6; same fp32 tolerances)
+            s_el, s_kern, _, _ = timed(w1, "f32_split")
+            v1["split"] = (B * a.steps / s_el, s_el / a.steps * 1e3, s_kern, w1.path)
         del w1
         torch.cuda.empty_cache()
     torch.cuda.synchronize()
@@ -581,6 +584,15 @@ def main():
                 "bytes_per_sample": b1 / v1["B"],
                 "hbm_frac_algorithmic": b1 / v1["kern"] / PEAK_HBM,
             }
+            if "split" in v1:
+                sv, sms, sk, spath = v1["split"]
+                res["v1"]["split_f16"] = {
+                    "value": sv, "ms_per_step": sms, "kernel_ms": sk * 1e3,
+                    "path": {4: "fused-split-f16"}.get(spath, spath),
+                    "roofline_frac_f16_over_3": f1 / sk / (PEAK_BF16_MFMA / 3),
+                    "note": "same V1 workload, fp32 GEMMs as three exactly split f16 MFMA "
+                            "products, the per-sample betas in the split kernel's epilogue "
+                            "(fp32 parity tolerances)"}
         if cfg3 is not None:
             f3 = (4 * K + 2) * m * n * cfg3["B"]
             res["cfg3_strong"] = {

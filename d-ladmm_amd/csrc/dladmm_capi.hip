@@ -432,7 +432,9 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
     p->off_zw = p->off_umax + align256((size_t)(nw + 1) * sizeof(unsigned));
     const bool lean = !d->keep_all && K > 1;
     p->off_loss = p->off_zw + (lean ? align256((size_t)2 * d->n * p->ldzw * sizeof(float)) : 0);
-    p->total = p->off_loss + align256((size_t)2 * K * p->nslots * sizeof(float));
+    p->off_btab = p->off_loss + align256((size_t)2 * K * p->nslots * sizeof(float));
+    p->total = p->off_btab +
+               (d->variant == DLADMM_V1_LENA ? align256((size_t)2 * K * sizeof(void*)) : 0);
     return 0;
   }
   if (s >= 0 && fits_32bit(d) && !force_layered && !bf16) {
@@ -632,6 +634,18 @@ inline int run_fused_x3(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipSt
   a.wexp = wexp;
   a.Zw = (float*)(ws + p.off_zw); a.ldzw = p.ldzw;
   a.dbg = dbg_ptr();  // diagnostic builds (X3_STAMP) write per-wave cycle sums here
+  if (d->variant == DLADMM_V1_LENA) {
+    // V1: the per-layer beta pointers as device tables (scalar-loaded per G2 pass, any depth)
+    a.ldb = d->ld_beta;
+    const void** tab = (const void**)(ws + p.off_btab);
+    if (hipError_t e = write_ptr_table((const void* const*)d->beta1_elem, d->layers, tab, s))
+      return (int)e;
+    if (hipError_t e = write_ptr_table((const void* const*)d->beta2_elem, d->layers,
+                                       tab + d->layers, s))
+      return (int)e;
+    a.b1t = (const float* const*)tab;
+    a.b2t = (const float* const*)(tab + d->layers);
+  }
   if (d->ev_kernel_start) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_start, s)) return (int)e;
   }

@@ -6,7 +6,7 @@ namespace dladmm {
 
 bool x3_supports(int variant) {
   return variant == DLADMM_V4_SCALAR || variant == DLADMM_V5_TIED ||
-         variant == DLADMM_V6_LASSO;
+         variant == DLADMM_V6_LASSO || variant == DLADMM_V1_LENA;
 }
 
 hipError_t launch_fused_x3_shape(int shape, int variant, const FusedArgs& a, int grid,

@@ -214,7 +214,7 @@ struct ZChunks {
 // that loads them by dword issues more, which only waits longer).  A step or chunk of the
 // other pass type (the window reaching across a pass boundary) counts with that pass's
 // schedule; the unrolled tails between passes only add younger operations.
-template <int MB, int NB, int KS1, int KS2, int SPC, bool SAVEP = false>
+template <int MB, int NB, int KS1, int KS2, int SPC, bool SAVEP = false, int PF = 0>
 struct Win {
   using Z = ZChunks<NB, KS1, SPC>;
   static constexpr int ST = NB * KS1;
@@ -249,10 +249,12 @@ struct Win {
   // G1 step body: the Z tile store (one dwordx4 per lane)
   static constexpr int ops1(int t) { return stores_at(t / KS1, t % KS1, KS1, 1); }
   // G2 step body: the E, L, T tile stores (+ SAVEP: one P dword store per epilogue row, block
-  // ib - 1's rows running in block ib's steps)
+  // ib - 1's rows running in block ib's steps; + PF: V1's per-element beta loads of block
+  // ib + 1, PF per row at the row steps of block ib)
   static constexpr int ops2(int t) {
     return stores_at(t / KS2, t % KS2, KS2, 3) +
-           ((SAVEP && t / KS2 >= 1) ? rows_at(t % KS2, KS2) : 0);
+           ((SAVEP && t / KS2 >= 1) ? rows_at(t % KS2, KS2) : 0) +
+           ((PF && t / KS2 + 1 < MB) ? PF * rows_at(t % KS2, KS2) : 0);
   }
   // DMA group of chunk c (c >= NCH: chunk c - NCH of the other pass)
   static constexpr int group(int c, bool g1) {
@@ -317,8 +319,10 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
   constexpr int STG_F4 = kWaves * 4 * 64;  // per wave 4 output tiles of 16 x 16 floats
   static_assert(FPC == 16, "DMA issue: 4 fragments per wave and chunk");
   static_assert((RING_F4 + X_F4 + STG_F4) * 16 <= 160 * 1024, "LDS budget");
-  static_assert(PKIND == PK_SCALAR || PKIND == PK_S1, "x3 path: scalar-parameter variants");
-  using W = Win<MB, NB, KS1, KS2, SPC, SAVEP>;
+  static_assert(PKIND == PK_SCALAR || PKIND == PK_S1 || (PKIND == PK_ELEM && EMODE == EM_V1),
+                "x3 path: scalar-parameter variants and V1's per-sample betas");
+  constexpr bool kElem = PKIND == PK_ELEM;
+  using W = Win<MB, NB, KS1, KS2, SPC, SAVEP, kElem ? 3 : 0>;
   __shared__ f32x4 smem[RING_F4 + X_F4 + STG_F4];
   f32x4* ring = smem;
   f32x4* xs = smem + RING_F4;  // xs[w][b][lane] = X rows 16b+4g+0..3 of this lane's column
@@ -553,6 +557,10 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     flush(3, O.t, oo4, soff);
   };
   float vmx = 0.f, vpend = 0.f;
+  // V1 (PK_ELEM): the per-sample betas of the G2 rows -- beta1_k (the L update, main_lena.py:89),
+  // beta2_k (the E-step, :87) and beta1_{k+1} (the next Var, :85) of block b, row r -- loaded two
+  // blocks ahead of their epilogue row into a 3-block ring of registers (pf_block below)
+  float pb[kElem ? 3 : 1][3][4];
   auto epi2_row = [&](const LayerP& P, bool pro, int b, int r, float Pv, float x, const OutR& O) {
     // SAVEP: A Z_k for the backward, the product exactly as the updates below consume it (a
     // dword store per row: the staging tiles carry E, L, T); mw still at block b's rows here
@@ -565,9 +573,15 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     }
     const float l0 = Lr[b][r];
     const float e0 = Er[b][r];
+    float b2 = P.b2, b3 = P.b3, b1n = P.b1n;
+    if constexpr (kElem) {
+      b3 = pb[b % 3][0][r];
+      b2 = pb[b % 3][1][r];
+      b1n = pb[b % 3][2][r];
+    }
     float e;
     if constexpr (EMODE == EM_V1) {
-      e = shrink_u((x - Pv) - P.b2 * l0, P.the);                     // main_lena.py:87
+      e = shrink_u((x - Pv) - b2 * l0, P.the);                       // main_lena.py:87
     } else if constexpr (EMODE == EM_VVAR) {
       const float vv = l0 + P.b2 * ((Pv + e0) - x);                  // scalar :114
       e = shrink_u(e0 - P.ss2 * vv, P.the);                          // scalar :115
@@ -576,7 +590,7 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     }
     e = pro ? e0 : e;
     const float t = (Pv + e) - x;                                    // main_lena.py:88
-    float l = l0 + P.b3 * t;                                         // main_lena.py:89
+    float l = l0 + b3 * t;                                           // main_lena.py:89
     l = pro ? l0 : l;
     Er[b][r] = e;
     Lr[b][r] = l;
@@ -586,7 +600,7 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
     const float res = x - Pv;
     if constexpr (LQ) fit = __builtin_fmaf(res, res, fit);
     else fit += fabsf(res);
-    const float v = l + P.b1n * t;                                   // main_lena.py:85
+    const float v = l + b1n * t;                                     // main_lena.py:85
     if (r & 1) vmx = amax2(vmx, vpend, v);  // rows in pairs: one v_max3
     else vpend = v;
     asm volatile("" : "+v"(fit), "+v"(vmx));
@@ -796,12 +810,42 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
   };
 
   // ---------------------------------------------------------------- G2(k): A Z_k -> E, L, T, Var
+  // V1: per-element beta views of the pass, lane offset (rows 4g.. of the lane's column; padded
+  // columns and rows past m read 0 through the buffer range)
+  const uint32_t vb = lane_off(a.ldb);
+  rsrc_t rb1 = mkrsrc(nullptr, 0u), rb2 = rb1, rbn = rb1;
+  // row offsets walk in program order (one SGPR pair, advanced per block): precomputed per
+  // (block, row) they were hoisted into ~64 SGPRs and spilled
+  SWalk bw{0u, (uint32_t)(a.ldb * 4)};
+  auto pf_row = [&](auto B_, auto R_) {
+    constexpr int bb = decltype(B_)::value, rr = decltype(R_)::value;
+    if constexpr (kElem) {
+      const int so = (int)bw.at(rr);
+      pb[bb % 3][0][rr] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb1, (int)vb, so, 0));
+      pb[bb % 3][1][rr] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb2, (int)vb, so, 0));
+      pb[bb % 3][2][rr] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rbn, (int)vb, so, 0));
+      if constexpr (rr == 3) bw.next();
+    }
+  };
   auto g2_pass = [&](auto PRO_, int k, const LayerP& P, const OutR& O, float zinv) {
     constexpr bool PRO = decltype(PRO_)::value;
     const int gi = 2 * k + 2;
     mw.reset();
     f32x4 qp = zero4;
     f32x4 xv;
+    if constexpr (kElem) {
+      // beta1_k, beta2_k, beta1_{k+1} (the prologue: beta1_0 for Var_0 only), from the device
+      // tables by scalar loads; then block 0's rows, ahead of the pass
+      typedef const float* const __attribute__((address_space(4)))* ctab_p;
+      const ctab_p t1 = (ctab_p)a.b1t, t2 = (ctab_p)a.b2t;
+      const uint32_t eb = (uint32_t)(m * a.ldb * 4);
+      const int kn = k + 1;
+      rb1 = mkrsrc(PRO ? nullptr : t1[k < 0 ? 0 : k], PRO ? 0u : eb);
+      rb2 = mkrsrc(PRO ? nullptr : t2[k < 0 ? 0 : k], PRO ? 0u : eb);
+      rbn = mkrsrc(kn < K ? t1[kn] : nullptr, kn < K ? eb : 0u);
+      bw.reset();
+      static_for<4>([&](auto R_) { pf_row(std::integral_constant<int, 0>{}, R_); });
+    }
     static_for<MB>([&](auto IB_) {
       constexpr int ib = decltype(IB_)::value;
       f32x4 acc = zero4;
@@ -810,6 +854,13 @@ __global__ __launch_bounds__(256, 1) void fused_x3_kernel(const FusedArgs a) {
         constexpr int s = decltype(S_)::value;
         constexpr int t = ib * KS2 + s;
         step_head(std::false_type{}, std::integral_constant<int, t>{}, gi);
+        // V1: block ib + 1's betas, one row per epilogue-row step (two blocks ahead of use)
+        if constexpr (kElem && ib + 1 < MB) {
+          static_for<4>([&](auto R_) {
+            if constexpr (W::row_step(decltype(R_)::value, KS2) == s)
+              pf_row(std::integral_constant<int, ib + 1>{}, R_);
+          });
+        }
         // XE: X rows of block ib (for its epilogue rows in block ib+1's steps / the tail), read
         // once block ib-1's last row has used xv
         if constexpr (XE && s == (ib == 0 ? 0 : S32 + 1)) xv = xs[(w * MB + ib) * 64 + lane];
@@ -979,6 +1030,7 @@ hipError_t dispatch_x3_variant(int variant, const FusedArgs& a, int grid, hipStr
     case DLADMM_V4_SCALAR: return launch_x3<MP, NP, EM_VVAR, PK_SCALAR, SAVEP>(a, grid, s);
     case DLADMM_V5_TIED: return launch_x3<MP, NP, EM_VVAR, PK_S1, SAVEP>(a, grid, s);
     case DLADMM_V6_LASSO: return launch_x3<MP, NP, EM_LASSO, PK_SCALAR, SAVEP>(a, grid, s);
+    case DLADMM_V1_LENA: return launch_x3<MP, NP, EM_V1, PK_ELEM, SAVEP>(a, grid, s);
   }
   return hipErrorInvalidValue;
 }

@@ -206,7 +206,8 @@ class _DLADMMBase(nn.Module):
     # GEMM precision of forward / run: "f32" (fp32 MFMA: every GEMM an exact fp32 fma chain),
     # "f32_split" (the same fp32 GEMMs on the f16 matrix cores: operands split exactly into
     # scaled hi + lo f16 halves, hi*hi + hi*lo + lo*hi accumulated in fp32 -- the error of an fp32
-    # GEMM, ~3x the throughput; V4-V6 fused shapes, others run f32) or "bf16" (BASELINE config 5:
+    # GEMM, ~3x the throughput; V1 and V4-V6 at the fused shapes, V2 / V3 run f32) or "bf16"
+    # (BASELINE config 5:
     # bf16 MFMA operands, fp32 accumulation and fp32 elementwise state).  Training runs "f32" or
     # "f32_split": the split-f16 forward saves the product A Z_k its updates consumed, and the
     # (fp32) backward differentiates that forward; "bf16" is inference-only.

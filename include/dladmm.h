@@ -147,7 +147,8 @@ typedef struct dladmm_fwd_desc {
          hi + lo f16 halves (22 significant bits), the product formed as hi*hi + hi*lo + lo*hi with
          fp32 accumulation (every f16 x f16 product is exact in fp32).  Error of an fp32 GEMM
          (same tolerance tests as PREC_F32); every elementwise update stays fp32.  Fused path
-         (m <= 256, n <= 512) for V4/V5/V6; other shapes / variants run PREC_F32;
+         (m <= 256, n <= 512) for V1 (per-sample betas) and V4/V5/V6; other shapes / variants
+         run PREC_F32;
        DLADMM_PREC_BF16 (BASELINE config 5: A, W_k and the state operands Var / Z_k rounded to bf16
          for the MFMAs, fp32 accumulation, every elementwise update -- shrinks, E, dual L, T -- in
          fp32).  bf16 runs on the per-layer kernels (path 3). */

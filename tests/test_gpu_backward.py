@@ -44,7 +44,7 @@ def nrel(a, b):
 
 # variants whose fused forward has a split-f16 form (csrc/dladmm_fused_x3.hip: V4-V6 and the
 # newS schedules built on them); the others train f32 under "f32_split"
-SPLIT_VARIANTS = ("v4", "v5", "v6", "v7", "v7t", "v7p")
+SPLIT_VARIANTS = ("v1", "v4", "v5", "v6", "v7", "v7t", "v7p")
 PRECISIONS = ("f32", "f32_split")
 
 

@@ -79,12 +79,17 @@ CASES = [
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["f32", "f32_split"])
 @pytest.mark.parametrize("name,K", CASES, ids=[c[0] for c in CASES])
-def test_lena_loss_and_grads_vs_fp64(dl, name, K):
+def test_lena_loss_and_grads_vs_fp64(dl, name, K, precision):
+    """At both training precisions: "f32_split" runs V1 (round 6) and V4 on the split-f16 forward
+    (V2 falls back to fp32), its saved A Z_k into the reverse sweep and the split-f16 weight
+    gradient -- main_lena.py's training step on the f16 matrix cores, at the fp32 bars."""
     defn = P.FIXTURES[name]
     coeffs = [0.6 if k < K - 1 else 1.0 for k in range(K)]
     net, inp, sd = build(dl, defn, K)
     net.requires_grad_(True)
+    net.precision = precision
     X = torch.from_numpy(inp["X"]).cuda()
     A = torch.from_numpy(inp["A"]).cuda()
     # fused
