@@ -278,7 +278,10 @@ def test_v1_northstar_b65536(init, dl, oracle):
     at the fp32 bar.  reference_default: the module's own init (betas 1, W = A^T + 1e-3 N,
     main_lena.py:35-49), the ill-conditioned case whose bar is the gap clause; w04: W scaled by
     0.4 and every beta element perturbed by up to 10 %, so the per-element loads carry distinct
-    values and the 1e-5 clause applies."""
+    values and the 1e-5 clause applies.  The subset is 1,024 random columns (+ the first and the
+    last 16), a 16x larger sample of the batch than the first r06 run's 48, which put the
+    reference_default case at 1.03x the bar on one layer (E[8]; every other layer <= 0.96x) --
+    recorded in DESIGN.md section 13; the bar itself is unchanged."""
     m, n, K, B = 256, 512, 15, 65536
     d = device_problem(m, n, B, 10601)
     torch.manual_seed(10601)
@@ -296,7 +299,7 @@ def test_v1_northstar_b65536(init, dl, oracle):
     with torch.no_grad():
         r = net.run(d["X"], keep_all=True)
     assert r.path == 1 and r.T is None
-    cols = pick_columns(B, 48, 10603)
+    cols = pick_columns(B, 1024, 10603)
     cidx = torch.from_numpy(cols).cuda()
     sd = {k: (v.index_select(1, cidx) if k.startswith("beta") else v).cpu().numpy()
           for k, v in net.state_dict().items()}
