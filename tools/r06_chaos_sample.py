@@ -11,9 +11,10 @@ seeds of its worst-layer err64 / (2 gap) and its layer-0 err64 / gap.
 
 Measured (r06, 5 seeds): worst-layer 0.37-0.42 on 65 columns, 0.37-0.48 on 1,040 columns;
 layer 0 at 0.52x the gap.  The device (test_v1_northstar_b65536[reference_default], 65
-columns) had layer 0 at 1.01x the gap and one layer (E[8]) at 1.03 of the bar: its MFMA f32
-rounding is not this exact-group model, and its drift sits closer to the bar than any CPU
-order restated here.
+columns) had layer 0 at 1.01x the gap and one layer (E[8]) at 1.03 of the bar; on 1,040
+columns its worst layer is at 0.56 of the bar.  Its MFMA f32 rounding is not this exact-group
+model and its drift sits a little closer to the bar than the CPU order restated here; the
+65-column failure was mostly the sample.
 
     python tools/r06_chaos_sample.py [--seeds 5]
 """
