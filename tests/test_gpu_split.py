@@ -83,8 +83,9 @@ def test_split_vs_oracle_baseline_shape(variant, B, dl, oracle):
 @pytest.mark.parametrize("shape", [(16, 32), (30, 70), (64, 256), (250, 500), (200, 512)])
 def test_split_padded_shapes(shape, dl, oracle):
     m, n = shape
-    for variant in ("v4", "v6"):
-        inp, sd, ref = _oracle_case(oracle, variant, m, n, 76, 5, seed=3000 + m)
+    for variant in ("v4", "v6", "v1"):   # V1: per-sample betas read past the last row as 0
+        inp, sd, ref = _oracle_case(oracle, variant, m, n, 76, 5, seed=3000 + m,
+                                    wscale=0.4 if variant == "v1" else None)
         net = split_net(dl, variant, inp, sd, 5)
         assert _path(dl, net, torch.from_numpy(inp["X"]).cuda()) == 4
         with torch.no_grad():
