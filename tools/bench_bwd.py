@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--layers", type=int, default=15)
+    ap.add_argument("--gz", action="store_true",
+                    help="per-layer Z cotangents (a loss built from the returned Z_k with torch "
+                         "ops, the reference's training loops) instead of the fused objective")
     ap.add_argument("--per-layer", action="store_true",
                     help="plan flag bwd_per_layer: the per-layer backward kernels")
     a = ap.parse_args()
@@ -51,6 +54,9 @@ def main():
                                loss_kind=L.LOSS_L1L1, **tables)
     coef = torch.tensor([[1e-3 / B, 1.0 / B]] * K, device=dev)
     kw = dict(loss_kind=L.LOSS_L1L1, loss_coef=coef, **tables)
+    if a.gz:
+        g = torch.Generator(device=dev).manual_seed(7)
+        kw = dict(gZ=[torch.randn(n, B, generator=g, device=dev) / B for _ in range(K)], **tables)
     libs = {}
     for spec in a.libs.split(","):
         L._LIB = None
@@ -73,7 +79,7 @@ def main():
             del res
     out = {s: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))}
            for s, t in times.items()}
-    out["config"] = dict(m=m, n=n, K=K, B=B, reps=a.reps, rev=not a.per_layer)
+    out["config"] = dict(m=m, n=n, K=K, B=B, reps=a.reps, rev=not a.per_layer, gz=a.gz)
     print(json.dumps(out))
 
 
