@@ -4,8 +4,12 @@
 // Per layer the LSKM forward evaluates, from the same state, a classic KM/LADMM step and a
 // learned (L2O) step, then one more KM step from the L2O candidate to form the fixed-point
 // residual S (test_syn_l1l1_scalar.py:160-178); those three steps are 1-layer calls of the fused
-// forward kernel.  This kernel does the rest, one batch column per thread (columns are
-// independent; a thread walks its column's rows, so a wave's loads are coalesced across columns):
+// forward kernel.  This kernel does the rest.  A workgroup owns 16 batch columns and splits
+// their rows over 16 row lanes (256 threads; a wave covers 16 columns x 4 rows, 64-B segments):
+// each lane sums every 16th row of its column, the 16 partial sums are added in lane order (a
+// fixed order: deterministic), one lane per column decides, and all 256 threads copy the chosen
+// candidate.  (Round 6: one thread per column walked all rows alone -- 494 us per call at
+// B = 1,000, half of the LSKM forward's GPU time; tools/prof_lskm.py.)
 //   |S|   = sqrt( sum_i (beta Ts_i)^2 + (c ((Es_i - 2 El_i) + Ep_i))^2 )      (:173-175, :124-126)
 //   keep  = |S| < (1 - delta) mu                                            (:232)
 //   mu    = updater(|S|, keep)                                              (mu_updater.py)
@@ -32,49 +36,70 @@ struct SafeguardArgs {
   float param;
 };
 
+constexpr int kSgCols = 16, kSgRows = 16;  // columns x row lanes of a workgroup (256 threads)
+
 __global__ __launch_bounds__(256) void safeguard_kernel(const SafeguardArgs a) {
-  const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  __shared__ double part[kSgRows][kSgCols];
+  __shared__ int keep_s[kSgCols];
+  const int tc = threadIdx.x % kSgCols, tr = threadIdx.x / kSgCols;
+  const int64_t col = (int64_t)blockIdx.x * kSgCols + tc;
   const bool cv = col < a.B;
-  int flag = 0;
+  double s = 0.0;
   if (cv) {
-    double s = 0.0;
-    for (int i = 0; i < a.m; ++i) {
+    for (int i = tr; i < a.m; i += kSgRows) {
       const int64_t o = (int64_t)i * a.ld + col;
       const float t = a.beta * a.Ts[o];
       const float e = a.c * ((a.Es[o] - 2.0f * a.El[o]) + a.Ep[o]);
       s += (double)t * t + (double)e * e;
     }
-    const float nrm = (float)sqrt(s);
-    const float mu0 = a.mu[col];
-    const bool keep = nrm < a.thresh * mu0;
-    float mu1 = mu0;
-    switch (a.updater) {
-      case DLADMM_MU_EMA: mu1 = keep ? a.param * nrm + (1.0f - a.param) * mu0 : mu0; break;
-      case DLADMM_MU_GS: mu1 = keep ? (1.0f - a.param) * mu0 : mu0; break;
-      case DLADMM_MU_RT: mu1 = keep ? nrm : mu0; break;
-      default: mu1 = 1e10f; break;  // BlankUpdater.step returns 10**10 (mu_updater.py:108-110)
-    }
-    if (a.norm_out) a.norm_out[col] = nrm;
-    if (!a.Zo) {  // initialisation: mu_0 = |S_0| (test_syn_l1l1_scalar.py:190-197)
-      a.mu[col] = nrm;
-      return;  // whole-grid uniform: no wave reaches the ballot below
-    }
-    a.mu[col] = mu1;
-    for (int i = 0; i < a.n; ++i) {
-      const int64_t o = (int64_t)i * a.ld + col;
-      a.Zo[o] = keep ? a.Zl[o] : a.Zk[o];
-    }
-    for (int i = 0; i < a.m; ++i) {
-      const int64_t o = (int64_t)i * a.ld + col;
-      a.Eo[o] = keep ? a.El[o] : a.Ek[o];
-      a.Lo[o] = keep ? a.Ll[o] : a.Lk[o];
-      a.To[o] = keep ? a.Tl[o] : a.Tk[o];
-    }
-    flag = keep ? 0 : 1;
   }
-  // one atomic per wave (integer: order-independent)
+  part[tr][tc] = s;
+  __syncthreads();
+  int flag = 0;
+  if (tr == 0) {
+    double t = 0.0;
+    for (int j = 0; j < kSgRows; ++j) t += part[j][tc];
+    bool keep = false;
+    if (cv) {
+      const float nrm = (float)sqrt(t);
+      const float mu0 = a.mu[col];
+      keep = nrm < a.thresh * mu0;
+      float mu1 = mu0;
+      switch (a.updater) {
+        case DLADMM_MU_EMA: mu1 = keep ? a.param * nrm + (1.0f - a.param) * mu0 : mu0; break;
+        case DLADMM_MU_GS: mu1 = keep ? (1.0f - a.param) * mu0 : mu0; break;
+        case DLADMM_MU_RT: mu1 = keep ? nrm : mu0; break;
+        default: mu1 = 1e10f; break;  // BlankUpdater.step returns 10**10 (mu_updater.py:108-110)
+      }
+      if (a.norm_out) a.norm_out[col] = nrm;
+      // initialisation (no outputs): mu_0 = |S_0| (test_syn_l1l1_scalar.py:190-197)
+      a.mu[col] = a.Zo ? mu1 : nrm;
+      flag = keep ? 0 : 1;
+    }
+    keep_s[tc] = keep ? 1 : 0;
+  }
+  if (!a.Zo) return;  // whole-grid uniform
+  __syncthreads();
+  // one atomic per workgroup (integer: order-independent); the deciding lanes are wave 0's
+  // first 16 threads
   const unsigned long long bal = __ballot(flag);
-  if ((threadIdx.x & 63) == 0 && bal) atomicAdd(a.count, (int)__popcll(bal));
+  if (threadIdx.x == 0 && bal) atomicAdd(a.count, (int)__popcll(bal));
+  if (!cv) return;
+  const bool keep = keep_s[tc] != 0;
+  const float* zs = keep ? a.Zl : a.Zk;
+  const float* es = keep ? a.El : a.Ek;
+  const float* ls = keep ? a.Ll : a.Lk;
+  const float* ts = keep ? a.Tl : a.Tk;
+  for (int i = tr; i < a.n; i += kSgRows) {
+    const int64_t o = (int64_t)i * a.ld + col;
+    a.Zo[o] = zs[o];
+  }
+  for (int i = tr; i < a.m; i += kSgRows) {
+    const int64_t o = (int64_t)i * a.ld + col;
+    a.Eo[o] = es[o];
+    a.Lo[o] = ls[o];
+    a.To[o] = ts[o];
+  }
 }
 
 }  // namespace dladmm
@@ -103,7 +128,8 @@ extern "C" int dladmm_safeguard_f32(const dladmm_safeguard_desc* d, void* stream
   a.mu = d->mu; a.norm_out = d->norm_out; a.count = d->count;
   a.beta = d->beta; a.c = d->c; a.thresh = (float)(1.0 - d->delta);  // python (1.0-delta)
   a.updater = d->updater; a.param = d->mu_param;
-  hipLaunchKernelGGL(safeguard_kernel, dim3((unsigned)((d->batch + 255) / 256)), dim3(256), 0,
+  hipLaunchKernelGGL(safeguard_kernel, dim3((unsigned)((d->batch + kSgCols - 1) / kSgCols)),
+                     dim3(256), 0,
                      (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }

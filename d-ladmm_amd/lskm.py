@@ -64,14 +64,19 @@ class DLADMMNetLSKM(DLADMMNetScalar):
             self._At_c = self.A.t().contiguous()
         return self._At_c
 
-    def _km(self, x, Z, E, L, K: int):
-        """K KM iterations from (Z, E, L) as one fused launch; T_0 = A Z + E - X."""
+    def _km(self, x, Z, E, L, K: int, table: Optional[torch.Tensor] = None):
+        """K KM iterations from (Z, E, L) as one fused launch; T_0 = A Z + E - X.  `table`: a
+        precomputed _km_table(K) (the safeguarded loop builds the 1-step table once per call)."""
         return dladmm_forward(_lib.V5_TIED, x, self.A, [self._At()] * K, Z, E, L, keep_all=True,
-                              want_T=True, scalar_params=self._km_table(K))
+                              want_T=True,
+                              scalar_params=self._km_table(K) if table is None else table)
 
-    def _l2o(self, x, Z, E, L, k: int, nl: int = 1):
-        """Learned layers k .. k+nl-1 (the V4 body, :206-227) from (Z, E, L)."""
-        tab = self._tables(self.A.device)["scalar_params"][k:k + nl].contiguous()
+    def _l2o(self, x, Z, E, L, k: int, nl: int = 1, tables: Optional[torch.Tensor] = None):
+        """Learned layers k .. k+nl-1 (the V4 body, :206-227) from (Z, E, L).  `tables`: the
+        module's parameter table, if the caller already assembled it for this call."""
+        if tables is None:
+            tables = self._tables(self.A.device)["scalar_params"]
+        tab = tables[k:k + nl].contiguous()
         return dladmm_forward(_lib.V4_SCALAR, x, self.A,
                               [self.fc[j].weight.detach() for j in range(k, k + nl)], Z, E, L,
                               keep_all=True, want_T=True, scalar_params=tab)
@@ -149,14 +154,17 @@ class DLADMMNetLSKM(DLADMMNetScalar):
                 count = torch.zeros(self.layers, dtype=torch.int32, device=dev)
                 mu = torch.empty(B, device=dev)
                 # mu_0 = |S(Z0, E0, L0, T0, X, E0)| (:190-197); T0 = A Z0 + E0 - X
-                s0 = self._km(x, self.Z0, self.E0, self.L0, 1)
+                # the parameter tables of this call, assembled once (not per layer)
+                km1 = self._km_table(1)
+                ptab = self._tables(dev)["scalar_params"]
+                s0 = self._km(x, self.Z0, self.E0, self.L0, 1, km1)
                 To[0].copy_(s0.T[0])
                 self._safeguard(x, mu, None, None, s0, self.E0, None, 0, None)
                 Zc, Ec, Lc = self.Z0, self.E0, self.L0
                 for k in range(nl):
-                    cl = self._l2o(x, Zc, Ec, Lc, k)                       # :218-227
-                    ck = self._km(x, Zc, Ec, Lc, 1)                        # :215-216
-                    cs = self._km(x, cl.Z[0], cl.E[0], cl.L[0], 1)         # S(L2O, Ep) :244
+                    cl = self._l2o(x, Zc, Ec, Lc, k, tables=ptab)          # :218-227
+                    ck = self._km(x, Zc, Ec, Lc, 1, km1)                   # :215-216
+                    cs = self._km(x, cl.Z[0], cl.E[0], cl.L[0], 1, km1)    # S(L2O, Ep) :244
                     self._safeguard(x, mu, cl, ck, cs, Ec, (Zo, Eo, Lo, To), k, count[k:k + 1])
                     Zc, Ec, Lc = Zo[k], Eo[k], Lo[k]
                 Z, E, L, T = list(Zo), list(Eo), list(Lo), list(To)
