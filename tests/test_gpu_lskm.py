@@ -65,3 +65,25 @@ def test_km_ground_truth_depth(dl):
     for k in (0, 9, 99, 1999):
         assert nrel(Z[k].cpu().numpy(), ref["Z"][k]) <= 1e-4, k
         assert nrel(E[k].cpu().numpy(), ref["E"][k]) <= 1e-4, k
+
+
+@pytest.mark.parametrize("B", [300, 1037])
+def test_safeguard_many_columns(B, dl):
+    """The safeguard kernel's workgroups of 16 columns x 16 row lanes (row sums in a fixed lane
+    order) over many workgroups and a ragged last one, at the test script's m = 250, n = 500:
+    safeguard counts and the selected outputs against the oracle's safeguarded forward."""
+    from oracle import dladmm_oracle_lskm as ol
+    d = dict(variant="v4", m=250, n=500, B=B, K=5, seed=1190 + B, perturb=0.2, wscale=0.9)
+    inp, sd = P.build_problem(d)
+    case = dict(layers=5, alpha=0.01, delta=0.05, mu="EMA", mu_param=0.5)
+    net = make(dl, case, inp, sd)
+    X = torch.from_numpy(inp["X"]).cuda()
+    Z, E, L, T, cnt = net(X, True, True, False)
+    ref = ol.lskm_forward(inp["X"], inp["A"], inp["Z0"], inp["E0"], inp["L0"], sd, 5, True,
+                          True, False, 5, 0.01, delta=0.05, mu_method="EMA", mu_param=0.5)
+    np.testing.assert_array_equal(cnt, ref["sg_count"])
+    assert 0 < ref["sg_count"].sum() < 5 * B   # both branches taken
+    for k in range(5):
+        assert nrel(Z[k].cpu().numpy(), ref["Z"][k]) <= 1e-5, k
+        assert nrel(E[k].cpu().numpy(), ref["E"][k]) <= 1e-5, k
+        assert nrel(T[k + 1].cpu().numpy(), ref["T"][k + 1]) <= 1e-5, k

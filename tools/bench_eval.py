@@ -55,6 +55,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--per-layer", action="store_true",
+                    help="also the KM lines on the per-layer kernels (plan flag per_layer)")
     a = ap.parse_args()
     dl = importlib.import_module("d-ladmm_amd")
     obj = importlib.import_module("d-ladmm_amd.objectives")
@@ -66,13 +68,18 @@ def main():
                            layers=LAYERS, alpha=ALPHA, mu_k_method="EMA", mu_k_param=0.5)
     net.cuda()
 
-    def km_line(B):
+    ops = importlib.import_module("d-ladmm_amd.ops")
+
+    def km_line(B, per_layer=False):
         nb = dl.DLADMMNetLSKM(m=M, n=0, d=N, batch_size=B, A=A, Z0=Z0[:, :B].contiguous(),
                               E0=E0[:, :B].contiguous(), L0=L0[:, :B].contiguous(),
                               layers=LAYERS, alpha=ALPHA)
         nb.cuda()
         xb = X[:, :B].contiguous()
-        ms, runs = timed(lambda: nb(xb, False, False, False, K=KGT), a.reps)
+        def call():
+            with ops.plan_flags(per_layer=per_layer):
+                return nb(xb, False, False, False, K=KGT)
+        ms, runs = timed(call, a.reps)
         flop = (4 * KGT + 2) * M * N * B
         return {"ms_per_call": ms, "runs_ms": runs, "samples_per_s": B / ms * 1e3,
                 "tflops": flop / ms / 1e9, "frac_fp32_mfma": flop / ms / 1e-3 / PEAK,
@@ -81,6 +88,9 @@ def main():
     res["km_gt_b20"] = km_line(20)
     res["km_gt_b20"]["test_pass_s"] = res["km_gt_b20"]["ms_per_call"] * 50 / 1e3
     res["km_gt_b1000"] = km_line(1000)
+    if a.per_layer:
+        res["km_gt_b20_per_layer"] = km_line(20, True)
+        res["km_gt_b1000_per_layer"] = km_line(1000, True)
     ms, runs = timed(lambda: net(X, True, True, False), a.reps)
     res["lskm_sg_b1000"] = {"ms_per_call": ms, "runs_ms": runs, "samples_per_s": 1000 / ms * 1e3,
                             "layers": LAYERS, "mu": "EMA 0.5"}
