@@ -324,7 +324,7 @@ inline int pick_shape(int m, int n) {
 inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 
 struct Plan {
-  int path;  // 1 fused, 2 per-layer, 3 bf16 tiles, 4 fused split-f16
+  int path;  // 1 fused, 2 per-layer, 3 bf16 tiles, 4 fused split-f16, 5 fused row-split
   // fused
   int shape, MP, NP, tiles;
   // per-layer
@@ -403,6 +403,28 @@ inline bool shared_weight(const dladmm_fwd_desc* d) {
 // to whole 32-column sub-chunks), unless fwd.flags holds DLADMM_F_WGRAD_F32
 inline bool use_wgrad_x3(bool x3w, const WgradArgs& wa) { return x3w && wgrad_x3_fits(wa); }
 
+// CUs of the current device (cached; the plan is host-only)
+inline int device_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+
+// Path 5: the fused kernel's arithmetic with each workgroup's 16 columns' rows split over its 4
+// waves, where the fused kernel's 64-column workgroups would leave most CUs idle -- a batch that
+// needs at most one 16-column workgroup per CU.  Inference only (no fused objective, no saved
+// product); DLADMM_F_NO_ROWSPLIT keeps path 1.
+inline bool use_rowsplit(const dladmm_fwd_desc* d, int shape) {
+  return rs_supports(shape, d->variant) && d->precision == DLADMM_PREC_F32 &&
+         d->loss_kind == 0 && !d->col_loss && !d->P && !(d->flags & DLADMM_F_NO_ROWSPLIT) &&
+         ceil_div(d->batch, 16) <= device_cus();
+}
+
 inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
   *p = Plan{};
   const int s = pick_shape(d->m, d->n);
@@ -438,7 +460,7 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
     return 0;
   }
   if (s >= 0 && fits_32bit(d) && !force_layered && !bf16) {
-    p->path = 1;
+    p->path = use_rowsplit(d, s) ? 5 : 1;
     p->shape = s;
     p->MP = kShapeMP[s];
     p->NP = kShapeNP[s];
@@ -575,9 +597,11 @@ inline int run_fused(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStrea
   if (d->ev_kernel_start) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_start, s)) return (int)e;
   }
-  if (hipError_t e = (savep ? launch_fused_shape_savep : launch_fused_shape)(p.shape, d->variant,
-                                                                          a, p.tiles, s))
-    return (int)e;
+  hipError_t e = p.path == 5
+                    ? launch_fused_rs(p.shape, d->variant, a, ceil_div(d->batch, 16), s)
+                    : (savep ? launch_fused_shape_savep : launch_fused_shape)(p.shape, d->variant,
+                                                                             a, p.tiles, s);
+  if (e) return (int)e;
   if (d->ev_kernel_stop) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_stop, s)) return (int)e;
   }
@@ -1436,7 +1460,7 @@ int dladmm_fwd_f32(const dladmm_fwd_desc* d, void* stream) {
   if (((uintptr_t)d->workspace) & 255) return DLADMM_E_ALIGN;
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)d->workspace;
-  const int rc = p.path == 1   ? run_fused(d, p, ws, s)
+  const int rc = p.path == 1 || p.path == 5 ? run_fused(d, p, ws, s)
                  : p.path == 4 ? run_fused_x3(d, p, ws, s)
                                : run_layered(d, p, ws, s);
   if (rc) return rc;

@@ -48,6 +48,10 @@ hipError_t launch_fused_shape(int shape, int variant, const FusedArgs& a, int gr
 // the same kernels that also store P_k = A Z_k (a.Po) for the backward (dladmm_fused_savep.hip)
 hipError_t launch_fused_shape_savep(int shape, int variant, const FusedArgs& a, int grid,
                                     hipStream_t s);
+// small-batch row-split form of the fused kernel (path 5, dladmm_fused_rs.hip): 16 columns per
+// workgroup, grid = ceil(B / 16)
+bool rs_supports(int shape, int variant);
+hipError_t launch_fused_rs(int shape, int variant, const FusedArgs& a, int grid, hipStream_t s);
 // split-f16 fused kernel (DLADMM_PREC_F32_SPLIT); Ap / Wp hold [step][hi|lo] f16 fragments
 bool x3_supports(int variant);
 hipError_t launch_fused_x3_shape(int shape, int variant, const FusedArgs& a, int grid,

@@ -67,8 +67,11 @@ def column_terms(Z, E=None, T=None, Zref=None, Eref=None, fit_kind: str = "l1l1"
     m = E[0].shape[0] if E is not None else 1
     out = {w: torch.empty((K, B), device=dev, dtype=torch.float64) for w in want}
     groups = [(0, K)]
+    # T: exactly the views the launch below reads (T_0 .. T_K: layer k reads T_{k+1} at one
+    # layer stride from T_0), not just T_1.. -- separately allocated tensors may happen to be
+    # equally spaced from T_1 on while T_0 is not
     stacks = [_stack(Z), _stack(E) if E is not None else (None, 0, 0),
-              _stack(T[1:]) if T is not None else (None, 0, 0)]
+              _stack(T[:K + 1]) if T is not None else (None, 0, 0)]
     if any(s is None for s in stacks):
         groups = [(k, k + 1) for k in range(K)]   # not one allocation: one launch per layer
     stream = torch.cuda.current_stream(dev).cuda_stream

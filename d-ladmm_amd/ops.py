@@ -35,7 +35,8 @@ class ForwardResult:
 _PLAN_FLAGS = contextvars.ContextVar("dladmm_plan_flags", default=0)
 _FLAG_NAMES = {"per_layer": _lib.F_PER_LAYER, "bf16_wide": _lib.F_BF16_WIDE,
                "bwd_per_layer": _lib.F_BWD_PER_LAYER, "bwd_unfused": _lib.F_BWD_UNFUSED,
-               "bwd_no_zmask": _lib.F_BWD_NO_ZMASK, "wgrad_f32": _lib.F_WGRAD_F32}
+               "bwd_no_zmask": _lib.F_BWD_NO_ZMASK, "wgrad_f32": _lib.F_WGRAD_F32,
+               "no_rowsplit": _lib.F_NO_ROWSPLIT}
 
 
 @contextlib.contextmanager
@@ -211,7 +212,8 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
         raise ValueError(f"dladmm: precision must be one of {sorted(_PRECISIONS)}, "
                          f"got {precision!r}")
     d.precision = _PRECISIONS[precision]
-    if want_P and keep_all and out.P is None and L.dladmm_fwd_path(ctypes.byref(d)) in (1, 4):
+    # (path 5, the small-batch row-split kernel, saves no product: with P set the plan is path 1)
+    if want_P and keep_all and out.P is None and L.dladmm_fwd_path(ctypes.byref(d)) in (1, 4, 5):
         out.P = torch.empty((K, m, B), device=dev, dtype=torch.float32)
         d.P = out.P.data_ptr()
     if want_col_loss:

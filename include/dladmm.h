@@ -179,7 +179,9 @@ enum dladmm_flags {
                                   launch instead of inside BK3's (bit-identical)                   */
   DLADMM_F_BWD_NO_ZMASK = 16,  /* per-layer backward, V2 / V3: form q = W_k Var_k in BK2 instead of
                                   reading the shrink masks off the saved Z_k                       */
-  DLADMM_F_WGRAD_F32 = 32      /* split-f16 backward: the weight gradient on the fp32-MFMA kernel  */
+  DLADMM_F_WGRAD_F32 = 32,     /* split-f16 backward: the weight gradient on the fp32-MFMA kernel  */
+  DLADMM_F_NO_ROWSPLIT = 64    /* forward: the fused kernel (path 1) where the small-batch
+                                  row-split kernel (path 5) would run (equivalence tests, A/B)    */
 };
 
 /* ABI version the library was built with. */
@@ -191,7 +193,10 @@ size_t dladmm_fwd_workspace_bytes(const dladmm_fwd_desc* d);
 /* Which kernel path this descriptor takes: 1 = fused persistent K-layer kernel,
    2 = per-layer kernel pair (large shapes, or one layer's matrix >= 2^31 bytes), 3 = per-layer
    tile kernels on bf16 operands, 4 = fused kernel on split-f16 operands (DLADMM_PREC_F32_SPLIT),
-   <0 = DLADMM_E_* error.  Host-only: no device work. */
+   5 = fused kernel with each workgroup's rows split over its waves (16 columns per workgroup):
+   small fp32 batches (at most one workgroup per CU) of V4 / V5 / V6 at m <= 256, n <= 512 (and
+   m > 64 or n > 256), inference without loss_kind or P -- the same arithmetic as path 1, bit for
+   bit; <0 = DLADMM_E_* error.  Host-only: no device work. */
 int dladmm_fwd_path(const dladmm_fwd_desc* d);
 
 /* Enqueue the whole K-layer forward on `stream` (hipStream_t). */

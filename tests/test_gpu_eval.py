@@ -206,3 +206,24 @@ def test_objectives_end_to_end_match_reference(name, dl):
                 gt = (Zp[-1], Ep[-1], Tp[-1])
         batches.append((Z, E, L, T, gt))
     _check(_run_evaluators(dl, c, inp, net, batches), g, 1e-4, name)
+
+
+def test_column_terms_layouts(dl):
+    """objectives.column_terms on every layout the evaluator can meet: one allocation for all
+    layers, separately allocated layers, and T_1..T_K one allocation with T_0 apart (T_1.. equally
+    spaced while T_0 is not must not be taken for one stacked view): same values each time."""
+    obj = importlib.import_module("d-ladmm_amd.objectives")
+    g = torch.Generator(device="cuda").manual_seed(9)
+    K, m, n, B = 4, 32, 64, 20
+    Zs = torch.randn(K, n, B, generator=g, device="cuda")
+    Es = torch.randn(K, m, B, generator=g, device="cuda")
+    Ts = torch.randn(K + 1, m, B, generator=g, device="cuda")
+    ref = obj.column_terms(list(Zs), list(Es), list(Ts), want=("reg", "fit"))
+    layouts = {
+        "separate": ([z.clone() for z in Zs], [e.clone() for e in Es], [t.clone() for t in Ts]),
+        "T0 apart": (list(Zs), list(Es), [Ts[0].clone()] + list(Ts[1:])),
+    }
+    for name, (Z, E, T) in layouts.items():
+        got = obj.column_terms(Z, E, T, want=("reg", "fit"))
+        for w in ("reg", "fit"):
+            assert torch.equal(got[w], ref[w]), (name, w)

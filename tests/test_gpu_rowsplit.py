@@ -1,0 +1,129 @@
+"""Path 5, the small-batch row-split form of the fused forward (csrc/dladmm_fused_rs.hip): a
+workgroup per 16 batch columns, each product's output rows split over its 4 waves.
+
+It performs the fused kernel's arithmetic operation for operation, so its outputs must equal
+path 1's (plan flag no_rowsplit) BIT FOR BIT -- every layer's Z, E, L and T -- for V4, V5 (and
+the KM iteration of the test scripts built on V5) and V6, at ragged batches and shapes, lean and
+keep_all; one case is also checked against the oracle at the fp32 bar directly.  The plan takes
+path 5 only where it applies (inference at the 256 x 512 shape, no fused objective, no saved
+product, at most one 16-column workgroup per CU)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import parity
+import problems as P
+from test_gpu_parity import _compare, _oracle_case
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(dl, variant, inp, sd, K, keep_all=True, flags=0, **kw):
+    ops = dl.ops
+    L = dl._lib
+    m, n = inp["A"].shape
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    cls = dl.VARIANTS[variant]
+    net = cls(m=m, n=0, d=n, batch_size=inp["X"].shape[1], A=t(inp["A"]), Z0=t(inp["Z0"]),
+              E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    net.cuda().requires_grad_(False)
+    X = t(inp["X"])
+    with torch.no_grad():
+        tables = net._tables(X.device)
+        W = [w.detach() for w in net._weights()]
+        r = ops.dladmm_forward(net.VARIANT, X, net.A, W, net.Z0, net.E0, net.L0,
+                               keep_all=keep_all, want_T=True, flags=flags,
+                               scalar_params=tables["scalar_params"], **kw)
+    torch.cuda.synchronize()
+    return r
+
+
+@pytest.mark.parametrize("variant", ["v4", "v5", "v6"])
+@pytest.mark.parametrize("B", [1, 20, 77, 300, 1000])
+def test_rowsplit_bit_equal_to_fused(variant, B, dl):
+    m, n, K = 250, 500, 6
+    d = dict(variant=variant, m=m, n=n, B=B, K=K, seed=5100 + B, perturb=0.2,
+             wscale=P.VARIANT_SPECS[variant]["wscale"])
+    inp, sd = P.build_problem(d)
+    rs = _run(dl, variant, inp, sd, K)
+    fu = _run(dl, variant, inp, sd, K, flags=dl._lib.F_NO_ROWSPLIT)
+    assert rs.path == 5 and fu.path == 1
+    for nm in ("Z", "E", "L", "T"):
+        a, b = getattr(rs, nm), getattr(fu, nm)
+        assert a.shape == b.shape, nm
+        assert torch.equal(a, b), (nm, float((a - b).abs().max()))
+
+
+@pytest.mark.parametrize("shape", [(256, 512), (100, 300), (65, 257)])
+def test_rowsplit_shapes_and_lean_mode(shape, dl):
+    """Ragged m / n inside the 256 x 512 instantiation (padded rows stay zero), lean mode (last
+    layer only), against path 1 bit for bit."""
+    m, n = shape
+    K, B = 4, 45
+    d = dict(variant="v4", m=m, n=n, B=B, K=K, seed=5200 + m, perturb=0.2, wscale=0.4)
+    inp, sd = P.build_problem(d)
+    for keep_all in (True, False):
+        rs = _run(dl, "v4", inp, sd, K, keep_all=keep_all)
+        fu = _run(dl, "v4", inp, sd, K, keep_all=keep_all, flags=dl._lib.F_NO_ROWSPLIT)
+        assert rs.path == 5 and fu.path == 1
+        for nm in ("Z", "E", "L", "T"):
+            assert torch.equal(getattr(rs, nm), getattr(fu, nm)), (keep_all, nm)
+
+
+def test_rowsplit_vs_oracle(dl, oracle):
+    """Independent of path 1: the oracle at the fp32 bar, V4 at m=250 n=500 K=15, B=100."""
+    m, n, K, B = 250, 500, 15, 100
+    inp, sd, ref = _oracle_case(oracle, "v4", m, n, B, K, seed=5300)
+    r = _run(dl, "v4", inp, sd, K)
+    assert r.path == 5
+    _compare((list(r.Z), list(r.E), list(r.L), list(r.T)), ref, tag="rowsplit v4 B=100",
+             path="f32")
+
+
+def test_km_ground_truth_on_rowsplit(dl):
+    """The test scripts' KM ground truth (V5, W = A^T shared, K iterations) at m=250 n=500, B=20:
+    path 5 equals path 1 bit for bit over 300 iterations."""
+    from test_gpu_lskm import make
+    d = dict(variant="v4", m=250, n=500, B=20, K=3, seed=5400, perturb=0.1)
+    inp, sd = P.build_problem(d)
+    case = dict(layers=3, alpha=0.01, delta=-99.0, mu="None", mu_param=0.0)
+    net = make(dl, case, inp, sd)
+    X = torch.from_numpy(inp["X"]).cuda()
+    ops = dl.ops
+    Z, E, L, T = net(X, False, False, False, K=300)
+    with ops.plan_flags(no_rowsplit=True):
+        Zf, Ef, Lf, Tf = net(X, False, False, False, K=300)
+    for a, b in zip(Z + E + L + T, Zf + Ef + Lf + Tf):
+        assert torch.equal(a, b)
+
+
+def test_rowsplit_plan_scope(dl):
+    """Path 5 only for inference without a fused objective or saved product, at batches of at
+    most one 16-column workgroup per CU, for V4 / V5 / V6 at the 256 x 512 shape."""
+    L = dl._lib
+    lib = L.lib()
+    m, n, K = 250, 500, 3
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+
+    def path(variant="v4", B=64, loss=0, P_=False, mn=(m, n)):
+        d = dict(variant=variant, m=mn[0], n=mn[1], B=B, K=K, seed=5500, perturb=0.1)
+        inp, sd = P.build_problem(d)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+        cls = dl.VARIANTS[variant]
+        net = cls(m=mn[0], n=0, d=mn[1], batch_size=B, A=t(inp["A"]), Z0=t(inp["Z0"]),
+                  E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K).cuda()
+        r = dl.ops.dladmm_forward(net.VARIANT, t(inp["X"]), net.A,
+                                  [w.detach() for w in net._weights()], net.Z0, net.E0, net.L0,
+                                  loss_kind=loss, want_P=P_, **net._tables(net.A.device))
+        return r.path
+    assert path() == 5
+    assert path(variant="v5") == 5 and path(variant="v6") == 5
+    assert path(B=16 * cus) == 5
+    assert path(B=16 * cus + 1) == 1
+    assert path(loss=L.LOSS_L1L1) == 1
+    assert path(P_=True) == 1
+    assert path(variant="v1") == 1
+    assert path(mn=(64, 128)) == 1   # the 64 x 256 instantiation: whole-row waves

@@ -55,6 +55,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--ab", action="store_true",
+                    help="also the KM lines on path 1 (plan flag no_rowsplit) and at B = 4,096")
     ap.add_argument("--per-layer", action="store_true",
                     help="also the KM lines on the per-layer kernels (plan flag per_layer)")
     a = ap.parse_args()
@@ -63,21 +65,22 @@ def main():
     dev = torch.device("cuda", 0)
     res = {}
     torch.manual_seed(1126)
-    A, X, Z0, E0, L0 = bench.synth(M, N, 1000, 0, dev)
+    A, X4, Z04, E04, L04 = bench.synth(M, N, 4096, 0, dev)   # the KM lines take B columns
+    X, Z0, E0, L0 = (t[:, :1000].contiguous() for t in (X4, Z04, E04, L04))
     net = dl.DLADMMNetLSKM(m=M, n=0, d=N, batch_size=1000, A=A, Z0=Z0, E0=E0, L0=L0,
                            layers=LAYERS, alpha=ALPHA, mu_k_method="EMA", mu_k_param=0.5)
     net.cuda()
 
     ops = importlib.import_module("d-ladmm_amd.ops")
 
-    def km_line(B, per_layer=False):
-        nb = dl.DLADMMNetLSKM(m=M, n=0, d=N, batch_size=B, A=A, Z0=Z0[:, :B].contiguous(),
-                              E0=E0[:, :B].contiguous(), L0=L0[:, :B].contiguous(),
+    def km_line(B, per_layer=False, no_rowsplit=False):
+        nb = dl.DLADMMNetLSKM(m=M, n=0, d=N, batch_size=B, A=A, Z0=Z04[:, :B].contiguous(),
+                              E0=E04[:, :B].contiguous(), L0=L04[:, :B].contiguous(),
                               layers=LAYERS, alpha=ALPHA)
         nb.cuda()
-        xb = X[:, :B].contiguous()
+        xb = X4[:, :B].contiguous()
         def call():
-            with ops.plan_flags(per_layer=per_layer):
+            with ops.plan_flags(per_layer=per_layer, no_rowsplit=no_rowsplit):
                 return nb(xb, False, False, False, K=KGT)
         ms, runs = timed(call, a.reps)
         flop = (4 * KGT + 2) * M * N * B
@@ -88,6 +91,11 @@ def main():
     res["km_gt_b20"] = km_line(20)
     res["km_gt_b20"]["test_pass_s"] = res["km_gt_b20"]["ms_per_call"] * 50 / 1e3
     res["km_gt_b1000"] = km_line(1000)
+    if a.ab:   # the same calls on path 1 (the fused kernel's 64-column workgroups)
+        res["km_gt_b20_fused"] = km_line(20, no_rowsplit=True)
+        res["km_gt_b1000_fused"] = km_line(1000, no_rowsplit=True)
+        res["km_gt_b4096"] = km_line(4096)
+        res["km_gt_b4096_fused"] = km_line(4096, no_rowsplit=True)
     if a.per_layer:
         res["km_gt_b20_per_layer"] = km_line(20, True)
         res["km_gt_b1000_per_layer"] = km_line(1000, True)
