@@ -416,13 +416,14 @@ inline int device_cus() {
 }
 
 // Path 5: the fused kernel's arithmetic with each workgroup's 16 columns' rows split over its 4
-// waves, where the fused kernel's 64-column workgroups would leave most CUs idle -- a batch that
-// needs at most one 16-column workgroup per CU.  Inference only (no fused objective, no saved
-// product); DLADMM_F_NO_ROWSPLIT keeps path 1.
+// waves, where the fused kernel's 64-column workgroups would leave most CUs idle -- a batch of at
+// most two 16-column workgroups per CU (KM ground truth, m = 250, n = 500: 22 / 39 us per step
+// at one / two per CU against path 1's 67; profiles/r06_rowsplit_ab.json).  Inference only (no
+// fused objective, no saved product); DLADMM_F_NO_ROWSPLIT keeps path 1.
 inline bool use_rowsplit(const dladmm_fwd_desc* d, int shape) {
   return rs_supports(shape, d->variant) && d->precision == DLADMM_PREC_F32 &&
          d->loss_kind == 0 && !d->col_loss && !d->P && !(d->flags & DLADMM_F_NO_ROWSPLIT) &&
-         ceil_div(d->batch, 16) <= device_cus();
+         ceil_div(d->batch, 16) <= 2 * device_cus();
 }
 
 inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {

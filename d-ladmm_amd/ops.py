@@ -28,7 +28,7 @@ class ForwardResult:
     col_loss: Optional[torch.Tensor] = None  # [K, 2, B] fp32 per-column terms (want_col_loss)
     P: Optional[torch.Tensor] = None  # [K, m, B] A Z_k per layer (want_P: training forwards)
     path: int = 0  # dladmm_fwd_path: the kernel path that ran (1 fused, 2 per-layer, 3 bf16
-                   # tiles, 4 fused split-f16; 0 = nothing launched)
+                   # tiles, 4 fused split-f16, 5 fused row-split; 0 = nothing launched)
     flags: int = 0  # the plan options (dladmm_flags) the forward ran with; its backward keeps them
 
 

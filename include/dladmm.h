@@ -194,7 +194,7 @@ size_t dladmm_fwd_workspace_bytes(const dladmm_fwd_desc* d);
    2 = per-layer kernel pair (large shapes, or one layer's matrix >= 2^31 bytes), 3 = per-layer
    tile kernels on bf16 operands, 4 = fused kernel on split-f16 operands (DLADMM_PREC_F32_SPLIT),
    5 = fused kernel with each workgroup's rows split over its waves (16 columns per workgroup):
-   small fp32 batches (at most one workgroup per CU) of V4 / V5 / V6 at m <= 256, n <= 512 (and
+   small fp32 batches (at most two workgroups per CU) of V4 / V5 / V6 at m <= 256, n <= 512 (and
    m > 64 or n > 256), inference without loss_kind or P -- the same arithmetic as path 1, bit for
    bit; <0 = DLADMM_E_* error.  Host-only: no device work. */
 int dladmm_fwd_path(const dladmm_fwd_desc* d);
