@@ -348,15 +348,15 @@ def main():
         cfg3 = dict(value=262144 * a.steps / c_el, ms_per_step=c_el / a.steps * 1e3,
                     kern=c_kern, kerns=c_kerns, B=w3.B, obj=float(c_obj.cpu().numpy()[-1]))
         del w3
-    # BASELINE config 2 (V4, B = 10,000 on one GPU) beside the headline at N = 1: 625 sixteen-
-    # column units on 1,024 SIMDs
+    # BASELINE config 2 (V4, B = 10,000 on one GPU) beside the headline at N = 1: on path 5 (the
+    # row-split fused kernel, 625 workgroups of 16 columns)
     cfg2 = None
     if world == 1 and not strong and not a.no_cfg3 and a.variant == "v4" and \
             a.precision == "f32" and (m, n, K) == (256, 512, 15) and B != 10000:
         w2 = Workload(dl, a, m, n, K, 10000, 10000, None, rank, dev, rank)
         c_el, c_kern, _, c_obj = timed(w2, "f32")
         cfg2 = dict(value=10000 * a.steps / c_el, ms_per_step=c_el / a.steps * 1e3, kern=c_kern,
-                    obj=float(c_obj.cpu().numpy()[-1]))
+                    obj=float(c_obj.cpu().numpy()[-1]), path=w2.path)
         if not a.no_split:   # the same batch on the split-f16 kernel (same fp32 tolerances)
             s_el, s_kern, _, _ = timed(w2, "f32_split")
             cfg2["split"] = (10000 * a.steps / s_el, s_el / a.steps * 1e3, s_kern, w2.path)
@@ -532,8 +532,10 @@ def main():
                 "value": cfg2["value"], "unit": "samples/s", "ms_per_step": cfg2["ms_per_step"],
                 "kernel_ms": cfg2["kern"] * 1e3,
                 "roofline_frac": f2 / cfg2["kern"] / PEAK_F32_MFMA,
-                "note": "625 sixteen-column units on 1,024 SIMDs: at most 61 % of the chip busy "
-                        "(DESIGN.md section 12)",
+                "path": {1: "fused", 5: "fused row-split"}.get(cfg2["path"], cfg2["path"]),
+                "note": "path 5: 625 workgroups of 16 columns, each product's output rows split "
+                        "over the 4 waves (the fused kernel's 64-column workgroups fill 157 of "
+                        "the 256 CUs; DESIGN.md sections 12, 13.3b)",
                 "objective_last_layer": cfg2["obj"],
             }
             if "split" in cfg2:

@@ -417,13 +417,19 @@ inline int device_cus() {
 
 // Path 5: the fused kernel's arithmetic with each workgroup's 16 columns' rows split over its 4
 // waves, where the fused kernel's 64-column workgroups would leave most CUs idle -- a batch of at
-// most two 16-column workgroups per CU (KM ground truth, m = 250, n = 500: 22 / 39 us per step
-// at one / two per CU against path 1's 67; profiles/r06_rowsplit_ab.json).  Inference only (no
-// fused objective, no saved product); DLADMM_F_NO_ROWSPLIT keeps path 1.
+// most three 16-column workgroups per CU (KM ground truth, m = 250, n = 500: 22 / 39 us per step
+// at one / two per CU against path 1's 67), e.g. the reference training loops' batches of
+// 20 / 25 and BASELINE config 2.  DLADMM_F_NO_ROWSPLIT keeps path 1.
+#ifndef DLADMM_RS_PER_CU
+#define DLADMM_RS_PER_CU 3  // path 5 up to this many 16-column workgroups per CU: V4 K = 15
+                            // with the fused objective, path 5 vs path 1 (ms): B = 4,096 0.52 /
+                            // 1.08, 8,192 0.72 / 1.10, 10,000 0.94 / 1.12 (3 per CU), 16,384
+                            // 1.28 / 1.17 (profiles/r06_rowsplit_ab.json)
+#endif
 inline bool use_rowsplit(const dladmm_fwd_desc* d, int shape) {
   return rs_supports(shape, d->variant) && d->precision == DLADMM_PREC_F32 &&
-         d->loss_kind == 0 && !d->col_loss && !d->P && !(d->flags & DLADMM_F_NO_ROWSPLIT) &&
-         ceil_div(d->batch, 16) <= 2 * device_cus();
+         !(d->flags & DLADMM_F_NO_ROWSPLIT) &&
+         ceil_div(d->batch, 16) <= DLADMM_RS_PER_CU * device_cus();
 }
 
 inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
@@ -466,7 +472,8 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
     p->MP = kShapeMP[s];
     p->NP = kShapeNP[s];
     p->tiles = ceil_div(d->batch, kTileCols);
-    p->ldl = p->tiles * kTileCols;
+    // per-column objective slots: every column the grid covers (64 / 16 per workgroup)
+    p->ldl = p->path == 5 ? ceil_div(d->batch, 16) * 16 : p->tiles * kTileCols;
     p->nslots = p->ldl;  // one slice
     const size_t frag_bytes = (size_t)p->MP * p->NP * sizeof(float);
     p->off_ap = 0;
@@ -879,7 +886,8 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   if (int e = make_plan(&f32, &p->fwd)) return e;
   p->x3w = f.precision == DLADMM_PREC_F32_SPLIT && !bwd_flag(f, DLADMM_F_WGRAD_F32);
   // the forward stored A Z_k only on the fused paths, fp32 and split-f16 (fwd_desc.P)
-  p->saved_p = f.P != nullptr && f.keep_all && (p->fwd.path == 1 || p->fwd.path == 4);
+  p->saved_p = f.P != nullptr && f.keep_all &&
+               (p->fwd.path == 1 || p->fwd.path == 4 || p->fwd.path == 5);
   const int m = f.m, n = f.n;
   const int64_t B = f.batch;
   p->MB = ceil_div(m, 16);

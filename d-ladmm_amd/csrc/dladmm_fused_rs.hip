@@ -15,10 +15,12 @@
 // Arithmetic is the fused kernel's, operation for operation: the same packed -W_k / A fragments
 // (pack order 2), G1 one fma chain per output block over k in order, G2 two chains (k sub-steps
 // x, z and y, w) summed once, the same elementwise expressions -- so the outputs are the fused
-// kernel's bit for bit (tests/test_gpu_rowsplit.py).  Scope: the scalar-parameter variants V4,
-// V5 (and the KM iteration built on it), V6 at the 256 x 512 register shape, inference (no
-// fused objective, no saved product); the plan (dladmm_capi.hip) picks it for batches that
-// leave most CUs idle on the fused kernel.
+// kernel's bit for bit (tests/test_gpu_rowsplit.py), the saved products P_k = A Z_k of a
+// training forward too.  The fused per-column objective is the same sum in another order (each
+// wave sums its quarter of the rows, then the 4 quarters in wave order): equal to fp32 rounding.
+// Scope: V1 (per-sample betas), V4, V5 (and the KM iteration built on it), V6 at the 256 x 512
+// register shape; the plan (dladmm_capi.hip) picks it for batches that leave most CUs idle on
+// the fused kernel.
 #include "dladmm_internal.h"
 
 #ifndef RS_PF
@@ -35,8 +37,10 @@ __global__ __launch_bounds__(256, 1) void fused_rs_kernel(const FusedArgs a) {
   constexpr int NB4 = NB / kWaves, MB4 = MB / kWaves;  // output blocks per wave
   static_assert(NB4 % 2 == 0 && MB4 % 2 == 0, "each wave computes whole pairs of blocks");
   constexpr int S1 = (NB4 / 2) * MB, S2 = (MB4 / 2) * NB;  // MFMA steps of a wave's G1 / G2
+  constexpr bool kElem = PKIND == PK_ELEM;  // V1: per-sample betas (m, B) of every layer
   __shared__ f32x4 zx[NB * 64];  // Z_k of the 16 columns, block b at zx[b * 64 + lane]
   __shared__ f32x4 vx[MB * 64];  // Var
+  __shared__ float red[kWaves][2][16];  // per-wave column partials of the fused objective
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -44,6 +48,8 @@ __global__ __launch_bounds__(256, 1) void fused_rs_kernel(const FusedArgs a) {
   const int64_t col = (int64_t)blockIdx.x * 16 + (lane & 15);
   const bool cv = col < a.B;
   const int m = a.m, n = a.n, K = a.K;
+  const bool lossz = a.loss_kind != 0;
+  const bool lasso = __builtin_amdgcn_readfirstlane(a.loss_kind) == DLADMM_LOSS_LASSO;
   auto lane_off = [&](int64_t ld) -> uint32_t {
     return cv ? (uint32_t)((col + (int64_t)(4 * g) * ld) * 4) : kOOB;
   };
@@ -94,6 +100,54 @@ __global__ __launch_bounds__(256, 1) void fused_rs_kernel(const FusedArgs a) {
     if constexpr (PKIND == PK_S1) p.s1 = sp[DLADMM_P_S1];
     p.b1n = ((cfloat_p)a.scal)[kn * DLADMM_NSCALAR + DLADMM_P_BETA1];
     return p;
+  };
+
+  float regsum = 0.f, fit1 = 0.f, fit2 = 0.f;  // this wave's rows of the layer's objective
+  // V1: per-element betas of the G2 epilogue rows (b3 = beta1_k, b2 = beta2_k, b1n = beta1_k+1),
+  // loaded at the start of the pass (scalar-loaded layer pointers, as the fused kernel)
+  float pb[kElem ? MB4 : 1][3][4];
+  const uint32_t vb = lane_off(a.ldb);
+  auto load_betas = [&](int k) {
+    if constexpr (kElem) {
+      typedef const float* const __attribute__((address_space(4)))* ctab_p;
+      const ctab_p t1 = (ctab_p)a.b1t, t2 = (ctab_p)a.b2t;
+      const int kk = k < 0 ? 0 : k, kn = k + 1 < K ? k + 1 : kk;
+      const uint32_t eb = (uint32_t)(m * a.ldb * 4);
+      const rsrc_t r1 = mkrsrc(k < 0 ? nullptr : t1[kk], k < 0 ? 0u : eb);
+      const rsrc_t r2 = mkrsrc(k < 0 ? nullptr : t2[kk], k < 0 ? 0u : eb);
+      const rsrc_t rn = mkrsrc(k + 1 < K ? t1[kn] : nullptr, k + 1 < K ? eb : 0u);
+#pragma unroll
+      for (int b = 0; b < MB4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t so = (uint32_t)(16 * (b2o + b) + r) * (uint32_t)(a.ldb * 4);
+          pb[b][0][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r1, (int)vb, (int)so, 0));
+          pb[b][1][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r2, (int)vb, (int)so, 0));
+          pb[b][2][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rn, (int)vb, (int)so, 0));
+        }
+    }
+  };
+  // the layer's per-column objective (fused kernel: flush_loss): each wave's quarter of the rows
+  // summed over its lane groups, then the 4 quarters in wave order by wave 0 after the barrier
+  auto stage_loss = [&]() {
+    const float rs_ = col_sum(regsum), fs = col_sum(lasso ? fit2 : fit1);
+    if (g == 0) {
+      red[w][0][lane] = rs_;
+      red[w][1][lane] = fs;
+    }
+    regsum = fit1 = fit2 = 0.f;
+  };
+  auto flush_loss = [&](int k) {  // after the barrier that follows stage_loss
+    if (w == 0 && g == 0) {
+      float r0 = red[0][0][lane], f0 = red[0][1][lane];
+#pragma unroll
+      for (int q = 1; q < kWaves; ++q) {
+        r0 += red[q][0][lane];
+        f0 += red[q][1][lane];
+      }
+      a.lossp[(int64_t)(2 * k + 0) * a.ldl + col] = r0;
+      a.lossp[(int64_t)(2 * k + 1) * a.ldl + col] = lasso ? 0.5f * f0 : f0;
+    }
   };
 
   const uint32_t vo = lane_off(a.ldo);
@@ -160,6 +214,7 @@ __global__ __launch_bounds__(256, 1) void fused_rs_kernel(const FusedArgs a) {
           Zr[lb][r] = z;
           zv[r] = z;
           bstore_s(rzo, vo, row_off(b1o + lb, r), z);
+          regsum += fabsf(z);
         }
         zx[(b1o + lb) * 64 + lane] = zv;
       });
@@ -168,10 +223,11 @@ __global__ __launch_bounds__(256, 1) void fused_rs_kernel(const FusedArgs a) {
 
   // G2(k): A Z_k for this wave's E / L / T blocks; Z_k (all n rows) from zx.  PRO: the prologue
   // (T0 = A Z0 + E0 - X; E, L stay E0, L0)
-  struct OutR { rsrc_t e, l, t; };
+  struct OutR { rsrc_t e, l, t, p; };
   const rsrc_t ra = mkrsrc(a.Ap + (int64_t)(b2o / 2) * NB * 2 * kFrag, (uint32_t)(S2 * 2 * kFrag * 4));
-  auto g2_pass = [&](auto PRO_, const LayerP& P, const OutR& O) {
+  auto g2_pass = [&](auto PRO_, int k, const LayerP& P, const OutR& O) {
     constexpr bool PRO = decltype(PRO_)::value;
+    load_betas(k);
     f32x4 fa[RS_PF], fb[RS_PF];
     static_for<RS_PF>([&](auto I_) {
       constexpr int i = decltype(I_)::value;
@@ -207,10 +263,20 @@ __global__ __launch_bounds__(256, 1) void fused_rs_kernel(const FusedArgs a) {
         for (int r = 0; r < 4; ++r) {
           const float Pv = q[r], x = Xr[lb][r];
           const float l0 = Lr[lb][r], e0 = Er[lb][r];
+          float b2 = P.b2, b3 = P.b3, b1n = P.b1n;
+          if constexpr (kElem) {
+            b3 = pb[lb][0][r];
+            b2 = pb[lb][1][r];
+            b1n = pb[lb][2][r];
+          }
           float e;
-          if constexpr (EMODE == EM_VVAR) {
+          if constexpr (EMODE == EM_V1) {
+            // E = S(X - A Z - b2*L, theta_e)                      main_lena.py:87
+            const float u = (x - Pv) - b2 * l0;
+            e = shrink_u(u, P.the);
+          } else if constexpr (EMODE == EM_VVAR) {
             // VVar = L + b2*(A Z + E - X); E = S(E - ss2*VVar)    main_syn_l1l1_scalar.py:114-115
-            const float vv = l0 + P.b2 * ((Pv + e0) - x);
+            const float vv = l0 + b2 * ((Pv + e0) - x);
             e = shrink_u(e0 - P.ss2 * vv, P.the);
           } else {
             // E = ss2_1*(X - A Z) - ss2_2*L                       main_syn_lasso_scalar.py:102-103
@@ -218,7 +284,7 @@ __global__ __launch_bounds__(256, 1) void fused_rs_kernel(const FusedArgs a) {
           }
           e = PRO ? e0 : e;
           const float t = (Pv + e) - x;
-          float l = l0 + P.b3 * t;
+          float l = l0 + b3 * t;
           l = PRO ? l0 : l;
           Er[lb][r] = e;
           Lr[lb][r] = l;
@@ -226,7 +292,11 @@ __global__ __launch_bounds__(256, 1) void fused_rs_kernel(const FusedArgs a) {
           bstore_s(O.e, vo, so, e);
           bstore_s(O.l, vo, so, l);
           bstore_s(O.t, vo, so, t);
-          vv4[r] = l + P.b1n * t;  // Var of the next layer: L + b1*T
+          bstore_s(O.p, vo, so, Pv);  // training forwards: A Z_k for the backward
+          const float res = x - Pv;
+          fit1 += fabsf(res);                       // |X - A Z|
+          fit2 = __builtin_fmaf(res, res, fit2);    // (X - A Z)^2
+          vv4[r] = l + b1n * t;  // Var of the next layer: L + b1*T
         }
         vx[(b2o + lb) * 64 + lane] = vv4;
       });
@@ -237,9 +307,10 @@ __global__ __launch_bounds__(256, 1) void fused_rs_kernel(const FusedArgs a) {
   __syncthreads();  // every wave's Z0 blocks are in zx
   {
     const OutR Op{none, none,
-                  mkrsrc(a.keep_all ? a.To : nullptr, (a.keep_all && a.To) ? mbytes : 0u)};
-    g2_pass(std::true_type{}, layer_params(-1), Op);
+                  mkrsrc(a.keep_all ? a.To : nullptr, (a.keep_all && a.To) ? mbytes : 0u), none};
+    g2_pass(std::true_type{}, -1, layer_params(-1), Op);
   }
+  regsum = fit1 = fit2 = 0.f;  // the prologue's sums are not an objective
   __syncthreads();  // Var_0 complete
   for (int k = 0; k < K; ++k) {
     const bool st = a.keep_all || k == K - 1;
@@ -250,9 +321,13 @@ __global__ __launch_bounds__(256, 1) void fused_rs_kernel(const FusedArgs a) {
     const OutR O{mkrsrc(a.Eo + (int64_t)ko * m * a.ldo, st ? mbytes : 0u),
                  mkrsrc(a.Lo + (int64_t)ko * m * a.ldo, st ? mbytes : 0u),
                  mkrsrc(a.To ? a.To + (int64_t)(a.keep_all ? k + 1 : 0) * m * a.ldo : nullptr,
-                        (a.To && st) ? mbytes : 0u)};
-    g2_pass(std::false_type{}, P, O);
+                        (a.To && st) ? mbytes : 0u),
+                 mkrsrc(a.Po && a.keep_all ? a.Po + (int64_t)k * m * a.ldo : nullptr,
+                        a.Po && a.keep_all ? mbytes : 0u)};
+    g2_pass(std::false_type{}, k, P, O);
+    if (lossz) stage_loss();
     __syncthreads();  // Var_{k+1} complete; every wave is done reading Z_k
+    if (lossz) flush_loss(k);
   }
 }
 
@@ -263,14 +338,15 @@ hipError_t launch_rs(const FusedArgs& a, int grid, hipStream_t s) {
 }
 
 bool rs_supports(int shape, int variant) {
-  return shape == 2 && (variant == DLADMM_V4_SCALAR || variant == DLADMM_V5_TIED ||
-                        variant == DLADMM_V6_LASSO);
+  return shape == 2 && (variant == DLADMM_V1_LENA || variant == DLADMM_V4_SCALAR ||
+                        variant == DLADMM_V5_TIED || variant == DLADMM_V6_LASSO);
 }
 
 hipError_t launch_fused_rs(int shape, int variant, const FusedArgs& a, int grid, hipStream_t s) {
   if (shape != 2) return hipErrorInvalidValue;
   constexpr int MP = kShapeMP[2], NP = kShapeNP[2];
   switch (variant) {
+    case DLADMM_V1_LENA: return launch_rs<MP, NP, EM_V1, PK_ELEM>(a, grid, s);
     case DLADMM_V4_SCALAR: return launch_rs<MP, NP, EM_VVAR, PK_SCALAR>(a, grid, s);
     case DLADMM_V5_TIED: return launch_rs<MP, NP, EM_VVAR, PK_S1>(a, grid, s);
     case DLADMM_V6_LASSO: return launch_rs<MP, NP, EM_LASSO, PK_SCALAR>(a, grid, s);

@@ -159,8 +159,8 @@ typedef struct dladmm_fwd_desc {
   int32_t flags;
 
   /* optional (training): P [K][m][ld_out] receives A Z_k of every layer, exactly the product the
-     E/L/T updates consumed (main_syn_l1l1_scalar.py:114-117).  Written only on path 1 (fused
-     fp32 kernel, keep_all = 1; dladmm_fwd_path() tells); ignored on every other path.  A backward
+     E/L/T updates consumed (main_syn_l1l1_scalar.py:114-117).  Written only on paths 1, 4 and 5
+     (fused kernels, keep_all = 1; dladmm_fwd_path() tells); ignored on every other path.  A backward
      whose fwd.P is set reads it instead of recomputing the product (one GEMM per layer less). */
   float* P;
 } dladmm_fwd_desc;
@@ -194,9 +194,10 @@ size_t dladmm_fwd_workspace_bytes(const dladmm_fwd_desc* d);
    2 = per-layer kernel pair (large shapes, or one layer's matrix >= 2^31 bytes), 3 = per-layer
    tile kernels on bf16 operands, 4 = fused kernel on split-f16 operands (DLADMM_PREC_F32_SPLIT),
    5 = fused kernel with each workgroup's rows split over its waves (16 columns per workgroup):
-   small fp32 batches (at most two workgroups per CU) of V4 / V5 / V6 at m <= 256, n <= 512 (and
-   m > 64 or n > 256), inference without loss_kind or P -- the same arithmetic as path 1, bit for
-   bit; <0 = DLADMM_E_* error.  Host-only: no device work. */
+   small fp32 batches (at most three workgroups per CU) of V1 / V4 / V5 / V6 at m <= 256,
+   n <= 512 (and m > 64 or n > 256) -- the same arithmetic as path 1, bit for bit (the fused
+   objective's per-column sums: to fp32 rounding); <0 = DLADMM_E_* error.  Host-only: no device
+   work. */
 int dladmm_fwd_path(const dladmm_fwd_desc* d);
 
 /* Enqueue the whole K-layer forward on `stream` (hipStream_t). */

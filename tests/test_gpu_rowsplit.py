@@ -5,8 +5,9 @@ It performs the fused kernel's arithmetic operation for operation, so its output
 path 1's (plan flag no_rowsplit) BIT FOR BIT -- every layer's Z, E, L and T -- for V4, V5 (and
 the KM iteration of the test scripts built on V5) and V6, at ragged batches and shapes, lean and
 keep_all; one case is also checked against the oracle at the fp32 bar directly.  The plan takes
-path 5 only where it applies (inference at the 256 x 512 shape, no fused objective, no saved
-product, at most two 16-column workgroups per CU)."""
+path 5 where it applies (V1 / V4 / V5 / V6 at the 256 x 512 shape, fp32, at most three 16-column
+workgroups per CU), training forwards included: their saved products bit for bit, the fused
+objective to fp32 rounding."""
 import numpy as np
 import pytest
 import torch
@@ -31,18 +32,17 @@ def _run(dl, variant, inp, sd, K, keep_all=True, flags=0, **kw):
         tables = net._tables(X.device)
         W = [w.detach() for w in net._weights()]
         r = ops.dladmm_forward(net.VARIANT, X, net.A, W, net.Z0, net.E0, net.L0,
-                               keep_all=keep_all, want_T=True, flags=flags,
-                               scalar_params=tables["scalar_params"], **kw)
+                               keep_all=keep_all, want_T=True, flags=flags, **tables, **kw)
     torch.cuda.synchronize()
     return r
 
 
-@pytest.mark.parametrize("variant", ["v4", "v5", "v6"])
+@pytest.mark.parametrize("variant", ["v1", "v4", "v5", "v6"])
 @pytest.mark.parametrize("B", [1, 20, 77, 300, 1000])
 def test_rowsplit_bit_equal_to_fused(variant, B, dl):
     m, n, K = 250, 500, 6
     d = dict(variant=variant, m=m, n=n, B=B, K=K, seed=5100 + B, perturb=0.2,
-             wscale=P.VARIANT_SPECS[variant]["wscale"])
+             wscale=0.4 if variant == "v1" else P.VARIANT_SPECS[variant]["wscale"])
     inp, sd = P.build_problem(d)
     rs = _run(dl, variant, inp, sd, K)
     fu = _run(dl, variant, inp, sd, K, flags=dl._lib.F_NO_ROWSPLIT)
@@ -67,6 +67,31 @@ def test_rowsplit_shapes_and_lean_mode(shape, dl):
         assert rs.path == 5 and fu.path == 1
         for nm in ("Z", "E", "L", "T"):
             assert torch.equal(getattr(rs, nm), getattr(fu, nm)), (keep_all, nm)
+
+
+@pytest.mark.parametrize("variant", ["v1", "v4", "v6"])
+@pytest.mark.parametrize("B", [20, 25, 300])
+def test_rowsplit_training_forward(variant, B, dl):
+    """A training forward on path 5 (the reference loops' batches of 20 / 25): the saved
+    products P_k = A Z_k bit for bit with path 1's, the fused objective's per-layer sums and
+    per-column terms to fp32 rounding (each wave sums a quarter of the rows, then the quarters)."""
+    m, n, K = 250, 500, 5
+    d = dict(variant=variant, m=m, n=n, B=B, K=K, seed=5150 + B, perturb=0.2,
+             wscale=0.4 if variant == "v1" else P.VARIANT_SPECS[variant]["wscale"])
+    inp, sd = P.build_problem(d)
+    L = dl._lib
+    kind = L.LOSS_LASSO if variant == "v6" else L.LOSS_L1L1
+    kw = dict(want_P=True, loss_kind=kind, want_col_loss=True)
+    rs = _run(dl, variant, inp, sd, K, **kw)
+    fu = _run(dl, variant, inp, sd, K, flags=L.F_NO_ROWSPLIT, **kw)
+    assert rs.path == 5 and fu.path == 1
+    for nm in ("Z", "E", "L", "T", "P"):
+        assert torch.equal(getattr(rs, nm), getattr(fu, nm)), nm
+    # 1e-5: the fused objective's bar elsewhere (test_gpu_configs objective_vs_reduction)
+    np.testing.assert_allclose(rs.loss_sums.cpu().numpy(), fu.loss_sums.cpu().numpy(),
+                               rtol=1e-5)
+    np.testing.assert_allclose(rs.col_loss.cpu().numpy(), fu.col_loss.cpu().numpy(),
+                               rtol=1e-5, atol=1e-6)
 
 
 def test_rowsplit_vs_oracle(dl, oracle):
@@ -97,8 +122,8 @@ def test_km_ground_truth_on_rowsplit(dl):
 
 
 def test_rowsplit_plan_scope(dl):
-    """Path 5 only for inference without a fused objective or saved product, at batches of at
-    most two 16-column workgroups per CU, for V4 / V5 / V6 at the 256 x 512 shape."""
+    """Path 5 at batches of at most three 16-column workgroups per CU, for V1 / V4 / V5 / V6 at
+    the 256 x 512 shape, inference or training (fused objective, saved product); fp32 only."""
     L = dl._lib
     m, n, K = 250, 500, 3
     cus = torch.cuda.get_device_properties(0).multi_processor_count
@@ -116,9 +141,10 @@ def test_rowsplit_plan_scope(dl):
         return r.path
     assert path() == 5
     assert path(variant="v5") == 5 and path(variant="v6") == 5
-    assert path(B=32 * cus) == 5
-    assert path(B=32 * cus + 1) == 1
-    assert path(loss=L.LOSS_L1L1) == 1
-    assert path(P_=True) == 1
-    assert path(variant="v1") == 1
+    assert path(B=48 * cus) == 5
+    assert path(B=48 * cus + 1) == 1
+    assert path(loss=L.LOSS_L1L1) == 5
+    assert path(P_=True) == 5
+    assert path(variant="v1") == 5
+    assert path(variant="v2") == 1 and path(variant="v3") == 1   # per-row parameters
     assert path(mn=(64, 128)) == 1   # the 64 x 256 instantiation: whole-row waves
