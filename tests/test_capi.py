@@ -41,7 +41,15 @@ def _desc(dl, **kw):
 def test_workspace_and_path(dl):
     L = dl._lib.lib()
     d, _keep = _desc(dl)
+    # B = 1,000 at 256 x 512: the small-batch row-split form of the fused kernel (path 5; up to
+    # three 16-column workgroups per CU -- the plan assumes 256 CUs where no device answers)
+    assert L.dladmm_fwd_path(ctypes.byref(d)) == 5
+    d.flags = dl._lib.F_NO_ROWSPLIT
     assert L.dladmm_fwd_path(ctypes.byref(d)) == 1
+    d.flags = 0
+    big, _k2 = _desc(dl, batch=65536, ld_x=65536, ld_z0=65536, ld_e0=65536, ld_l0=65536,
+                     ld_out=65536)
+    assert L.dladmm_fwd_path(ctypes.byref(big)) == 1
     ws = L.dladmm_fwd_workspace_bytes(ctypes.byref(d))
     # packed A + 15 packed W_k (256 x 512 fp32 each) + per-wave loss partials
     assert ws >= 16 * 256 * 512 * 4 + 2 * 15 * 16 * 4 * 4
@@ -117,11 +125,13 @@ def test_plan_flags_select_kernels(dl):
     off the reverse sweep; unknown bits change nothing."""
     L = dl._lib.lib()
     d, _keep = _desc(dl)
+    assert L.dladmm_fwd_path(ctypes.byref(d)) == 5
+    d.flags = dl._lib.F_NO_ROWSPLIT
     assert L.dladmm_fwd_path(ctypes.byref(d)) == 1
     d.flags = dl._lib.F_PER_LAYER
     assert L.dladmm_fwd_path(ctypes.byref(d)) == 2
     d.flags = 1 << 20
-    assert L.dladmm_fwd_path(ctypes.byref(d)) == 1
+    assert L.dladmm_fwd_path(ctypes.byref(d)) == 5
     d.precision = dl._lib.PREC_BF16
     for f in (0, dl._lib.F_BF16_WIDE):
         d.flags = f
