@@ -20,7 +20,7 @@ UNITS = ("dladmm_capi.hip", "dladmm_fused.hip", "dladmm_fused_savep.hip", "dladm
          "dladmm_fused_x3_savep.hip", "dladmm_fused_rs.hip",
          "dladmm_layered.hip", "dladmm_backward.hip", "dladmm_lskm.hip", "dladmm_eval.hip",
          "dladmm_tile_bf16.hip", "dladmm_wgrad_x3.hip",
-         "dladmm_reverse.hip",
+         "dladmm_reverse.hip", "dladmm_reverse_rs.hip",
          "dladmm_lena.hip",
          # reverse-sweep instantiations: one unit per E-step form and shape group (minutes each)
          "dladmm_reverse_vvar.hip", "dladmm_reverse_v1.hip", "dladmm_reverse_lasso.hip",

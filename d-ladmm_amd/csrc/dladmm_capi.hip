@@ -820,6 +820,7 @@ struct BwdPlan {
   // layer (rows padded to Rn2 / Rm2 for the weight gradient), per-wave parameter partials
   bool rev;
   int rtiles, rncg;
+  bool rrs;  // reverse sweep on the row-split kernel (16 columns per workgroup)
   int64_t Rn2, Rm2;
   size_t off_ratp, off_rmtp, off_gu, off_rvar, off_rpart, off_rptab, off_rrow;
 };
@@ -939,7 +940,16 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
       p->Bpad = bpad;
       p->Rn = p->Rn2;  // the weight gradient reads the reverse kernel's row padding
       p->Rm = p->Rm2;
-      p->rtiles = ceil_div(f.batch, kTileCols);
+      // after a path-5 forward (a small batch), the row-split sweep: 16 columns per workgroup,
+      // each product's rows over its waves (bit-equal gU_k / Var_k)
+      // (the forward itself ran path 5: an fp32 forward -- the plan above is recomputed in fp32
+      // for every forward precision)
+      // At most one workgroup per CU: backward (V4, K = 15, fused objective) 0.68 vs 1.32 ms at
+      // B = 25, 1.03 vs 1.66 at 4,096, but 2.42 vs 1.90 at 10,000 (profiles/r06_rowsplit_ab.json)
+      p->rrs = p->fwd.path == 5 && f.precision == DLADMM_PREC_F32 &&
+               reverse_rs_supports(p->fwd.shape, f.variant) && !(d->gE || d->gL || d->gT) &&
+               ceil_div((int)f.batch, 16) <= device_cus();
+      p->rtiles = p->rrs ? ceil_div(f.batch, 16) : ceil_div(f.batch, kTileCols);
       p->rncg = p->rtiles * kWaves;
     }
   }
@@ -1079,7 +1089,9 @@ inline int run_reverse(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hip
     r.rowp = f.row_params; r.rstride = f.row_stride;
     r.rpart = (float*)(ws + p.off_rrow);
   }
-  if (hipError_t e = launch_reverse_shape(shape, f.variant, r, p.rtiles, s)) return (int)e;
+  if (hipError_t e = p.rrs ? launch_reverse_rs(shape, f.variant, r, p.rtiles, s)
+                           : launch_reverse_shape(shape, f.variant, r, p.rtiles, s))
+    return (int)e;
   // weight gradients gW_k = -s1 gU_k Var_k^T (split-K over the batch, fixed-order reduction),
   // layers K-1 .. 0 as the per-layer sweep visits them (a tied weight sums them in that order);
   // V5: each layer's <W, gU_k Var_k^T> for ss1_k's gradient
@@ -1501,7 +1513,7 @@ int dladmm_bwd_path(const dladmm_bwd_desc* d) {
   if (int e = validate_bwd(d)) return e;
   BwdPlan p;
   if (int e = make_bwd_plan(d, &p)) return e;
-  return p.rev ? 1 : 0;
+  return p.rev ? (p.rrs ? 2 : 1) : 0;
 }
 
 int dladmm_bwd_f32(const dladmm_bwd_desc* d, void* stream) {

@@ -228,6 +228,11 @@ struct RevArgs {
 static_assert(sizeof(RevArgs) <= 2048, "kernel argument size");
 bool reverse_supports(int variant);
 hipError_t launch_reverse_shape(int shape, int variant, const RevArgs& a, int grid, hipStream_t s);
+// the small-batch row-split reverse sweep (dladmm_reverse_rs.hip): 16 columns per workgroup,
+// grid = ceil(B / 16), after a path-5 forward; V4 / V5 / V6 at the 256 x 512 shape, no E / L / T
+// cotangents
+bool reverse_rs_supports(int shape, int variant);
+hipError_t launch_reverse_rs(int shape, int variant, const RevArgs& a, int grid, hipStream_t s);
 // fused main_lena.py objective (dladmm_lena.hip, dladmm_lena_f32): one workgroup per 64 columns,
 // every layer; mode 0 = per-column partial sums part[K][4][ldl], mode 1 = the cotangents gE / gL
 struct LenaArgs {

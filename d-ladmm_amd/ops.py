@@ -246,7 +246,8 @@ class BackwardResult:
     g_row: Optional[torch.Tensor]     # [K, 8, R] fp64 (V2, V3)
     g_beta1: List[torch.Tensor]       # V1: K tensors (m, B)
     g_beta2: List[torch.Tensor]
-    path: int = 0                     # dladmm_bwd_path: 1 = one reverse-sweep kernel, 0 = per layer
+    path: int = 0                     # dladmm_bwd_path: 1 = one reverse-sweep kernel (2: its
+                                      # small-batch row-split form), 0 = per layer
 
 
 def dladmm_backward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[torch.Tensor],

@@ -268,7 +268,12 @@ typedef struct dladmm_bwd_desc {
 size_t dladmm_bwd_workspace_bytes(const dladmm_bwd_desc* d);
 
 /* Which kernels the backward runs: 1 = one reverse-sweep kernel for every layer's adjoints,
-   0 = per-layer kernels, <0 = DLADMM_E_* error.  The reverse sweep runs when ALL of these hold:
+   2 = the same sweep in its small-batch row-split form (16 columns per workgroup, each
+   product's rows over its waves; after a path-5 forward of V4 / V5 / V6 without E / L / T
+   cotangents, at most one 16-column workgroup per CU: gU_k, Var_k and the weight gradients
+   bit-equal to path 1's, the parameter gradients to rounding), 0 = per-layer kernels,
+   <0 = DLADMM_E_* error.  The reverse sweep
+   runs when ALL of these hold:
      - any variant V1-V6 (and the newS models built on V4 / V5);
      - the forward saved P (fwd.P != NULL, keep_all): the fused fp32 path or the split-f16
        path (precision DLADMM_PREC_F32_SPLIT), both of which store the product A Z_k their

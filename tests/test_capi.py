@@ -137,8 +137,14 @@ def test_plan_flags_select_kernels(dl):
         d.flags = f
         assert L.dladmm_fwd_path(ctypes.byref(d)) == 3
     b, _k = _bdesc(dl)
-    b.fwd.P = 1 << 40   # a saved-product forward
+    b.fwd.P = 1 << 40   # a saved-product forward (B = 1,000: path 5, the row-split sweep)
+    assert L.dladmm_bwd_path(ctypes.byref(b)) == 2
+    b.fwd.flags = dl._lib.F_NO_ROWSPLIT   # a path-1 forward: the 64-column sweep
     assert L.dladmm_bwd_path(ctypes.byref(b)) == 1
+    b.fwd.precision = dl._lib.PREC_F32_SPLIT   # a split-f16 forward (path 4) likewise
+    b.fwd.flags = 0
+    assert L.dladmm_bwd_path(ctypes.byref(b)) == 1
+    b.fwd.precision = dl._lib.PREC_F32
     b.fwd.flags = dl._lib.F_BWD_PER_LAYER
     assert L.dladmm_bwd_path(ctypes.byref(b)) == 0
     assert L.dladmm_bwd_workspace_bytes(ctypes.byref(b)) > 0

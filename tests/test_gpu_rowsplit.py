@@ -148,3 +148,51 @@ def test_rowsplit_plan_scope(dl):
     assert path(variant="v1") == 5
     assert path(variant="v2") == 1 and path(variant="v3") == 1   # per-row parameters
     assert path(mn=(64, 128)) == 1   # the 64 x 256 instantiation: whole-row waves
+
+
+@pytest.mark.parametrize("variant,kind", [("v4", "l1l1"), ("v4", "lasso"), ("v5", "l1l1"),
+                                          ("v6", "lasso")])
+@pytest.mark.parametrize("B", [20, 25, 300])
+@pytest.mark.parametrize("gz", [False, True])
+def test_rowsplit_reverse_sweep(variant, kind, B, gz, dl):
+    """dladmm_bwd_path 2 (the row-split reverse sweep after a path-5 forward) against the reverse
+    sweep after a path-1 forward (plan flag no_rowsplit), same saved state: the weight gradients
+    bit for bit (from bit-equal gU_k / Var_k), the parameter slots within 2e-6 per layer (the
+    per-wave partials cover other element sets), with the fused objective or with Z
+    cotangents (a torch-op loss over the returned Z_k, the reference's own training loop)."""
+    from test_gpu_backward import make_train_net, nrel
+    ops = dl.ops
+    L = dl._lib
+    m, n, K = 250, 500, 4
+    d = dict(variant=variant, m=m, n=n, B=B, K=K, seed=5600 + B, perturb=0.1)
+    inp, sd = P.build_problem(d)
+    net = make_train_net(dl, variant, inp, sd, K).cuda()
+    X = torch.from_numpy(inp["X"]).cuda()
+    with torch.no_grad():
+        tables = net._tables(X.device)
+    W = [w.detach() for w in net._weights()]
+    args = (net.VARIANT, X, net.A, W, net.Z0, net.E0, net.L0)
+    lk = L.LOSS_LASSO if kind == "lasso" else L.LOSS_L1L1
+    g = torch.Generator(device="cuda").manual_seed(B)
+    coef = (torch.rand(K, 2, device="cuda", generator=g) *
+            torch.tensor([1e-2, 1.0], device="cuda")).contiguous()
+    out = {}
+    for fl in (0, L.F_NO_ROWSPLIT):
+        with torch.no_grad():
+            r = ops.dladmm_forward(*args, keep_all=True, want_T=True, want_P=True, loss_kind=lk,
+                                   flags=fl, **tables)
+        if gz:
+            gZ = [torch.randn(n, B, generator=g, device="cuda") / B for _ in range(K)]
+            kw = dict(gZ=gZ, **tables)
+        else:
+            kw = dict(loss_kind=lk, loss_coef=coef, **tables)
+        out[fl] = (r.path, ops.dladmm_backward(*args, r, **kw))
+        g.manual_seed(B)   # the same cotangents / coefficients for both
+        coef = (torch.rand(K, 2, device="cuda", generator=g) *
+                torch.tensor([1e-2, 1.0], device="cuda")).contiguous()
+    (fp, rs), (fp1, cl) = out[0], out[L.F_NO_ROWSPLIT]
+    assert fp == 5 and fp1 == 1 and rs.path == 2 and cl.path == 1
+    assert torch.equal(rs.gW, cl.gW)
+    gs_r, gs_c = rs.g_scalar.cpu().numpy(), cl.g_scalar.cpu().numpy()
+    for k in range(K):
+        assert nrel(gs_r[k], gs_c[k]) <= 2e-6, (k, gs_r[k], gs_c[k])

@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--gz", action="store_true",
                     help="per-layer Z cotangents (a loss built from the returned Z_k with torch "
                          "ops, the reference's training loops) instead of the fused objective")
+    ap.add_argument("--no-rowsplit", action="store_true",
+                    help="forward with the plan flag no_rowsplit (path 1), so a small batch's "
+                         "backward runs the 64-column reverse sweep instead of its row-split form")
     ap.add_argument("--per-layer", action="store_true",
                     help="plan flag bwd_per_layer: the per-layer backward kernels")
     a = ap.parse_args()
@@ -51,7 +54,8 @@ def main():
     args = (net.VARIANT, X, net.A, W, net.Z0, net.E0, net.L0)
     with torch.no_grad():
         r = ops.dladmm_forward(*args, keep_all=True, want_T=True, want_P=True,
-                               loss_kind=L.LOSS_L1L1, **tables)
+                               loss_kind=L.LOSS_L1L1, flags=L.F_NO_ROWSPLIT if a.no_rowsplit else 0,
+                               **tables)
     coef = torch.tensor([[1e-3 / B, 1.0 / B]] * K, device=dev)
     kw = dict(loss_kind=L.LOSS_L1L1, loss_coef=coef, **tables)
     if a.gz:
@@ -72,6 +76,7 @@ def main():
             ev0.record()
             with ops.plan_flags(bwd_per_layer=a.per_layer):
                 res = ops.dladmm_backward(*args, r, **kw)
+            bwd_path = res.path
             ev1.record()
             torch.cuda.synchronize()
             if rep:  # the first round warms every library's kernels and workspace
@@ -79,7 +84,8 @@ def main():
             del res
     out = {s: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))}
            for s, t in times.items()}
-    out["config"] = dict(m=m, n=n, K=K, B=B, reps=a.reps, rev=not a.per_layer, gz=a.gz)
+    out["config"] = dict(m=m, n=n, K=K, B=B, reps=a.reps, rev=not a.per_layer, gz=a.gz,
+                         no_rowsplit=a.no_rowsplit, bwd_path=bwd_path)
     print(json.dumps(out))
 
 
