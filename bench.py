@@ -428,6 +428,17 @@ def main():
             except Exception as e:  # noqa: BLE001
                 train["split_f16"] = {"error": f"{type(e).__name__}: {e}"}
             torch.cuda.empty_cache()
+        if "error" not in train:
+            # the reference training loop's own batch (main_syn_l1l1_scalar.py -bs 25): the
+            # row-split forward and reverse sweep; host-bound at this size
+            tr = bench_train.parser().parse_args(["--variant", "v4", "--fused-loss", "--batch",
+                                                  "25", "--steps", "50", "--warmup", "5"])
+            try:
+                train["ref_batch"] = {k: v for k, v in bench_train.run(tr).items()
+                                      if k in ("batch", "step_ms", "samples_per_s", "forward_ms",
+                                               "backward_ms")}
+            except Exception as e:  # noqa: BLE001
+                train["ref_batch"] = {"error": f"{type(e).__name__}: {e}"}
 
     if rank == 0:
         path = {1: "fused", 2: "per-layer", 3: "bf16-tiles", 4: "fused-split-f16"}.get(
@@ -618,7 +629,8 @@ def main():
         if train is not None:
             res["train"] = {k: train[k] for k in (
                 "metric", "batch", "step_ms", "samples_per_s", "forward_ms", "backward_ms",
-                "backward_tflops", "backward_frac_fp32_mfma", "loss_path", "split_f16", "error")
+                "backward_tflops", "backward_frac_fp32_mfma", "loss_path", "split_f16",
+                "ref_batch", "error")
                 if k in train}
             res["train"]["note"] = ("V4 m=256 n=512 K=15 training step (zero_grad, forward with "
                                     "saved A Z_k, fused L1L1 objective with decay, reverse-sweep "
