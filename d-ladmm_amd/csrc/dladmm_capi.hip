@@ -947,7 +947,7 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
       // At most one workgroup per CU: backward (V4, K = 15, fused objective) 0.68 vs 1.32 ms at
       // B = 25, 1.03 vs 1.66 at 4,096, but 2.42 vs 1.90 at 10,000 (profiles/r06_rowsplit_ab.json)
       p->rrs = p->fwd.path == 5 && f.precision == DLADMM_PREC_F32 &&
-               reverse_rs_supports(p->fwd.shape, f.variant) && !(d->gE || d->gL || d->gT) &&
+               reverse_rs_supports(p->fwd.shape, f.variant) &&
                ceil_div((int)f.batch, 16) <= device_cus();
       p->rtiles = p->rrs ? ceil_div(f.batch, 16) : ceil_div(f.batch, kTileCols);
       p->rncg = p->rtiles * kWaves;

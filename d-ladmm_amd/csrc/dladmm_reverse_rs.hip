@@ -13,9 +13,11 @@
 // order: gU_k and Var_k (and with them every weight gradient) are that kernel's bit for bit.
 // The parameter partials are per (layer, slot, wave) as there, but each wave's partial covers a
 // quarter of the rows of 16 columns, so the parameter gradients agree to rounding
-// (tests/test_gpu_rowsplit.py).  Scope: V4 / V5 (EM_VVAR) and V6 (EM_LASSO) at the 256 x 512
-// shape, with or without cotangents of Z (the reference's torch-op loss over the Z_k), no
-// E / L / T cotangents.
+// (tests/test_gpu_rowsplit.py); V1's per-sample beta gradients are per-element stores, equal
+// bit for bit.  Scope: V1 (EM_V1), V4 / V5 (EM_VVAR) and V6 (EM_LASSO) at the 256 x 512 shape,
+// with or without cotangents of Z and of E / L / T (the reference's torch-op losses over the
+// returned states, main_lena.py:221-228).  The operands of a G2' output pair are loaded as the
+// pair's products start, in flight across its 32 MFMA steps.
 #include "dladmm_internal.h"
 
 #ifndef RRS_PF
@@ -24,13 +26,14 @@
 
 namespace dladmm {
 
-template <int MP, int NP, int EMODE, bool GZ>
+template <int MP, int NP, int EMODE, bool GZ, bool COT>
 __global__ __launch_bounds__(256, 1) void reverse_rs_kernel(const RevArgs a) {
   constexpr int MB = MP / 16, NB = NP / 16;
   constexpr int NB4 = NB / kWaves, MB4 = MB / kWaves;
   static_assert(NB4 % 2 == 0 && MB4 % 2 == 0, "each wave computes whole pairs of blocks");
   constexpr int S1 = (NB4 / 2) * MB, S2 = (MB4 / 2) * NB;  // MFMA steps of a wave's G1' / G2'
   constexpr bool kAE = EMODE == EM_VVAR;  // the adjoint of E is carried through the workspace
+  constexpr bool kV1 = EMODE == EM_V1;     // V1: per-sample betas and their gradients
   __shared__ f32x4 gpx[MB * 64];  // gP_k of the 16 columns (G1''s B operand)
   __shared__ f32x4 gux[NB * 64];  // gU_k (G2''s B operand)
 
@@ -89,10 +92,12 @@ __global__ __launch_bounds__(256, 1) void reverse_rs_kernel(const RevArgs a) {
   }
   float psz = 0.f, psb1 = 0.f, ps[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   auto flush = [&](int layer, int slot, float v) {
+    if constexpr (kV1) return;  // V1: per-sample betas (element gradients), fixed thresholds
     const float s = wave_sum(v);
     if (lane == 0) a.part[((int64_t)layer * DLADMM_NSCALAR + slot) * a.ncg + cg] = s;
   };
   auto flush_bk1 = [&](int j) {
+    if constexpr (kV1) return;
     flush(j, DLADMM_P_BETA3, ps[0]);
     if constexpr (EMODE == EM_VVAR) {
       flush(j, DLADMM_P_BETA2, ps[1]);
@@ -212,42 +217,88 @@ __global__ __launch_bounds__(256, 1) void reverse_rs_kernel(const RevArgs a) {
     const int j = MODE == 2 ? K - 1 : k - 1;   // the BK1 layer
     const LP2 P = MODE == 2 ? lp2(K, K - 1) : (MODE == 1 ? lp2(0, -1) : lp2(k, k - 1));
     // operand views (the reverse sweep's res2 / res2_last)
+    auto tview = [&](int t, int kk) -> rsrc_t {
+      const float* p = tab[rev_tab_at(t, K, kk)];
+      return urs(p, p ? mbytes : 0u);
+    };
     rsrc_t oP, oL, oE = none;
+    rsrc_t oB1K = none, oGB1K = none, oB1J = none, oB2J = none, oGB1J = none, oGB2J = none;
+    rsrc_t oGE = none, oGL = none, oGT = none;
     if constexpr (MODE == 1) {
       oP = mkrsrc(a.T, mbytes);
       oL = urs(a.L0, mbytes);
+      if constexpr (kV1) {
+        oB1K = tview(RT_B1, 0);
+        oGB1K = tview(RT_GB1, 0);
+      }
     } else {
       oP = urs(a.P + j * ml, mbytes);
       oL = urs(j >= 1 ? a.L + (j - 1) * ml : a.L0, mbytes);
       if constexpr (kAE) oE = urs(j >= 1 ? a.E + (j - 1) * ml : a.E0, mbytes);
+      if constexpr (kV1) {
+        const bool bk3 = j + 1 < K;   // the prologue (j = K - 1) has no BK3
+        oB1K = bk3 ? tview(RT_B1, j + 1) : none;
+        oGB1K = bk3 ? tview(RT_GB1, j + 1) : none;
+        oB1J = tview(RT_B1, j);
+        oB2J = tview(RT_B2, j);
+        oGB1J = tview(RT_GB1, j);
+        oGB2J = tview(RT_GB2, j);
+      }
+      if constexpr (COT) {
+        oGE = tview(RT_GE, j);
+        oGL = tview(RT_GL, j);
+        oGT = tview(RT_GT, j + 1);
+      }
     }
     // Var_j's workspace block and the next layer's (which holds the adjoint of E_{j})
     const int jr = MODE == 1 ? 0 : j;
     const rsrc_t rv = urs(a.VAR + jr * a.vas, (uint32_t)((jr + 1 < K ? 2 : 1) * a.vas * 4));
-    float pP[MB4][4], pL[MB4][4], pE[kAE ? MB4 : 1][4], pA[kAE ? MB4 : 1][4];
+    // operands of one pair of m blocks, loaded as the pair's products start (in flight during
+    // its 32 MFMA steps)
+    enum { O_P = 0, O_L = 1, O_E = 2, O_A = 3, O_B1K = 4, O_B1J = 5, O_B2J = 6, O_GB1 = 7,
+           O_GE = 8, O_GL = 9, O_GT = 10 };
+    float op[2][11][4];
+    auto load_pair = [&](int pp) {
 #pragma unroll
-    for (int b = 0; b < MB4; ++b)
+      for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const uint32_t so = row_off(b2o + b, r, ldo4);
-        pP[b][r] = ld(oP, vo, so);
-        pL[b][r] = ld(oL, vo, so);
-        if constexpr (kAE) {
-          pE[b][r] = MODE == 1 ? 0.f : ld(oE, vo, so);
-          pA[b][r] = MODE == 0 ? ld(rv, vw, vas4 + aeo + row_off(b2o + b, r, ldw4)) : 0.f;
+        for (int r = 0; r < 4; ++r) {
+          const int b = 2 * pp + h;
+          const uint32_t so = row_off(b2o + b, r, ldo4);
+          op[h][O_P][r] = ld(oP, vo, so);
+          op[h][O_L][r] = ld(oL, vo, so);
+          if constexpr (kAE) {
+            op[h][O_E][r] = MODE == 1 ? 0.f : ld(oE, vo, so);
+            op[h][O_A][r] = MODE == 0 ? ld(rv, vw, vas4 + aeo + row_off(b2o + b, r, ldw4)) : 0.f;
+          }
+          if constexpr (kV1) {
+            op[h][O_B1K][r] = ld(oB1K, vo, so);
+            op[h][O_B1J][r] = ld(oB1J, vo, so);
+            op[h][O_B2J][r] = ld(oB2J, vo, so);
+            op[h][O_GB1][r] = ld(oGB1K, vo, so);
+          }
+          if constexpr (COT) {
+            op[h][O_GE][r] = ld(oGE, vo, so);
+            op[h][O_GL][r] = ld(oGL, vo, so);
+            op[h][O_GT][r] = ld(oGT, vo, so);
+          }
         }
-      }
-    f32x4 qa4[MB4];
+    };
+    const rsrc_t rmt = MODE == 2 ? none
+                                 : mkrsrc(a.Mtp + (int64_t)k * wl + (int64_t)(b2o / 2) * NB * 2 * kFrag,
+                                          (uint32_t)(S2 * 2 * kFrag * 4));
+    f32x4 fa[RRS_PF], fb[RRS_PF];
     if constexpr (MODE != 2) {
-      const rsrc_t rmt = mkrsrc(a.Mtp + (int64_t)k * wl + (int64_t)(b2o / 2) * NB * 2 * kFrag,
-                                (uint32_t)(S2 * 2 * kFrag * 4));
-      f32x4 fa[RRS_PF], fb[RRS_PF];
       static_for<RRS_PF>([&](auto I_) {
         constexpr int i = decltype(I_)::value;
         if constexpr (i < S2) frag2(rmt, I_, fa[i], fb[i]);
       });
-      static_for<MB4 / 2>([&](auto P_) {
-        constexpr int pp = decltype(P_)::value;
+    }
+    static_for<MB4 / 2>([&](auto P_) {
+      constexpr int pp = decltype(P_)::value;
+      load_pair(pp);
+      f32x4 qa4[2] = {zero4, zero4};
+      if constexpr (MODE != 2) {
         f32x4 ca = zero4, cb = zero4;
         static_for<NB>([&](auto K_) {
           constexpr int kb = decltype(K_)::value;
@@ -265,36 +316,59 @@ __global__ __launch_bounds__(256, 1) void reverse_rs_kernel(const RevArgs a) {
           ca = mfma4(wa.w, u[3], ca);
           cb = mfma4(wb.w, u[3], cb);
         });
-        qa4[2 * pp] = ca;
-        qa4[2 * pp + 1] = cb;
-      });
-    } else {
+        qa4[0] = ca;
+        qa4[1] = cb;
+      }
+      // epilogue rows (the reverse sweep's epi2_row)
 #pragma unroll
-      for (int b = 0; b < MB4; ++b) qa4[b] = zero4;
-    }
-    // epilogue rows (the reverse sweep's epi2_row, scalar parameters, no E / L / T cotangents)
-#pragma unroll
-    for (int lb = 0; lb < MB4; ++lb) {
+    for (int h = 0; h < 2; ++h) {
+      const int lb = 2 * pp + h;
       f32x4 gp4;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float gVar = qa4[lb][r];
+        const float gVar = qa4[h][r];
         const uint32_t sw = row_off(b2o + lb, r, ldw4);
+        const uint32_t sb = row_off(b2o + lb, r, ldo4);
+        const float b1k = kV1 ? op[h][O_B1K][r] : P.b1k;
         if constexpr (MODE == 1) {
-          psb1 += gVar * pP[lb][r];   // beta1_0's gradient: gVar T_0
+          if constexpr (kV1) {
+            // beta1_0's gradient: BK1(0)'s term + gVar T_0
+            bstore_s(oGB1K, vo, sb, op[h][O_GB1][r] + gVar * op[h][O_P][r]);
+          } else {
+            psb1 += gVar * op[h][O_P][r];   // beta1_0's gradient: gVar T_0
+          }
           // Var_0 = L0 + beta1_0 T_0, the forward's prologue expression
-          bstore_s(rv, vw, sw, pL[lb][r] + P.b1k * pP[lb][r]);
+          bstore_s(rv, vw, sw, op[h][O_L][r] + b1k * op[h][O_P][r]);
           continue;
         }
-        const float aL = AL[lb][r] + gVar;  // complete adjoint of L_{k-1}
-        const float aT = P.b1k * gVar;      // adjoint of T_k
-        const float aE = MODE == 0 ? (kAE ? pA[lb][r] : 0.f) : 0.f;
-        const float Pv = pP[lb][r], lp = pL[lb][r], x = Xr[lb][r];
+        const float aLin = AL[lb][r] + gVar;  // complete adjoint of L_{k-1} (upstream aside)
+        const float aTin = b1k * gVar;        // adjoint of T_k
+        const float aL = COT ? aLin + op[h][O_GL][r] : aLin;
+        const float aT = COT ? aTin + op[h][O_GT][r] : aTin;
+        const float aE0 = MODE == 0 ? (kAE ? op[h][O_A][r] : 0.f) : 0.f;
+        const float aE = COT ? aE0 + op[h][O_GE][r] : aE0;
+        const float Pv = op[h][O_P][r], lp = op[h][O_L][r], x = Xr[lb][r];
+        const float b1 = kV1 ? op[h][O_B1J][r] : 0.f;
         float gP, gEp = 0.f, gLp, t;
         (void)gEp;
         float p3 = 0.f, p2 = 0.f, pe = 0.f, ps2 = 0.f, ps2b = 0.f;
-        if constexpr (EMODE == EM_VVAR) {
-          const float ep = pE[lb][r];
+        if constexpr (EMODE == EM_V1) {
+          const float b2 = op[h][O_B2J][r];
+          const float u = (x - Pv) - b2 * lp;               // main_lena.py:87
+          const float e = shrink_u(u, shrink_params(P.the));
+          t = (Pv + e) - x;                                 // T_k
+          const float gTn = aT + b1 * aL;                   // L_{k-1} = L_{k-2} + b1 T_k (:89)
+          p3 = aL * t;
+          const float gEt = aE + gTn;
+          const float ga = (u - P.the) > 0.0f ? gEt : 0.f;
+          const float gb = (-u - P.the) > 0.0f ? gEt : 0.f;
+          const float gEh = ga + gb;
+          pe = gb - ga;
+          gP = gTn - gEh;
+          p2 = -gEh * lp;
+          gLp = aL - b2 * gEh;
+        } else if constexpr (EMODE == EM_VVAR) {
+          const float ep = op[h][O_E][r];
           const float r0 = (Pv + ep) - x;
           const float vv = lp + P.b2 * r0;                  // main_syn_l1l1_scalar.py:114
           const float eh = ep - P.ss2 * vv;                 // :115
@@ -331,19 +405,29 @@ __global__ __launch_bounds__(256, 1) void reverse_rs_kernel(const RevArgs a) {
               float, (lqm & __builtin_bit_cast(uint32_t, res)) | (~lqm & __builtin_bit_cast(uint32_t, sg)));
           gP = gP - P.cf * dfit;
         }
-        if constexpr (MODE == 0) psb1 += gVar * t;  // beta1 of layer k: gVar * T_k
-        ps[0] += p3; ps[1] += p2; ps[2] += pe; ps[3] += ps2; ps[4] += ps2b;
+        if constexpr (kV1) {
+          // beta1_k's gradient = BK1(k)'s term + gVar T_k; beta1_{k-1} gets BK1(k-1)'s term
+          // aL T_k now and BK3(k-1)'s next pass; beta2_{k-1} complete
+          bstore_s(MODE == 0 ? oGB1K : none, vo, sb, op[h][O_GB1][r] + gVar * t);
+          bstore_s(oGB1J, vo, sb, p3);
+          bstore_s(oGB2J, vo, sb, p2);
+        } else {
+          if constexpr (MODE == 0) psb1 += gVar * t;  // beta1 of layer k: gVar * T_k
+          ps[0] += p3; ps[1] += p2; ps[2] += pe; ps[3] += ps2; ps[4] += ps2b;
+        }
         gp4[r] = gP;
         AL[lb][r] = gLp;
         // Var of layer k: L_{k-1} + beta1_k T_k from the recomputed values (the prologue's,
         // layer K, runs past the workspace: dropped)
-        const float lk = lp + P.b3 * t;
-        const float vark = lk + P.b1k * t;
+        const float lcoef = kV1 ? b1 : P.b3;
+        const float lk = lp + lcoef * t;
+        const float vark = lk + b1k * t;
         bstore_s(rv, vw, vas4 + sw, vark);
         if constexpr (kAE) bstore_s(rv, vw, sw + aeo, gEp);  // adjoint of E_{k-2}
       }
       if constexpr (MODE != 1) gpx[(b2o + lb) * 64 + lane] = gp4;
     }
+    });
   };
 
   // prologue BK1(K-1), then per layer G1'(k), G2'(k)
@@ -365,23 +449,30 @@ __global__ __launch_bounds__(256, 1) void reverse_rs_kernel(const RevArgs a) {
   flush(0, DLADMM_P_BETA1, psb1);
 }
 
-template <int EM, bool GZ>
+template <int EM, bool GZ, bool COT>
 hipError_t launch_rrs(const RevArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((reverse_rs_kernel<kShapeMP[2], kShapeNP[2], EM, GZ>), dim3(grid), dim3(256),
-                     0, s, a);
+  hipLaunchKernelGGL((reverse_rs_kernel<kShapeMP[2], kShapeNP[2], EM, GZ, COT>), dim3(grid),
+                     dim3(256), 0, s, a);
   return hipGetLastError();
+}
+template <int EM>
+hipError_t launch_rrs_em(const RevArgs& a, int grid, hipStream_t s) {
+  if (a.has_gz && a.has_cot) return launch_rrs<EM, true, true>(a, grid, s);
+  if (a.has_gz) return launch_rrs<EM, true, false>(a, grid, s);
+  if (a.has_cot) return launch_rrs<EM, false, true>(a, grid, s);
+  return launch_rrs<EM, false, false>(a, grid, s);
 }
 
 bool reverse_rs_supports(int shape, int variant) {
-  return shape == 2 && (variant == DLADMM_V4_SCALAR || variant == DLADMM_V5_TIED ||
-                        variant == DLADMM_V6_LASSO);
+  return shape == 2 && (variant == DLADMM_V1_LENA || variant == DLADMM_V4_SCALAR ||
+                        variant == DLADMM_V5_TIED || variant == DLADMM_V6_LASSO);
 }
 
 hipError_t launch_reverse_rs(int shape, int variant, const RevArgs& a, int grid, hipStream_t s) {
-  if (!reverse_rs_supports(shape, variant) || a.has_cot) return hipErrorInvalidValue;
-  if (variant == DLADMM_V6_LASSO)
-    return a.has_gz ? launch_rrs<EM_LASSO, true>(a, grid, s) : launch_rrs<EM_LASSO, false>(a, grid, s);
-  return a.has_gz ? launch_rrs<EM_VVAR, true>(a, grid, s) : launch_rrs<EM_VVAR, false>(a, grid, s);
+  if (!reverse_rs_supports(shape, variant)) return hipErrorInvalidValue;
+  if (variant == DLADMM_V1_LENA) return launch_rrs_em<EM_V1>(a, grid, s);
+  if (variant == DLADMM_V6_LASSO) return launch_rrs_em<EM_LASSO>(a, grid, s);
+  return launch_rrs_em<EM_VVAR>(a, grid, s);
 }
 
 }  // namespace dladmm

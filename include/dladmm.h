@@ -269,9 +269,10 @@ size_t dladmm_bwd_workspace_bytes(const dladmm_bwd_desc* d);
 
 /* Which kernels the backward runs: 1 = one reverse-sweep kernel for every layer's adjoints,
    2 = the same sweep in its small-batch row-split form (16 columns per workgroup, each
-   product's rows over its waves; after a path-5 forward of V4 / V5 / V6 without E / L / T
-   cotangents, at most one 16-column workgroup per CU: gU_k, Var_k and the weight gradients
-   bit-equal to path 1's, the parameter gradients to rounding), 0 = per-layer kernels,
+   product's rows over its waves; after an fp32 path-5 forward of V1 / V4 / V5 / V6, any
+   cotangents, at most one 16-column workgroup per CU: gU_k, Var_k, the weight gradients and
+   V1's beta gradients bit-equal to path 1's, the scalar-parameter gradients to rounding),
+   0 = per-layer kernels,
    <0 = DLADMM_E_* error.  The reverse sweep
    runs when ALL of these hold:
      - any variant V1-V6 (and the newS models built on V4 / V5);

@@ -196,3 +196,47 @@ def test_rowsplit_reverse_sweep(variant, kind, B, gz, dl):
     gs_r, gs_c = rs.g_scalar.cpu().numpy(), cl.g_scalar.cpu().numpy()
     for k in range(K):
         assert nrel(gs_r[k], gs_c[k]) <= 2e-6, (k, gs_r[k], gs_c[k])
+
+
+@pytest.mark.parametrize("variant,kind", [("v1", "l1l1"), ("v4", "l1l1"), ("v6", "lasso")])
+@pytest.mark.parametrize("B", [20, 300])
+@pytest.mark.parametrize("cot", ["elt", "all"])
+def test_rowsplit_reverse_sweep_cotangents(variant, kind, B, cot, dl):
+    """The row-split reverse sweep with cotangents of E_k / L_k / T_k (main_lena.py:221-228 reads
+    E and L; "all" adds Z's) and V1's per-sample betas, against the reverse sweep after a path-1
+    forward: weight gradients and V1's beta gradients (per-element stores) bit for bit, the
+    scalar-parameter slots within 2e-6 per layer."""
+    from test_gpu_backward import make_train_net, nrel
+    ops = dl.ops
+    L = dl._lib
+    m, n, K = 250, 500, 4
+    d = dict(variant=variant, m=m, n=n, B=B, K=K, seed=5700 + B, perturb=0.1)
+    inp, sd = P.build_problem(d)
+    net = make_train_net(dl, variant, inp, sd, K).cuda()
+    X = torch.from_numpy(inp["X"]).cuda()
+    with torch.no_grad():
+        tables = net._tables(X.device)
+    W = [w.detach() for w in net._weights()]
+    args = (net.VARIANT, X, net.A, W, net.Z0, net.E0, net.L0)
+    lk = L.LOSS_LASSO if kind == "lasso" else L.LOSS_L1L1
+    out = {}
+    for fl in (0, L.F_NO_ROWSPLIT):
+        with torch.no_grad():
+            r = ops.dladmm_forward(*args, keep_all=True, want_T=True, want_P=True, loss_kind=lk,
+                                   flags=fl, **tables)
+        g = torch.Generator(device="cuda").manual_seed(B)
+        rnd = lambda rows, cnt: [torch.randn(rows, B, generator=g, device="cuda") / B  # noqa: E731
+                                 for _ in range(cnt)]
+        gE, gL, gT = rnd(m, K), rnd(m, K), rnd(m, r.T.shape[0])
+        gZ = rnd(n, K) if cot == "all" else None
+        out[fl] = (r.path, ops.dladmm_backward(*args, r, gZ=gZ, gE=gE, gL=gL, gT=gT, **tables))
+    (fp, rs), (fp1, cl) = out[0], out[L.F_NO_ROWSPLIT]
+    assert fp == 5 and fp1 == 1 and rs.path == 2 and cl.path == 1
+    assert torch.equal(rs.gW, cl.gW)
+    if variant == "v1":
+        for a, b in zip(rs.g_beta1 + rs.g_beta2, cl.g_beta1 + cl.g_beta2):
+            assert torch.equal(a, b)
+    else:
+        gs_r, gs_c = rs.g_scalar.cpu().numpy(), cl.g_scalar.cpu().numpy()
+        for k in range(K):
+            assert nrel(gs_r[k], gs_c[k]) <= 2e-6, (k, gs_r[k], gs_c[k])
