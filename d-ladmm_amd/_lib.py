@@ -21,6 +21,7 @@ NSCALAR = 8
 F_PER_LAYER, F_BF16_WIDE, F_BWD_PER_LAYER, F_BWD_UNFUSED, F_BWD_NO_ZMASK, F_WGRAD_F32 = \
     1, 2, 4, 8, 16, 32
 F_NO_ROWSPLIT = 64
+F_NO_XSPLIT = 128
 # enum dladmm_variant
 V1_LENA, V2_LTHETA, V3_FULL, V4_SCALAR, V5_TIED, V6_LASSO = 1, 2, 3, 4, 5, 6
 # enum dladmm_loss_kind

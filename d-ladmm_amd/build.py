@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 UNITS = ("dladmm_capi.hip", "dladmm_fused.hip", "dladmm_fused_savep.hip", "dladmm_fused_x3.hip",
-         "dladmm_fused_x3_savep.hip", "dladmm_fused_rs.hip",
+         "dladmm_fused_x3_savep.hip", "dladmm_fused_rs.hip", "dladmm_fused_xs.hip",
          "dladmm_layered.hip", "dladmm_backward.hip", "dladmm_lskm.hip", "dladmm_eval.hip",
          "dladmm_tile_bf16.hip", "dladmm_wgrad_x3.hip",
          "dladmm_reverse.hip", "dladmm_reverse_rs.hip",

@@ -335,6 +335,7 @@ struct Plan {
   bool narrow;  // bf16 path: 128-column tiles (two workgroups per CU; DLADMM_F_BF16_WIDE: 256)
   size_t off_ap, off_wp, off_v, off_zb, off_zw, off_ew, off_lw, off_loss, total;
   size_t off_btab;            // path 1, V1: device tables of the per-layer beta pointers
+  size_t off_xch, off_xcnt;   // path 6: exchange buffers, hand-off counters
   size_t off_wexp, off_umax;  // path 4
   int64_t ldzw;               // path 4: lean-mode Z_k workspace row stride
 };
@@ -432,6 +433,14 @@ inline bool use_rowsplit(const dladmm_fwd_desc* d, int shape) {
          ceil_div(d->batch, 16) <= DLADMM_RS_PER_CU * device_cus();
 }
 
+// Path 6: the row split spread over four workgroups per 16 columns (exchange through global
+// memory once per product), where the whole grid fits one workgroup per CU (B <= 1,024 on 256
+// CUs): a quarter of path 5's MFMA cycles per SIMD.  DLADMM_F_NO_XSPLIT keeps path 5.
+inline bool use_xsplit(const dladmm_fwd_desc* d, int shape) {
+  return use_rowsplit(d, shape) && !(d->flags & DLADMM_F_NO_XSPLIT) &&
+         xs_grid(d->batch) <= device_cus();
+}
+
 inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
   *p = Plan{};
   const int s = pick_shape(d->m, d->n);
@@ -467,13 +476,13 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
     return 0;
   }
   if (s >= 0 && fits_32bit(d) && !force_layered && !bf16) {
-    p->path = use_rowsplit(d, s) ? 5 : 1;
+    p->path = use_xsplit(d, s) ? 6 : use_rowsplit(d, s) ? 5 : 1;
     p->shape = s;
     p->MP = kShapeMP[s];
     p->NP = kShapeNP[s];
     p->tiles = ceil_div(d->batch, kTileCols);
     // per-column objective slots: every column the grid covers (64 / 16 per workgroup)
-    p->ldl = p->path == 5 ? ceil_div(d->batch, 16) * 16 : p->tiles * kTileCols;
+    p->ldl = p->path >= 5 ? ceil_div(d->batch, 16) * 16 : p->tiles * kTileCols;
     p->nslots = p->ldl;  // one slice
     const size_t frag_bytes = (size_t)p->MP * p->NP * sizeof(float);
     p->off_ap = 0;
@@ -482,6 +491,12 @@ inline int make_plan(const dladmm_fwd_desc* d, Plan* p) {
     p->off_btab = p->off_loss + align256((size_t)2 * K * p->nslots * sizeof(float));
     p->total = p->off_btab +
                (d->variant == DLADMM_V1_LENA ? align256((size_t)2 * K * sizeof(void*)) : 0);
+    if (p->path == 6) {  // exchange buffers and hand-off counters of every (padded) group
+      const size_t groups = (size_t)xs_grid(d->batch) / 4;
+      p->off_xch = p->total;
+      p->off_xcnt = p->off_xch + align256(groups * xs_group_floats() * sizeof(float));
+      p->total = p->off_xcnt + align256(groups * 64 * sizeof(unsigned));
+    }
     return 0;
   }
   // per-layer path; path 3 = bf16 operands: 2-D tiles of 256 x 256, k-blocks of 32
@@ -605,7 +620,14 @@ inline int run_fused(const dladmm_fwd_desc* d, const Plan& p, char* ws, hipStrea
   if (d->ev_kernel_start) {
     if (hipError_t e = hipEventRecord((hipEvent_t)d->ev_kernel_start, s)) return (int)e;
   }
-  hipError_t e = p.path == 5
+  if (p.path == 6) {
+    a.xch = (float*)(ws + p.off_xch);
+    a.xstride = (int64_t)xs_group_floats();
+    a.xcnt = (unsigned*)(ws + p.off_xcnt);
+    if (hipError_t e = zero_async(a.xcnt, p.total - p.off_xcnt, s)) return (int)e;
+  }
+  hipError_t e = p.path == 6 ? launch_fused_xs(p.shape, d->variant, a, s)
+                 : p.path == 5
                     ? launch_fused_rs(p.shape, d->variant, a, ceil_div(d->batch, 16), s)
                     : (savep ? launch_fused_shape_savep : launch_fused_shape)(p.shape, d->variant,
                                                                              a, p.tiles, s);
@@ -888,7 +910,7 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
   p->x3w = f.precision == DLADMM_PREC_F32_SPLIT && !bwd_flag(f, DLADMM_F_WGRAD_F32);
   // the forward stored A Z_k only on the fused paths, fp32 and split-f16 (fwd_desc.P)
   p->saved_p = f.P != nullptr && f.keep_all &&
-               (p->fwd.path == 1 || p->fwd.path == 4 || p->fwd.path == 5);
+               (p->fwd.path == 1 || p->fwd.path == 4 || p->fwd.path >= 5);
   const int m = f.m, n = f.n;
   const int64_t B = f.batch;
   p->MB = ceil_div(m, 16);
@@ -946,7 +968,7 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
       // for every forward precision)
       // At most one workgroup per CU: backward (V4, K = 15, fused objective) 0.68 vs 1.32 ms at
       // B = 25, 1.03 vs 1.66 at 4,096, but 2.42 vs 1.90 at 10,000 (profiles/r06_rowsplit_ab.json)
-      p->rrs = p->fwd.path == 5 && f.precision == DLADMM_PREC_F32 &&
+      p->rrs = p->fwd.path >= 5 && f.precision == DLADMM_PREC_F32 &&
                reverse_rs_supports(p->fwd.shape, f.variant) &&
                ceil_div((int)f.batch, 16) <= device_cus();
       p->rtiles = p->rrs ? ceil_div(f.batch, 16) : ceil_div(f.batch, kTileCols);
@@ -1485,7 +1507,7 @@ int dladmm_fwd_f32(const dladmm_fwd_desc* d, void* stream) {
   if (((uintptr_t)d->workspace) & 255) return DLADMM_E_ALIGN;
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)d->workspace;
-  const int rc = p.path == 1 || p.path == 5 ? run_fused(d, p, ws, s)
+  const int rc = p.path == 1 || p.path >= 5 ? run_fused(d, p, ws, s)
                  : p.path == 4 ? run_fused_x3(d, p, ws, s)
                                : run_layered(d, p, ws, s);
   if (rc) return rc;

@@ -35,6 +35,10 @@ struct FusedArgs {
   float* Zw; int64_t ldzw;
   // diagnostic builds only (X3_STAMP): per-wave cycle sums; DLADMM_DBG_PTR (device address)
   unsigned long long* dbg;
+  // path 6 (dladmm_fused_xs.hip): per-group exchange buffers (xstride floats each) and hand-off
+  // counters (64 per group, zeroed before the launch)
+  float* xch; int64_t xstride;
+  unsigned* xcnt;
 };
 
 
@@ -52,6 +56,11 @@ hipError_t launch_fused_shape_savep(int shape, int variant, const FusedArgs& a, 
 // workgroup, grid = ceil(B / 16)
 bool rs_supports(int shape, int variant);
 hipError_t launch_fused_rs(int shape, int variant, const FusedArgs& a, int grid, hipStream_t s);
+// the smallest batches (path 6, dladmm_fused_xs.hip): four workgroups per 16 columns, exchange
+// through a.xch / a.xcnt; xs_grid(B) workgroups, xs_group_floats() floats per group's buffer
+int xs_grid(int64_t B);
+size_t xs_group_floats();
+hipError_t launch_fused_xs(int shape, int variant, const FusedArgs& a, hipStream_t s);
 // split-f16 fused kernel (DLADMM_PREC_F32_SPLIT); Ap / Wp hold [step][hi|lo] f16 fragments
 bool x3_supports(int variant);
 hipError_t launch_fused_x3_shape(int shape, int variant, const FusedArgs& a, int grid,

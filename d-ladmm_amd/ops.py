@@ -28,7 +28,8 @@ class ForwardResult:
     col_loss: Optional[torch.Tensor] = None  # [K, 2, B] fp32 per-column terms (want_col_loss)
     P: Optional[torch.Tensor] = None  # [K, m, B] A Z_k per layer (want_P: training forwards)
     path: int = 0  # dladmm_fwd_path: the kernel path that ran (1 fused, 2 per-layer, 3 bf16
-                   # tiles, 4 fused split-f16, 5 fused row-split; 0 = nothing launched)
+                   # tiles, 4 fused split-f16, 5 fused row-split, 6 its four-workgroup
+                   # form; 0 = nothing launched)
     flags: int = 0  # the plan options (dladmm_flags) the forward ran with; its backward keeps them
 
 
@@ -36,7 +37,7 @@ _PLAN_FLAGS = contextvars.ContextVar("dladmm_plan_flags", default=0)
 _FLAG_NAMES = {"per_layer": _lib.F_PER_LAYER, "bf16_wide": _lib.F_BF16_WIDE,
                "bwd_per_layer": _lib.F_BWD_PER_LAYER, "bwd_unfused": _lib.F_BWD_UNFUSED,
                "bwd_no_zmask": _lib.F_BWD_NO_ZMASK, "wgrad_f32": _lib.F_WGRAD_F32,
-               "no_rowsplit": _lib.F_NO_ROWSPLIT}
+               "no_rowsplit": _lib.F_NO_ROWSPLIT, "no_xsplit": _lib.F_NO_XSPLIT}
 
 
 @contextlib.contextmanager
@@ -213,7 +214,7 @@ def dladmm_forward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[t
                          f"got {precision!r}")
     d.precision = _PRECISIONS[precision]
     # (path 5, the small-batch row-split kernel, saves no product: with P set the plan is path 1)
-    if want_P and keep_all and out.P is None and L.dladmm_fwd_path(ctypes.byref(d)) in (1, 4, 5):
+    if want_P and keep_all and out.P is None and L.dladmm_fwd_path(ctypes.byref(d)) in (1, 4, 5, 6):
         out.P = torch.empty((K, m, B), device=dev, dtype=torch.float32)
         d.P = out.P.data_ptr()
     if want_col_loss:

@@ -180,8 +180,11 @@ enum dladmm_flags {
   DLADMM_F_BWD_NO_ZMASK = 16,  /* per-layer backward, V2 / V3: form q = W_k Var_k in BK2 instead of
                                   reading the shrink masks off the saved Z_k                       */
   DLADMM_F_WGRAD_F32 = 32,     /* split-f16 backward: the weight gradient on the fp32-MFMA kernel  */
-  DLADMM_F_NO_ROWSPLIT = 64    /* forward: the fused kernel (path 1) where the small-batch
-                                  row-split kernel (path 5) would run (equivalence tests, A/B)    */
+  DLADMM_F_NO_ROWSPLIT = 64,   /* forward: the fused kernel (path 1) where the small-batch
+                                  row-split kernels (paths 5 / 6) would run (equivalence tests,
+                                  A/B)                                                             */
+  DLADMM_F_NO_XSPLIT = 128     /* forward: the one-workgroup row split (path 5) where the
+                                  four-workgroup one (path 6) would run                            */
 };
 
 /* ABI version the library was built with. */

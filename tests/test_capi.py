@@ -41,8 +41,11 @@ def _desc(dl, **kw):
 def test_workspace_and_path(dl):
     L = dl._lib.lib()
     d, _keep = _desc(dl)
-    # B = 1,000 at 256 x 512: the small-batch row-split form of the fused kernel (path 5; up to
-    # three 16-column workgroups per CU -- the plan assumes 256 CUs where no device answers)
+    # B = 1,000 at 256 x 512: the four-workgroup row split (path 6; its 256-workgroup grid fits
+    # one per CU -- the plan assumes 256 CUs where no device answers); no_xsplit: the
+    # one-workgroup row split (path 5, up to three per CU)
+    assert L.dladmm_fwd_path(ctypes.byref(d)) == 6
+    d.flags = dl._lib.F_NO_XSPLIT
     assert L.dladmm_fwd_path(ctypes.byref(d)) == 5
     d.flags = dl._lib.F_NO_ROWSPLIT
     assert L.dladmm_fwd_path(ctypes.byref(d)) == 1
@@ -125,13 +128,15 @@ def test_plan_flags_select_kernels(dl):
     off the reverse sweep; unknown bits change nothing."""
     L = dl._lib.lib()
     d, _keep = _desc(dl)
+    assert L.dladmm_fwd_path(ctypes.byref(d)) == 6
+    d.flags = dl._lib.F_NO_XSPLIT
     assert L.dladmm_fwd_path(ctypes.byref(d)) == 5
     d.flags = dl._lib.F_NO_ROWSPLIT
     assert L.dladmm_fwd_path(ctypes.byref(d)) == 1
     d.flags = dl._lib.F_PER_LAYER
     assert L.dladmm_fwd_path(ctypes.byref(d)) == 2
     d.flags = 1 << 20
-    assert L.dladmm_fwd_path(ctypes.byref(d)) == 5
+    assert L.dladmm_fwd_path(ctypes.byref(d)) == 6
     d.precision = dl._lib.PREC_BF16
     for f in (0, dl._lib.F_BF16_WIDE):
         d.flags = f

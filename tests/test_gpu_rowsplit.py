@@ -1,5 +1,9 @@
-"""Path 5, the small-batch row-split form of the fused forward (csrc/dladmm_fused_rs.hip): a
-workgroup per 16 batch columns, each product's output rows split over its 4 waves.
+"""Paths 5 and 6, the small-batch row-split forms of the fused forward: path 5
+(csrc/dladmm_fused_rs.hip) a workgroup per 16 batch columns, each product's output rows split
+over its 4 waves; path 6 (csrc/dladmm_fused_xs.hip) four workgroups per 16 columns, the rows over
+their 16 waves, the column state handed between the workgroups through global memory once per
+product.  Each test runs both: split "xs" = the default plan (path 6 where its grid fits one
+workgroup per CU, B <= 1,024 on 256 CUs), "rs" = plan flag no_xsplit (path 5).
 
 It performs the fused kernel's arithmetic operation for operation, so its outputs must equal
 path 1's (plan flag no_rowsplit) BIT FOR BIT -- every layer's Z, E, L and T -- for V4, V5 (and
@@ -16,6 +20,23 @@ import problems as P
 from test_gpu_parity import _compare, _oracle_case
 
 pytestmark = pytest.mark.gpu
+
+
+def _cus():
+    return torch.cuda.get_device_properties(0).multi_processor_count
+
+
+def _xs_grid(B):
+    """dladmm_fused_xs.hip xs_grid: four workgroups per 16-column group, groups padded to 8."""
+    groups = -(-B // 16)
+    return -(-groups // 8) * 8 * 4
+
+
+def _split(dl, split, B):
+    """(plan flags, expected forward path) of a row-split flavour at batch B."""
+    if split == "rs":
+        return dl._lib.F_NO_XSPLIT, 5
+    return 0, (6 if _xs_grid(B) <= _cus() else 5)
 
 
 def _run(dl, variant, inp, sd, K, keep_all=True, flags=0, **kw):
@@ -37,41 +58,46 @@ def _run(dl, variant, inp, sd, K, keep_all=True, flags=0, **kw):
     return r
 
 
+@pytest.mark.parametrize("split", ["xs", "rs"])
 @pytest.mark.parametrize("variant", ["v1", "v4", "v5", "v6"])
 @pytest.mark.parametrize("B", [1, 20, 77, 300, 1000])
-def test_rowsplit_bit_equal_to_fused(variant, B, dl):
+def test_rowsplit_bit_equal_to_fused(variant, B, split, dl):
     m, n, K = 250, 500, 6
     d = dict(variant=variant, m=m, n=n, B=B, K=K, seed=5100 + B, perturb=0.2,
              wscale=0.4 if variant == "v1" else P.VARIANT_SPECS[variant]["wscale"])
     inp, sd = P.build_problem(d)
-    rs = _run(dl, variant, inp, sd, K)
+    fl, want = _split(dl, split, B)
+    rs = _run(dl, variant, inp, sd, K, flags=fl)
     fu = _run(dl, variant, inp, sd, K, flags=dl._lib.F_NO_ROWSPLIT)
-    assert rs.path == 5 and fu.path == 1
+    assert rs.path == want and fu.path == 1
     for nm in ("Z", "E", "L", "T"):
         a, b = getattr(rs, nm), getattr(fu, nm)
         assert a.shape == b.shape, nm
         assert torch.equal(a, b), (nm, float((a - b).abs().max()))
 
 
+@pytest.mark.parametrize("split", ["xs", "rs"])
 @pytest.mark.parametrize("shape", [(256, 512), (100, 300), (65, 257)])
-def test_rowsplit_shapes_and_lean_mode(shape, dl):
+def test_rowsplit_shapes_and_lean_mode(shape, split, dl):
     """Ragged m / n inside the 256 x 512 instantiation (padded rows stay zero), lean mode (last
     layer only), against path 1 bit for bit."""
     m, n = shape
     K, B = 4, 45
     d = dict(variant="v4", m=m, n=n, B=B, K=K, seed=5200 + m, perturb=0.2, wscale=0.4)
     inp, sd = P.build_problem(d)
+    fl, want = _split(dl, split, B)
     for keep_all in (True, False):
-        rs = _run(dl, "v4", inp, sd, K, keep_all=keep_all)
+        rs = _run(dl, "v4", inp, sd, K, keep_all=keep_all, flags=fl)
         fu = _run(dl, "v4", inp, sd, K, keep_all=keep_all, flags=dl._lib.F_NO_ROWSPLIT)
-        assert rs.path == 5 and fu.path == 1
+        assert rs.path == want and fu.path == 1
         for nm in ("Z", "E", "L", "T"):
             assert torch.equal(getattr(rs, nm), getattr(fu, nm)), (keep_all, nm)
 
 
+@pytest.mark.parametrize("split", ["xs", "rs"])
 @pytest.mark.parametrize("variant", ["v1", "v4", "v6"])
 @pytest.mark.parametrize("B", [20, 25, 300])
-def test_rowsplit_training_forward(variant, B, dl):
+def test_rowsplit_training_forward(variant, B, split, dl):
     """A training forward on path 5 (the reference loops' batches of 20 / 25): the saved
     products P_k = A Z_k bit for bit with path 1's, the fused objective's per-layer sums and
     per-column terms to fp32 rounding (each wave sums a quarter of the rows, then the quarters)."""
@@ -82,9 +108,10 @@ def test_rowsplit_training_forward(variant, B, dl):
     L = dl._lib
     kind = L.LOSS_LASSO if variant == "v6" else L.LOSS_L1L1
     kw = dict(want_P=True, loss_kind=kind, want_col_loss=True)
-    rs = _run(dl, variant, inp, sd, K, **kw)
+    fl, want = _split(dl, split, B)
+    rs = _run(dl, variant, inp, sd, K, flags=fl, **kw)
     fu = _run(dl, variant, inp, sd, K, flags=L.F_NO_ROWSPLIT, **kw)
-    assert rs.path == 5 and fu.path == 1
+    assert rs.path == want and fu.path == 1
     for nm in ("Z", "E", "L", "T", "P"):
         assert torch.equal(getattr(rs, nm), getattr(fu, nm)), nm
     # 1e-5: the fused objective's bar elsewhere (test_gpu_configs objective_vs_reduction)
@@ -94,19 +121,21 @@ def test_rowsplit_training_forward(variant, B, dl):
                                rtol=1e-5, atol=1e-6)
 
 
-def test_rowsplit_vs_oracle(dl, oracle):
+@pytest.mark.parametrize("split", ["xs", "rs"])
+def test_rowsplit_vs_oracle(split, dl, oracle):
     """Independent of path 1: the oracle at the fp32 bar, V4 at m=250 n=500 K=15, B=100."""
     m, n, K, B = 250, 500, 15, 100
     inp, sd, ref = _oracle_case(oracle, "v4", m, n, B, K, seed=5300)
-    r = _run(dl, "v4", inp, sd, K)
-    assert r.path == 5
-    _compare((list(r.Z), list(r.E), list(r.L), list(r.T)), ref, tag="rowsplit v4 B=100",
+    fl, want = _split(dl, split, B)
+    r = _run(dl, "v4", inp, sd, K, flags=fl)
+    assert r.path == want
+    _compare((list(r.Z), list(r.E), list(r.L), list(r.T)), ref, tag=f"rowsplit {split} v4 B=100",
              path="f32")
 
 
 def test_km_ground_truth_on_rowsplit(dl):
     """The test scripts' KM ground truth (V5, W = A^T shared, K iterations) at m=250 n=500, B=20:
-    path 5 equals path 1 bit for bit over 300 iterations."""
+    paths 6 and 5 equal path 1 bit for bit over 300 iterations."""
     from test_gpu_lskm import make
     d = dict(variant="v4", m=250, n=500, B=20, K=3, seed=5400, perturb=0.1)
     inp, sd = P.build_problem(d)
@@ -115,20 +144,24 @@ def test_km_ground_truth_on_rowsplit(dl):
     X = torch.from_numpy(inp["X"]).cuda()
     ops = dl.ops
     Z, E, L, T = net(X, False, False, False, K=300)
+    with ops.plan_flags(no_xsplit=True):
+        Z5, E5, L5, T5 = net(X, False, False, False, K=300)
     with ops.plan_flags(no_rowsplit=True):
         Zf, Ef, Lf, Tf = net(X, False, False, False, K=300)
-    for a, b in zip(Z + E + L + T, Zf + Ef + Lf + Tf):
+    for a, a5, b in zip(Z + E + L + T, Z5 + E5 + L5 + T5, Zf + Ef + Lf + Tf):
         assert torch.equal(a, b)
+        assert torch.equal(a5, b)
 
 
 def test_rowsplit_plan_scope(dl):
-    """Path 5 at batches of at most three 16-column workgroups per CU, for V1 / V4 / V5 / V6 at
-    the 256 x 512 shape, inference or training (fused objective, saved product); fp32 only."""
+    """Path 6 where its grid fits one workgroup per CU, path 5 up to three 16-column workgroups
+    per CU, for V1 / V4 / V5 / V6 at the 256 x 512 shape, inference or training (fused
+    objective, saved product); fp32 only."""
     L = dl._lib
     m, n, K = 250, 500, 3
     cus = torch.cuda.get_device_properties(0).multi_processor_count
 
-    def path(variant="v4", B=64, loss=0, P_=False, mn=(m, n)):
+    def path(variant="v4", B=64, loss=0, P_=False, mn=(m, n), flags=0):
         d = dict(variant=variant, m=mn[0], n=mn[1], B=B, K=K, seed=5500, perturb=0.1)
         inp, sd = P.build_problem(d)
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
@@ -137,15 +170,19 @@ def test_rowsplit_plan_scope(dl):
                   E0=t(inp["E0"]), L0=t(inp["L0"]), layers=K).cuda()
         r = dl.ops.dladmm_forward(net.VARIANT, t(inp["X"]), net.A,
                                   [w.detach() for w in net._weights()], net.Z0, net.E0, net.L0,
-                                  loss_kind=loss, want_P=P_, **net._tables(net.A.device))
+                                  loss_kind=loss, want_P=P_, flags=flags,
+                                  **net._tables(net.A.device))
         return r.path
-    assert path() == 5
-    assert path(variant="v5") == 5 and path(variant="v6") == 5
+    assert path() == 6
+    assert path(flags=L.F_NO_XSPLIT) == 5
+    assert path(variant="v5") == 6 and path(variant="v6") == 6
+    xs_max = cus // 32 * 8 * 16   # the largest batch whose padded xs grid fits the CUs
+    assert path(B=xs_max) == 6 and path(B=xs_max + 1) == 5
     assert path(B=48 * cus) == 5
     assert path(B=48 * cus + 1) == 1
-    assert path(loss=L.LOSS_L1L1) == 5
-    assert path(P_=True) == 5
-    assert path(variant="v1") == 5
+    assert path(loss=L.LOSS_L1L1) == 6
+    assert path(P_=True) == 6
+    assert path(variant="v1") == 6
     assert path(variant="v2") == 1 and path(variant="v3") == 1   # per-row parameters
     assert path(mn=(64, 128)) == 1   # the 64 x 256 instantiation: whole-row waves
 
@@ -191,7 +228,7 @@ def test_rowsplit_reverse_sweep(variant, kind, B, gz, dl):
         coef = (torch.rand(K, 2, device="cuda", generator=g) *
                 torch.tensor([1e-2, 1.0], device="cuda")).contiguous()
     (fp, rs), (fp1, cl) = out[0], out[L.F_NO_ROWSPLIT]
-    assert fp == 5 and fp1 == 1 and rs.path == 2 and cl.path == 1
+    assert fp in (5, 6) and fp1 == 1 and rs.path == 2 and cl.path == 1
     assert torch.equal(rs.gW, cl.gW)
     gs_r, gs_c = rs.g_scalar.cpu().numpy(), cl.g_scalar.cpu().numpy()
     for k in range(K):
@@ -231,7 +268,7 @@ def test_rowsplit_reverse_sweep_cotangents(variant, kind, B, cot, dl):
         gZ = rnd(n, K) if cot == "all" else None
         out[fl] = (r.path, ops.dladmm_backward(*args, r, gZ=gZ, gE=gE, gL=gL, gT=gT, **tables))
     (fp, rs), (fp1, cl) = out[0], out[L.F_NO_ROWSPLIT]
-    assert fp == 5 and fp1 == 1 and rs.path == 2 and cl.path == 1
+    assert fp in (5, 6) and fp1 == 1 and rs.path == 2 and cl.path == 1
     assert torch.equal(rs.gW, cl.gW)
     if variant == "v1":
         for a, b in zip(rs.g_beta1 + rs.g_beta2, cl.g_beta1 + cl.g_beta2):

@@ -5,7 +5,7 @@ each dladmm_forward call): V4 (or --variant) at m x n, K layers, the fused L1L1 
 and (--no-rowsplit) with the plan flag no_rowsplit.  Prints one JSON line (median ms, path).
 
     python tools/bench_fwd_ab.py --libs main,d-ladmm_amd/lib/abl/x/libdladmm_hip.so \
-        --batches 10000,16384 [--reps 10] [--no-rowsplit]
+        --batches 10000,16384 [--reps 10] [--no-rowsplit | --flag-set 0,128,64]
 """
 from __future__ import annotations
 
@@ -34,6 +34,9 @@ def main():
     ap.add_argument("--layers", type=int, default=15)
     ap.add_argument("--no-loss", action="store_true")
     ap.add_argument("--no-rowsplit", action="store_true")
+    ap.add_argument("--flag-set", default="",
+                    help="comma-separated plan-flag values to compare, e.g. 0,128,64 "
+                         "(default plan, no_xsplit, no_rowsplit); overrides --no-rowsplit")
     a = ap.parse_args()
     dl = importlib.import_module("d-ladmm_amd")
     ops = importlib.import_module("d-ladmm_amd.ops")
@@ -46,7 +49,11 @@ def main():
         L.LIB_PATH = os.path.join(ROOT, "d-ladmm_amd", "lib", "libdladmm_hip.so") \
             if spec == "main" else os.path.join(ROOT, spec)
         libs[spec] = L.lib()
-    modes = [(s, False) for s in libs] + ([(s, True) for s in libs] if a.no_rowsplit else [])
+    if a.flag_set:
+        modes = [(s, int(f)) for s in libs for f in a.flag_set.split(",")]
+    else:
+        modes = [(s, 0) for s in libs] + \
+            ([(s, L.F_NO_ROWSPLIT) for s in libs] if a.no_rowsplit else [])
     calls = {}
     torch.manual_seed(1126)
     for B in Bs:
@@ -69,7 +76,7 @@ def main():
                 r = ops.dladmm_forward(net.VARIANT, X, net.A, W, net.Z0, net.E0, net.L0,
                                        keep_all=True, want_T=True,
                                        loss_kind=0 if a.no_loss else L.LOSS_L1L1,
-                                       flags=L.F_NO_ROWSPLIT if f else 0, **tables)
+                                       flags=f, **tables)
                 ev1.record()
                 torch.cuda.synchronize()
                 paths[(s, f, B)] = r.path
@@ -78,7 +85,7 @@ def main():
                 del r
     res = {}
     for (s, f, B), t in times.items():
-        res.setdefault(s + (":no_rowsplit" if f else ""), {})[str(B)] = {
+        res.setdefault(s + (f":flags={f}" if f else ""), {})[str(B)] = {
             "median_ms": float(np.median(t)), "min_ms": float(np.min(t)), "path": paths[(s, f, B)]}
     res["config"] = dict(variant=a.variant, m=a.m, n=a.n, K=a.layers, reps=a.reps,
                          loss=not a.no_loss)
