@@ -199,8 +199,10 @@ size_t dladmm_fwd_workspace_bytes(const dladmm_fwd_desc* d);
    5 = fused kernel with each workgroup's rows split over its waves (16 columns per workgroup):
    small fp32 batches (at most three workgroups per CU) of V1 / V4 / V5 / V6 at m <= 256,
    n <= 512 (and m > 64 or n > 256) -- the same arithmetic as path 1, bit for bit (the fused
-   objective's per-column sums: to fp32 rounding); <0 = DLADMM_E_* error.  Host-only: no device
-   work. */
+   objective's per-column sums: to fp32 rounding), 6 = the same split over four workgroups per
+   16 columns (16 waves; the column state handed between them through the workspace once per
+   product) where that grid fits one workgroup per CU (B <= 1,024 on 256 CUs), also bit for bit;
+   <0 = DLADMM_E_* error.  Host-only: no device work. */
 int dladmm_fwd_path(const dladmm_fwd_desc* d);
 
 /* Enqueue the whole K-layer forward on `stream` (hipStream_t). */
@@ -272,7 +274,7 @@ size_t dladmm_bwd_workspace_bytes(const dladmm_bwd_desc* d);
 
 /* Which kernels the backward runs: 1 = one reverse-sweep kernel for every layer's adjoints,
    2 = the same sweep in its small-batch row-split form (16 columns per workgroup, each
-   product's rows over its waves; after an fp32 path-5 forward of V1 / V4 / V5 / V6, any
+   product's rows over its waves; after an fp32 path-5 / 6 forward of V1 / V4 / V5 / V6, any
    cotangents, at most one 16-column workgroup per CU: gU_k, Var_k, the weight gradients and
    V1's beta gradients bit-equal to path 1's, the scalar-parameter gradients to rounding),
    0 = per-layer kernels,
