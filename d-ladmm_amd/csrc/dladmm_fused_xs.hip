@@ -18,8 +18,9 @@
 // `sc1` loads of the buffer into LDS (MI355X_MICROARCH.md, inter-workgroup visibility, the first
 // hand-off row: valid at any placement).  Members are blocks b, b + 8, b + 16, b + 24, which the
 // dispatcher deals to one XCD (observed, speed only: the hand-off stays in that XCD's L2).  Every
-// spin is bounded (it ends after ~2^22 polls, the outputs then being wrong, never a hang); a group
-// is resident together because the plan launches at most one workgroup per CU.
+// spin is bounded (it ends after ~2^22 polls, never a hang; every output written after a timed-out
+// hand-off is NaN, not silently wrong); a group is resident together because the plan launches at
+// most one workgroup per CU.
 //
 // Arithmetic is path 5's, operation for operation (the same packed fragments, G1 one chain per
 // block over k in order, G2 the two chains summed once, the same elementwise expressions): the
@@ -29,7 +30,18 @@
 #include "dladmm_internal.h"
 
 #ifndef XS_PF
-#define XS_PF 4  // weight-fragment read-ahead (MFMA steps) per wave
+#define XS_PF 8  // weight-fragment read-ahead (MFMA steps) per wave; the first XS_PF steps of each
+                 // pass are fetched during the hand-off before it
+#endif
+#ifndef XS_ABL
+#define XS_ABL 0  // timing ablations only (wrong results): 1 no poll wait, 2 no exchange loads
+                  // into LDS, 4 no exchange stores (tools/ablate_units.py)
+#endif
+#ifndef XS_PRE_LATE
+#define XS_PRE_LATE 1  // 1: fetch the next pass's first fragments right behind the exchange
+                       // loads (the LDS writes wait for those only); 0: before the poll.  V4
+                       // K = 15 (ms, B = 20 / 1,000): 0.201 / 0.214 vs 0.207 / 0.221; read-ahead
+                       // 12: 0.197 / 0.216; before both changes 0.27 (profiles/r06_xsplit_ab.json)
 #endif
 #ifndef XS_SPIN
 #define XS_SPIN (1 << 22)  // bound of every hand-off poll
@@ -77,25 +89,47 @@ __global__ __launch_bounds__(256, 1) void fused_xs_kernel(const FusedArgs a) {
   const rsrc_t rxz = mkrsrc((const float*)xz, (uint32_t)(NB * 64 * 16));
   const rsrc_t rxv = mkrsrc((const float*)xv, (uint32_t)(MB * 64 * 16));
   unsigned hand = 0;
+  __shared__ int xerr;  // sticky: a hand-off timed out
+  if (threadIdx.x == 0) xerr = 0;
+  bool bad = false;
+  // an output value, or NaN once a hand-off has timed out (the outputs of every later product
+  // would be computed on incomplete operands: poisoned, not silently wrong)
+  auto fin = [&](float x) -> float { return bad ? __builtin_nanf("") : x; };
   // hand-off: this member's stores are done; wait for every member's, then the buffer's blocks
   // (sc1: past this CU's L1) into LDS.  Called by every wave of the workgroup.
-  auto handoff = [&](const rsrc_t& rb, f32x4* dst, int nblk) {
+  auto handoff = [&](const rsrc_t& rb, f32x4* dst, auto NBLK_, auto&& pre) {
+    constexpr int nblk = decltype(NBLK_)::value;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if constexpr (!XS_PRE_LATE) pre();  // the next pass's first weight fragments: in flight
+                                        // while lane 0 polls
     hand += kXsMembers;
     if (threadIdx.x == 0) {
       __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       int it = 0;
-      while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hand &&
-             ++it < XS_SPIN)
+      unsigned c = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while (!(XS_ABL & 1) && c < hand && ++it < XS_SPIN) {
         __builtin_amdgcn_s_sleep(1);
+        c = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (!(XS_ABL & 1) && c < hand) xerr = 1;  // a member never arrived: everything from here on is NaN
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < nblk * 64; i += 256)
-      dst[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, i * 16, 0, 16));
+    bad = __builtin_amdgcn_readfirstlane(xerr) != 0;
+    constexpr int per = (XS_ABL & 2) ? 0 : nblk * 64 / 256;  // f32x4 per thread
+    f32x4 t[per > 0 ? per : 1];
+#pragma unroll
+    for (int j = 0; j < per; ++j)
+      t[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           rb, (threadIdx.x + 256 * j) * 16, 0, 16));
+    if constexpr (XS_PRE_LATE) pre();  // issued behind the exchange loads: the LDS writes below
+                                       // wait for those only
+#pragma unroll
+    for (int j = 0; j < per; ++j) dst[threadIdx.x + 256 * j] = t[j];
     __syncthreads();
   };
   auto xstore = [&](const rsrc_t& rb, int blk, const f32x4& val) {
+    if constexpr (XS_ABL & 4) return;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, val), rb, (blk * 64 + lane) * 16, 0, 16);
   };
 
@@ -190,8 +224,8 @@ __global__ __launch_bounds__(256, 1) void fused_xs_kernel(const FusedArgs a) {
       }
       // every slot of the group, padding columns too (their sums are zero): the reduction
       // reads ldl = 16 * groups columns
-      a.lossp[(int64_t)(2 * k + 0) * a.ldl + col] = r0;
-      a.lossp[(int64_t)(2 * k + 1) * a.ldl + col] = lasso ? 0.5f * f0 : f0;
+      a.lossp[(int64_t)(2 * k + 0) * a.ldl + col] = fin(r0);
+      a.lossp[(int64_t)(2 * k + 1) * a.ldl + col] = fin(lasso ? 0.5f * f0 : f0);
     }
   };
 
@@ -212,14 +246,20 @@ __global__ __launch_bounds__(256, 1) void fused_xs_kernel(const FusedArgs a) {
 
   // G1(k): this wave's Z pair; Var (all m rows) from vx.  Pack order 2: pair P's k-block kb at
   // fragments 2 (P MB + kb) + h
-  auto g1_pass = [&](int k, const LayerP& P, rsrc_t rzo) {
+  f32x4 fa[XS_PF], fb[XS_PF];  // the weight-fragment window, shared by the passes
+  auto rw_of = [&](int k) -> rsrc_t {
     const float* wk = a.Wp + (int64_t)(k * a.wstep) * wl + (int64_t)v * MB * 2 * kFrag;
-    const rsrc_t rw = mkrsrc(wk, (uint32_t)(S1 * 2 * kFrag * 4));
-    f32x4 fa[XS_PF], fb[XS_PF];
+    return mkrsrc(wk, (uint32_t)(S1 * 2 * kFrag * 4));
+  };
+  auto pre1 = [&](int k) {  // G1(k)'s first XS_PF steps
+    const rsrc_t rw = rw_of(k);
     static_for<XS_PF>([&](auto I_) {
       constexpr int i = decltype(I_)::value;
       if constexpr (i < S1) { fa[i] = frag(rw, 2 * i * 1024); fb[i] = frag(rw, (2 * i + 1) * 1024); }
     });
+  };
+  auto g1_pass = [&](int k, const LayerP& P, rsrc_t rzo) {
+    const rsrc_t rw = rw_of(k);
     f32x4 ca = zero4, cb = zero4;
     static_for<S1>([&](auto J_) {
       constexpr int s = decltype(J_)::value;
@@ -248,7 +288,7 @@ __global__ __launch_bounds__(256, 1) void fused_xs_kernel(const FusedArgs a) {
         const float z = shrink_u(u, P.thz);
         Zr[h][r] = z;
         zv[r] = z;
-        bstore_s(rzo, vo, row_off(b1o + h, r), z);
+        bstore_s(rzo, vo, row_off(b1o + h, r), fin(z));
         regsum += fabsf(z);
       }
       xstore(rxz, b1o + h, zv);
@@ -260,14 +300,15 @@ __global__ __launch_bounds__(256, 1) void fused_xs_kernel(const FusedArgs a) {
   struct OutR { rsrc_t e, l, t, p; };
   const rsrc_t ra = mkrsrc(a.Ap + ((int64_t)(v >> 1) * NB * 2 + (v & 1)) * kFrag,
                            (uint32_t)((2 * S2 - 1) * kFrag * 4));
-  auto g2_pass = [&](auto PRO_, int k, const LayerP& P, const OutR& O) {
-    constexpr bool PRO = decltype(PRO_)::value;
-    load_betas(k);
-    f32x4 fa[XS_PF];
+  auto pre2 = [&]() {  // G2's first XS_PF steps (A: the same every layer)
     static_for<XS_PF>([&](auto I_) {
       constexpr int i = decltype(I_)::value;
       if constexpr (i < S2) fa[i] = frag(ra, 2 * i * 1024);
     });
+  };
+  auto g2_pass = [&](auto PRO_, int k, const LayerP& P, const OutR& O) {
+    constexpr bool PRO = decltype(PRO_)::value;
+    load_betas(k);
     f32x4 ca = zero4, ca2 = zero4;
     static_for<S2>([&](auto K_) {
       constexpr int s = decltype(K_)::value;
@@ -308,10 +349,10 @@ __global__ __launch_bounds__(256, 1) void fused_xs_kernel(const FusedArgs a) {
       Er[r] = e;
       Lr[r] = l;
       const uint32_t so = row_off(b2o, r);
-      bstore_s(O.e, vo, so, e);
-      bstore_s(O.l, vo, so, l);
-      bstore_s(O.t, vo, so, t);
-      bstore_s(O.p, vo, so, Pv);
+      bstore_s(O.e, vo, so, fin(e));
+      bstore_s(O.l, vo, so, fin(l));
+      bstore_s(O.t, vo, so, fin(t));
+      bstore_s(O.p, vo, so, fin(Pv));
       const float res = x - Pv;
       fit1 += fabsf(res);
       fit2 = __builtin_fmaf(res, res, fit2);
@@ -325,16 +366,17 @@ __global__ __launch_bounds__(256, 1) void fused_xs_kernel(const FusedArgs a) {
   {
     const OutR Op{none, none,
                   mkrsrc(a.keep_all ? a.To : nullptr, (a.keep_all && a.To) ? mbytes : 0u), none};
+    pre2();
     g2_pass(std::true_type{}, -1, layer_params(-1), Op);
   }
   regsum = fit1 = fit2 = 0.f;
-  handoff(rxv, vx, MB);  // Var_0 of the group
+  handoff(rxv, vx, std::integral_constant<int, MB>{}, [&] { if (K > 0) pre1(0); });  // Var_0 of the group
   for (int k = 0; k < K; ++k) {
     const bool st = a.keep_all || k == K - 1;
     const int ko = a.keep_all ? k : 0;
     const LayerP P = layer_params(k);
     g1_pass(k, P, mkrsrc(a.Zo + (int64_t)ko * n * a.ldo, st ? zbytes : 0u));
-    handoff(rxz, zx, NB);  // Z_k of the group
+    handoff(rxz, zx, std::integral_constant<int, NB>{}, pre2);  // Z_k of the group
     const OutR O{mkrsrc(a.Eo + (int64_t)ko * m * a.ldo, st ? mbytes : 0u),
                  mkrsrc(a.Lo + (int64_t)ko * m * a.ldo, st ? mbytes : 0u),
                  mkrsrc(a.To ? a.To + (int64_t)(a.keep_all ? k + 1 : 0) * m * a.ldo : nullptr,
@@ -343,7 +385,8 @@ __global__ __launch_bounds__(256, 1) void fused_xs_kernel(const FusedArgs a) {
                         a.Po && a.keep_all ? mbytes : 0u)};
     g2_pass(std::false_type{}, k, P, O);
     if (lossz) stage_loss();
-    handoff(rxv, vx, MB);  // Var_{k+1} (and the layer's objective partials)
+    handoff(rxv, vx, std::integral_constant<int, MB>{}, [&] { if (k + 1 < K) pre1(k + 1); });  // Var_{k+1} (and the layer's
+                                                                  // objective partials)
     if (lossz) flush_loss(k);
   }
 }
