@@ -843,6 +843,8 @@ struct BwdPlan {
   bool rev;
   int rtiles, rncg;
   bool rrs;  // reverse sweep on the row-split kernel (16 columns per workgroup)
+  bool rxs;  // ... over four workgroups per 16 columns (bwd path 3, after path 6)
+  size_t off_rxcnt, off_rxch;  // rxs: hand-off counters (zeroed with the partials), exchange
   int64_t Rn2, Rm2;
   size_t off_ratp, off_rmtp, off_gu, off_rvar, off_rpart, off_rptab, off_rrow;
 };
@@ -971,7 +973,11 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
       p->rrs = p->fwd.path >= 5 && f.precision == DLADMM_PREC_F32 &&
                reverse_rs_supports(p->fwd.shape, f.variant) &&
                ceil_div((int)f.batch, 16) <= device_cus();
-      p->rtiles = p->rrs ? ceil_div(f.batch, 16) : ceil_div(f.batch, kTileCols);
+      // after a path-6 forward, the same sweep over four workgroups per 16 columns (its grid one
+      // workgroup per CU at most, as the forward's)
+      p->rxs = p->rrs && p->fwd.path == 6;
+      p->rtiles = p->rxs ? xs_grid(f.batch)
+                  : p->rrs ? ceil_div(f.batch, 16) : ceil_div(f.batch, kTileCols);
       p->rncg = p->rtiles * kWaves;
     }
   }
@@ -999,6 +1005,8 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
     // adjoint of E_{k-1} (V4) that the next-lower layer's BK1 reads
     p->off_rvar = o; o += align256(colb * (p->Rm2 + kShapeMP[p->fwd.shape]) * K);
     p->off_rpart = o; o += align256(sizeof(float) * DLADMM_NSCALAR * K * p->rncg);
+    p->off_rxcnt = o;
+    if (p->rxs) o += align256(sizeof(unsigned) * 64 * (size_t)(p->rtiles / 4));
     // the weight gradients of up to wgl layers per launch (one grid over their tiles and
     // chunks; partials <= 256 MiB): no per-layer launch gaps and tails
     const size_t lpart = sizeof(float) * (size_t)p->nchunks * n * m;
@@ -1014,6 +1022,8 @@ inline int make_bwd_plan(const dladmm_bwd_desc* d, BwdPlan* p) {
     const int RS = kShapeMP[p->fwd.shape] > kShapeNP[p->fwd.shape] ? kShapeMP[p->fwd.shape]
                                                                     : kShapeNP[p->fwd.shape];
     if (rowk) o += align256(sizeof(float) * 8 * K * (size_t)RS * p->rncg);
+    p->off_rxch = o;
+    if (p->rxs) o += align256(sizeof(float) * rev_xs_group_floats() * (size_t)(p->rtiles / 4));
     p->total = o;
     return 0;
   }
@@ -1111,8 +1121,14 @@ inline int run_reverse(const dladmm_bwd_desc* d, const BwdPlan& p, char* ws, hip
     r.rowp = f.row_params; r.rstride = f.row_stride;
     r.rpart = (float*)(ws + p.off_rrow);
   }
-  if (hipError_t e = p.rrs ? launch_reverse_rs(shape, f.variant, r, p.rtiles, s)
-                           : launch_reverse_shape(shape, f.variant, r, p.rtiles, s))
+  if (p.rxs) {
+    r.xch = (float*)(ws + p.off_rxch);
+    r.xstride = (int64_t)rev_xs_group_floats();
+    r.xcnt = (unsigned*)(ws + p.off_rxcnt);   // zeroed with the partials above
+  }
+  if (hipError_t e = p.rxs ? launch_reverse_xs(shape, f.variant, r, s)
+                     : p.rrs ? launch_reverse_rs(shape, f.variant, r, p.rtiles, s)
+                             : launch_reverse_shape(shape, f.variant, r, p.rtiles, s))
     return (int)e;
   // weight gradients gW_k = -s1 gU_k Var_k^T (split-K over the batch, fixed-order reduction),
   // layers K-1 .. 0 as the per-layer sweep visits them (a tied weight sums them in that order);
@@ -1539,7 +1555,7 @@ int dladmm_bwd_path(const dladmm_bwd_desc* d) {
   if (int e = validate_bwd(d)) return e;
   BwdPlan p;
   if (int e = make_bwd_plan(d, &p)) return e;
-  return p.rev ? (p.rrs ? 2 : 1) : 0;
+  return p.rev ? (p.rxs ? 3 : p.rrs ? 2 : 1) : 0;
 }
 
 int dladmm_bwd_f32(const dladmm_bwd_desc* d, void* stream) {

@@ -233,6 +233,9 @@ struct RevArgs {
   int has_gz, has_cot;             // cotangents of Z; of E / L / T
   const float* rowp; int64_t rstride;  // V2 / V3: per-row parameter table [K][8][rstride]
   float* rpart;                    // V2 / V3: per-row partials [K][8][rstride][ncg]
+  // the four-workgroup row split (bwd path 3): per-group exchange buffers (xstride floats each)
+  // and hand-off counters (64 per group, zeroed before the launch)
+  float* xch; int64_t xstride; unsigned* xcnt;
 };
 static_assert(sizeof(RevArgs) <= 2048, "kernel argument size");
 bool reverse_supports(int variant);
@@ -242,6 +245,10 @@ hipError_t launch_reverse_shape(int shape, int variant, const RevArgs& a, int gr
 // cotangents
 bool reverse_rs_supports(int shape, int variant);
 hipError_t launch_reverse_rs(int shape, int variant, const RevArgs& a, int grid, hipStream_t s);
+// its four-workgroup form (bwd path 3, after path 6): grid xs_grid(B), exchange a.xch / a.xcnt
+// (rev_xs_group_floats() floats per group)
+size_t rev_xs_group_floats();
+hipError_t launch_reverse_xs(int shape, int variant, const RevArgs& a, hipStream_t s);
 // fused main_lena.py objective (dladmm_lena.hip, dladmm_lena_f32): one workgroup per 64 columns,
 // every layer; mode 0 = per-column partial sums part[K][4][ldl], mode 1 = the cotangents gE / gL
 struct LenaArgs {

@@ -23,27 +23,47 @@
 #ifndef RRS_PF
 #define RRS_PF 4  // weight-fragment read-ahead (MFMA steps) per wave
 #endif
+#ifndef RRS_SPIN
+#define RRS_SPIN (1 << 22)  // bound of every hand-off poll (bwd path 3)
+#endif
 
 namespace dladmm {
 
-template <int MP, int NP, int EMODE, bool GZ, bool COT>
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+// MEM: workgroups per 16-column group.  1 = the one-workgroup form (bwd path 2); 4 = bwd path 3,
+// after a path-6 forward: wave v = 4 member + w of the group's 16 owns G1' pair v and G2' block v
+// (half of an M_k^T pair), and the B operands (gU_k, gP_k) go between the members through the
+// group's exchange buffer once per product, by dladmm_fused_xs.hip's hand-off (sc1 stores, one
+// agent-scope counter add per member, one bounded sc1 poll; NaN adjoints after a timeout)
+template <int MP, int NP, int EMODE, bool GZ, bool COT, int MEM>
 __global__ __launch_bounds__(256, 1) void reverse_rs_kernel(const RevArgs a) {
   constexpr int MB = MP / 16, NB = NP / 16;
-  constexpr int NB4 = NB / kWaves, MB4 = MB / kWaves;
-  static_assert(NB4 % 2 == 0 && MB4 % 2 == 0, "each wave computes whole pairs of blocks");
-  constexpr int S1 = (NB4 / 2) * MB, S2 = (MB4 / 2) * NB;  // MFMA steps of a wave's G1' / G2'
+  constexpr int WPG = kWaves * MEM;                     // waves per 16-column group
+  constexpr int NB4 = NB / WPG, MB4 = MB / WPG;         // output blocks per wave
+  static_assert(NB4 % 2 == 0 && (MB4 % 2 == 0 || MB4 == 1), "G1' whole pairs; G2' pairs or one block");
+  constexpr int HP = MB4 >= 2 ? 2 : 1;                  // G2' blocks per output step group
+  constexpr int S1 = (NB4 / 2) * MB, S2 = (MB4 / HP) * NB;  // MFMA steps of a wave's G1' / G2'
   constexpr bool kAE = EMODE == EM_VVAR;  // the adjoint of E is carried through the workspace
   constexpr bool kV1 = EMODE == EM_V1;     // V1: per-sample betas and their gradients
+  // weight-fragment read-ahead: deeper in the four-workgroup form, whose waves wait on the
+  // weight stream rather than on their MFMAs (dladmm_fused_xs.hip)
+  constexpr int PF = MEM > 1 ? 8 : RRS_PF;
   __shared__ f32x4 gpx[MB * 64];  // gP_k of the 16 columns (G1''s B operand)
   __shared__ f32x4 gux[NB * 64];  // gU_k (G2''s B operand)
 
+  const int xb = blockIdx.x;
+  const int grp = MEM == 1 ? xb : (xb >> 5) * 8 + (xb & 7);  // members share xb % 8 (one XCD)
+  const int mem = MEM == 1 ? 0 : (xb >> 3) & 3;
+  if (MEM > 1 && grp * 16 >= a.B) return;   // a padding group: every member leaves
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int v = mem * kWaves + w;           // wave of the group
   const int g = lane >> 4;
-  const int64_t col = (int64_t)blockIdx.x * 16 + (lane & 15);
+  const int64_t col = (int64_t)grp * 16 + (lane & 15);
   const bool cv = col < a.B;
   const int m = a.m, K = a.K;
-  const int cg = blockIdx.x * kWaves + w;  // partial slot of this wave
+  const int cg = grp * WPG + v;  // partial slot of this wave
   const uint32_t lqm = __builtin_amdgcn_readfirstlane(a.loss_kind) == DLADMM_LOSS_LASSO ? ~0u : 0u;
   const int64_t ldo = a.ldo, ml = (int64_t)m * ldo, zl = (int64_t)a.n * ldo;
   auto lane_off = [&](int64_t ld, bool ok) -> uint32_t {
@@ -53,8 +73,55 @@ __global__ __launch_bounds__(256, 1) void reverse_rs_kernel(const RevArgs a) {
   const uint32_t ldo4 = (uint32_t)(ldo * 4), ldw4 = (uint32_t)(a.ldw * 4);
   const uint32_t aeo = (uint32_t)(a.aer * a.ldw * 4), vas4 = (uint32_t)(a.vas * 4);
   const uint32_t mbytes = (uint32_t)(ml * 4);
-  const int b1o = w * NB4, b2o = w * MB4;
+  const int b1o = v * NB4, b2o = v * MB4;
   const rsrc_t none = mkrsrc(nullptr, 0u);
+  // MEM = 4: the group's exchange buffer (gU blocks [NB][64] f32x4, then gP blocks [MB][64]) and
+  // its hand-off counter; MEM = 1: a workgroup barrier
+  __shared__ int xerr;  // sticky: a hand-off timed out
+  if (threadIdx.x == 0) xerr = 0;
+  bool bad = false;
+  auto fin = [&](float x) -> float { return bad ? __builtin_nanf("") : x; };
+  const f32x4* xu = (const f32x4*)(MEM > 1 ? a.xch + (int64_t)grp * a.xstride : nullptr);
+  const rsrc_t rxu = mkrsrc((const float*)xu, MEM > 1 ? (uint32_t)(NB * 64 * 16) : 0u);
+  const rsrc_t rxp = mkrsrc((const float*)(xu + NB * 64), MEM > 1 ? (uint32_t)(MB * 64 * 16) : 0u);
+  unsigned* cnt = MEM > 1 ? a.xcnt + grp * 64 : nullptr;
+  unsigned hand = 0;
+  auto xstore = [&](const rsrc_t& rb, int blk, const f32x4& val) {
+    if constexpr (MEM > 1)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, val), rb,
+                                             (blk * 64 + lane) * 16, 0, 16);
+  };
+  auto handoff = [&](const rsrc_t& rb, f32x4* dst, auto NBLK_) {
+    if constexpr (MEM == 1) {
+      __syncthreads();
+    } else {
+      constexpr int nblk = decltype(NBLK_)::value;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      hand += MEM;
+      if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int it = 0;
+        unsigned c = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (c < hand && ++it < RRS_SPIN) {
+          __builtin_amdgcn_s_sleep(1);
+          c = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (c < hand) xerr = 1;
+      }
+      __syncthreads();
+      bad = __builtin_amdgcn_readfirstlane(xerr) != 0;
+      constexpr int per = nblk * 64 / 256;
+      f32x4 t[per];
+#pragma unroll
+      for (int q = 0; q < per; ++q)
+        t[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rb, (threadIdx.x + 256 * q) * 16, 0, 16));
+#pragma unroll
+      for (int q = 0; q < per; ++q) dst[threadIdx.x + 256 * q] = t[q];
+      __syncthreads();
+    }
+  };
   // a wave-uniform (pointer, size) buffer view (readfirstlane: the selects stay in SGPRs)
   auto urs = [](const float* p, uint32_t bytes) -> rsrc_t {
     const uint64_t v = (uint64_t)p;
@@ -94,7 +161,7 @@ __global__ __launch_bounds__(256, 1) void reverse_rs_kernel(const RevArgs a) {
   auto flush = [&](int layer, int slot, float v) {
     if constexpr (kV1) return;  // V1: per-sample betas (element gradients), fixed thresholds
     const float s = wave_sum(v);
-    if (lane == 0) a.part[((int64_t)layer * DLADMM_NSCALAR + slot) * a.ncg + cg] = s;
+    if (lane == 0) a.part[((int64_t)layer * DLADMM_NSCALAR + slot) * a.ncg + cg] = fin(s);
   };
   auto flush_bk1 = [&](int j) {
     if constexpr (kV1) return;
@@ -160,8 +227,8 @@ __global__ __launch_bounds__(256, 1) void reverse_rs_kernel(const RevArgs a) {
         pz[b][r] = ld(rz, vo, so);
         if constexpr (GZ) pg[b][r] = ld(rgz, vo, so);
       }
-    f32x4 fa[RRS_PF], fb[RRS_PF];
-    static_for<RRS_PF>([&](auto I_) {
+    f32x4 fa[PF], fb[PF];
+    static_for<PF>([&](auto I_) {
       constexpr int i = decltype(I_)::value;
       if constexpr (i < S1) frag2(rat, I_, fa[i], fb[i]);
     });
@@ -172,9 +239,9 @@ __global__ __launch_bounds__(256, 1) void reverse_rs_kernel(const RevArgs a) {
         constexpr int jb = decltype(J_)::value;
         constexpr int s = pp * MB + jb;
         const f32x4 v = gpx[jb * 64 + lane];
-        const f32x4 wa = fa[s % RRS_PF], wb = fb[s % RRS_PF];
-        if constexpr (s + RRS_PF < S1)
-          frag2(rat, std::integral_constant<int, s + RRS_PF>{}, fa[s % RRS_PF], fb[s % RRS_PF]);
+        const f32x4 wa = fa[s % PF], wb = fb[s % PF];
+        if constexpr (s + PF < S1)
+          frag2(rat, std::integral_constant<int, s + PF>{}, fa[s % PF], fb[s % PF]);
         ca = mfma4(wa.x, v[0], ca);
         cb = mfma4(wb.x, v[0], cb);
         ca = mfma4(wa.y, v[1], ca);
@@ -199,10 +266,11 @@ __global__ __launch_bounds__(256, 1) void reverse_rs_kernel(const RevArgs a) {
           const float gU = ga + gb;
           psz += gb - ga;
           AZ[lb][r] = gU;
-          gu4[r] = gU;
-          bstore_s(rg, vw, row_off(b1o + lb, r, ldw4), gU);
+          gu4[r] = fin(gU);
+          bstore_s(rg, vw, row_off(b1o + lb, r, ldw4), gu4[r]);
         }
         gux[(b1o + lb) * 64 + lane] = gu4;
+        xstore(rxu, b1o + lb, gu4);
       });
     });
     flush(k, DLADMM_P_THETA_Z, psz);
@@ -260,10 +328,10 @@ __global__ __launch_bounds__(256, 1) void reverse_rs_kernel(const RevArgs a) {
     float op[2][11][4];
     auto load_pair = [&](int pp) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
+      for (int h = 0; h < HP; ++h)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int b = 2 * pp + h;
+          const int b = HP * pp + h;
           const uint32_t so = row_off(b2o + b, r, ldo4);
           op[h][O_P][r] = ld(oP, vo, so);
           op[h][O_L][r] = ld(oL, vo, so);
@@ -284,17 +352,31 @@ __global__ __launch_bounds__(256, 1) void reverse_rs_kernel(const RevArgs a) {
           }
         }
     };
-    const rsrc_t rmt = MODE == 2 ? none
-                                 : mkrsrc(a.Mtp + (int64_t)k * wl + (int64_t)(b2o / 2) * NB * 2 * kFrag,
-                                          (uint32_t)(S2 * 2 * kFrag * 4));
-    f32x4 fa[RRS_PF], fb[RRS_PF];
+    // M_k^T: HP = 2, this wave's pairs from b2o / 2 on (steps read fragments 2s, 2s + 1);
+    // HP = 1, half b2o & 1 of pair b2o / 2 (fragments 2 (P NB + kb) + h0: step s at 2s)
+    const rsrc_t rmt =
+        MODE == 2 ? none
+        : HP == 2 ? mkrsrc(a.Mtp + (int64_t)k * wl + (int64_t)(b2o / 2) * NB * 2 * kFrag,
+                           (uint32_t)(S2 * 2 * kFrag * 4))
+                  : mkrsrc(a.Mtp + (int64_t)k * wl + ((int64_t)(b2o >> 1) * NB * 2 + (b2o & 1)) * kFrag,
+                           (uint32_t)((2 * S2 - 1) * kFrag * 4));
+    f32x4 fa[PF], fb[HP == 2 ? PF : 1];
+    auto fetch = [&](auto S_, int slot) {
+      constexpr int st = decltype(S_)::value;
+      if constexpr (HP == 2) {
+        frag2(rmt, S_, fa[slot], fb[slot]);
+      } else {
+        fa[slot] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 rmt, (int)vf, 2 * st * 1024, 0));
+      }
+    };
     if constexpr (MODE != 2) {
-      static_for<RRS_PF>([&](auto I_) {
+      static_for<PF>([&](auto I_) {
         constexpr int i = decltype(I_)::value;
-        if constexpr (i < S2) frag2(rmt, I_, fa[i], fb[i]);
+        if constexpr (i < S2) fetch(I_, i);
       });
     }
-    static_for<MB4 / 2>([&](auto P_) {
+    static_for<MB4 / HP>([&](auto P_) {
       constexpr int pp = decltype(P_)::value;
       load_pair(pp);
       f32x4 qa4[2] = {zero4, zero4};
@@ -304,25 +386,26 @@ __global__ __launch_bounds__(256, 1) void reverse_rs_kernel(const RevArgs a) {
           constexpr int kb = decltype(K_)::value;
           constexpr int s = pp * NB + kb;
           const f32x4 u = gux[kb * 64 + lane];
-          const f32x4 wa = fa[s % RRS_PF], wb = fb[s % RRS_PF];
-          if constexpr (s + RRS_PF < S2)
-            frag2(rmt, std::integral_constant<int, s + RRS_PF>{}, fa[s % RRS_PF], fb[s % RRS_PF]);
+          const f32x4 wa = fa[s % PF];
+          const f32x4 wb = fb[HP == 2 ? s % PF : 0];
+          if constexpr (s + PF < S2)
+            fetch(std::integral_constant<int, s + PF>{}, s % PF);
           ca = mfma4(wa.x, u[0], ca);
-          cb = mfma4(wb.x, u[0], cb);
+          if constexpr (HP == 2) cb = mfma4(wb.x, u[0], cb);
           ca = mfma4(wa.y, u[1], ca);
-          cb = mfma4(wb.y, u[1], cb);
+          if constexpr (HP == 2) cb = mfma4(wb.y, u[1], cb);
           ca = mfma4(wa.z, u[2], ca);
-          cb = mfma4(wb.z, u[2], cb);
+          if constexpr (HP == 2) cb = mfma4(wb.z, u[2], cb);
           ca = mfma4(wa.w, u[3], ca);
-          cb = mfma4(wb.w, u[3], cb);
+          if constexpr (HP == 2) cb = mfma4(wb.w, u[3], cb);
         });
         qa4[0] = ca;
         qa4[1] = cb;
       }
       // epilogue rows (the reverse sweep's epi2_row)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int lb = 2 * pp + h;
+    for (int h = 0; h < HP; ++h) {
+      const int lb = HP * pp + h;
       f32x4 gp4;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -415,7 +498,7 @@ __global__ __launch_bounds__(256, 1) void reverse_rs_kernel(const RevArgs a) {
           if constexpr (MODE == 0) psb1 += gVar * t;  // beta1 of layer k: gVar * T_k
           ps[0] += p3; ps[1] += p2; ps[2] += pe; ps[3] += ps2; ps[4] += ps2b;
         }
-        gp4[r] = gP;
+        gp4[r] = fin(gP);
         AL[lb][r] = gLp;
         // Var of layer k: L_{k-1} + beta1_k T_k from the recomputed values (the prologue's,
         // layer K, runs past the workspace: dropped)
@@ -425,42 +508,59 @@ __global__ __launch_bounds__(256, 1) void reverse_rs_kernel(const RevArgs a) {
         bstore_s(rv, vw, vas4 + sw, vark);
         if constexpr (kAE) bstore_s(rv, vw, sw + aeo, gEp);  // adjoint of E_{k-2}
       }
-      if constexpr (MODE != 1) gpx[(b2o + lb) * 64 + lane] = gp4;
+      if constexpr (MODE != 1) {
+        gpx[(b2o + lb) * 64 + lane] = gp4;
+        xstore(rxp, b2o + lb, gp4);
+      }
     }
     });
   };
 
   // prologue BK1(K-1), then per layer G1'(k), G2'(k)
+  constexpr auto kNB = std::integral_constant<int, NB>{};
+  constexpr auto kMB = std::integral_constant<int, MB>{};
   g2_pass(std::integral_constant<int, 2>{}, K);
   flush_bk1(K - 1);
-  __syncthreads();  // gP_{K-1} complete
+  handoff(rxp, gpx, kMB);  // gP_{K-1} complete
   for (int k = K - 1; k >= 1; --k) {
     g1_pass(k);
-    __syncthreads();  // gU_k complete; every wave is done reading gP_k
+    handoff(rxu, gux, kNB);  // gU_k complete; every wave is done reading gP_k
     g2_pass(std::integral_constant<int, 0>{}, k);
     flush(k, DLADMM_P_BETA1, psb1);
     psb1 = 0.f;
     flush_bk1(k - 1);
-    __syncthreads();  // gP_{k-1} complete; every wave is done reading gU_k
+    handoff(rxp, gpx, kMB);  // gP_{k-1} complete; every wave is done reading gU_k
   }
   g1_pass(0);
-  __syncthreads();
+  handoff(rxu, gux, kNB);
   g2_pass(std::integral_constant<int, 1>{}, 0);
   flush(0, DLADMM_P_BETA1, psb1);
 }
 
-template <int EM, bool GZ, bool COT>
+template <int EM, bool GZ, bool COT, int MEM>
 hipError_t launch_rrs(const RevArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((reverse_rs_kernel<kShapeMP[2], kShapeNP[2], EM, GZ, COT>), dim3(grid),
+  hipLaunchKernelGGL((reverse_rs_kernel<kShapeMP[2], kShapeNP[2], EM, GZ, COT, MEM>), dim3(grid),
                      dim3(256), 0, s, a);
   return hipGetLastError();
 }
-template <int EM>
+template <int EM, int MEM = 1>
 hipError_t launch_rrs_em(const RevArgs& a, int grid, hipStream_t s) {
-  if (a.has_gz && a.has_cot) return launch_rrs<EM, true, true>(a, grid, s);
-  if (a.has_gz) return launch_rrs<EM, true, false>(a, grid, s);
-  if (a.has_cot) return launch_rrs<EM, false, true>(a, grid, s);
-  return launch_rrs<EM, false, false>(a, grid, s);
+  if (a.has_gz && a.has_cot) return launch_rrs<EM, true, true, MEM>(a, grid, s);
+  if (a.has_gz) return launch_rrs<EM, true, false, MEM>(a, grid, s);
+  if (a.has_cot) return launch_rrs<EM, false, true, MEM>(a, grid, s);
+  return launch_rrs<EM, false, false, MEM>(a, grid, s);
+}
+
+size_t rev_xs_group_floats() {
+  return (size_t)(kShapeNP[2] / 16 + kShapeMP[2] / 16) * 64 * 4;
+}
+
+hipError_t launch_reverse_xs(int shape, int variant, const RevArgs& a, hipStream_t s) {
+  if (!reverse_rs_supports(shape, variant) || !a.xch || !a.xcnt) return hipErrorInvalidValue;
+  const int grid = xs_grid(a.B);
+  if (variant == DLADMM_V1_LENA) return launch_rrs_em<EM_V1, 4>(a, grid, s);
+  if (variant == DLADMM_V6_LASSO) return launch_rrs_em<EM_LASSO, 4>(a, grid, s);
+  return launch_rrs_em<EM_VVAR, 4>(a, grid, s);
 }
 
 bool reverse_rs_supports(int shape, int variant) {

@@ -142,7 +142,9 @@ def test_plan_flags_select_kernels(dl):
         d.flags = f
         assert L.dladmm_fwd_path(ctypes.byref(d)) == 3
     b, _k = _bdesc(dl)
-    b.fwd.P = 1 << 40   # a saved-product forward (B = 1,000: path 5, the row-split sweep)
+    b.fwd.P = 1 << 40   # a saved-product forward (B = 1,000: path 6, the four-workgroup sweep)
+    assert L.dladmm_bwd_path(ctypes.byref(b)) == 3
+    b.fwd.flags = dl._lib.F_NO_XSPLIT   # a path-5 forward: the one-workgroup row-split sweep
     assert L.dladmm_bwd_path(ctypes.byref(b)) == 2
     b.fwd.flags = dl._lib.F_NO_ROWSPLIT   # a path-1 forward: the 64-column sweep
     assert L.dladmm_bwd_path(ctypes.byref(b)) == 1

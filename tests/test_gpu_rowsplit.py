@@ -22,6 +22,14 @@ from test_gpu_parity import _compare, _oracle_case
 pytestmark = pytest.mark.gpu
 
 
+# the scalar-parameter slots of the row-split sweeps against the 64-column sweep: the same terms
+# summed in another order (per-wave partials over a quarter -- bwd path 3: a sixteenth -- of the
+# rows, then fp64 over the waves); slots such as theta_z's sum terms that cancel, so two fp32
+# orders differ by up to ~2e-6 of the slot vector's norm.  1e-5 is the fp32 bar of the parity
+# tests.
+PSLOT_TOL = 1e-5
+
+
 def _cus():
     return torch.cuda.get_device_properties(0).multi_processor_count
 
@@ -191,11 +199,12 @@ def test_rowsplit_plan_scope(dl):
                                           ("v6", "lasso")])
 @pytest.mark.parametrize("B", [20, 25, 300])
 @pytest.mark.parametrize("gz", [False, True])
-def test_rowsplit_reverse_sweep(variant, kind, B, gz, dl):
+@pytest.mark.parametrize("split", ["xs", "rs"])
+def test_rowsplit_reverse_sweep(variant, kind, B, gz, split, dl):
     """dladmm_bwd_path 2 (the row-split reverse sweep after a path-5 forward) against the reverse
     sweep after a path-1 forward (plan flag no_rowsplit), same saved state: the weight gradients
-    bit for bit (from bit-equal gU_k / Var_k), the parameter slots within 2e-6 per layer (the
-    per-wave partials cover other element sets), with the fused objective or with Z
+    bit for bit (from bit-equal gU_k / Var_k), the parameter slots within PSLOT_TOL per layer
+    (the per-wave partials cover other element sets), with the fused objective or with Z
     cotangents (a torch-op loss over the returned Z_k, the reference's own training loop)."""
     from test_gpu_backward import make_train_net, nrel
     ops = dl.ops
@@ -214,7 +223,8 @@ def test_rowsplit_reverse_sweep(variant, kind, B, gz, dl):
     coef = (torch.rand(K, 2, device="cuda", generator=g) *
             torch.tensor([1e-2, 1.0], device="cuda")).contiguous()
     out = {}
-    for fl in (0, L.F_NO_ROWSPLIT):
+    xf, _ = _split(dl, split, B)
+    for fl in (xf, L.F_NO_ROWSPLIT):
         with torch.no_grad():
             r = ops.dladmm_forward(*args, keep_all=True, want_T=True, want_P=True, loss_kind=lk,
                                    flags=fl, **tables)
@@ -227,22 +237,23 @@ def test_rowsplit_reverse_sweep(variant, kind, B, gz, dl):
         g.manual_seed(B)   # the same cotangents / coefficients for both
         coef = (torch.rand(K, 2, device="cuda", generator=g) *
                 torch.tensor([1e-2, 1.0], device="cuda")).contiguous()
-    (fp, rs), (fp1, cl) = out[0], out[L.F_NO_ROWSPLIT]
-    assert fp in (5, 6) and fp1 == 1 and rs.path == 2 and cl.path == 1
+    (fp, rs), (fp1, cl) = out[xf], out[L.F_NO_ROWSPLIT]
+    assert fp in (5, 6) and fp1 == 1 and rs.path == fp - 3 and cl.path == 1
     assert torch.equal(rs.gW, cl.gW)
     gs_r, gs_c = rs.g_scalar.cpu().numpy(), cl.g_scalar.cpu().numpy()
     for k in range(K):
-        assert nrel(gs_r[k], gs_c[k]) <= 2e-6, (k, gs_r[k], gs_c[k])
+        assert nrel(gs_r[k], gs_c[k]) <= PSLOT_TOL, (k, gs_r[k], gs_c[k])
 
 
 @pytest.mark.parametrize("variant,kind", [("v1", "l1l1"), ("v4", "l1l1"), ("v6", "lasso")])
 @pytest.mark.parametrize("B", [20, 300])
 @pytest.mark.parametrize("cot", ["elt", "all"])
-def test_rowsplit_reverse_sweep_cotangents(variant, kind, B, cot, dl):
+@pytest.mark.parametrize("split", ["xs", "rs"])
+def test_rowsplit_reverse_sweep_cotangents(variant, kind, B, cot, split, dl):
     """The row-split reverse sweep with cotangents of E_k / L_k / T_k (main_lena.py:221-228 reads
     E and L; "all" adds Z's) and V1's per-sample betas, against the reverse sweep after a path-1
     forward: weight gradients and V1's beta gradients (per-element stores) bit for bit, the
-    scalar-parameter slots within 2e-6 per layer."""
+    scalar-parameter slots within PSLOT_TOL per layer."""
     from test_gpu_backward import make_train_net, nrel
     ops = dl.ops
     L = dl._lib
@@ -257,7 +268,8 @@ def test_rowsplit_reverse_sweep_cotangents(variant, kind, B, cot, dl):
     args = (net.VARIANT, X, net.A, W, net.Z0, net.E0, net.L0)
     lk = L.LOSS_LASSO if kind == "lasso" else L.LOSS_L1L1
     out = {}
-    for fl in (0, L.F_NO_ROWSPLIT):
+    xf, _ = _split(dl, split, B)
+    for fl in (xf, L.F_NO_ROWSPLIT):
         with torch.no_grad():
             r = ops.dladmm_forward(*args, keep_all=True, want_T=True, want_P=True, loss_kind=lk,
                                    flags=fl, **tables)
@@ -267,8 +279,8 @@ def test_rowsplit_reverse_sweep_cotangents(variant, kind, B, cot, dl):
         gE, gL, gT = rnd(m, K), rnd(m, K), rnd(m, r.T.shape[0])
         gZ = rnd(n, K) if cot == "all" else None
         out[fl] = (r.path, ops.dladmm_backward(*args, r, gZ=gZ, gE=gE, gL=gL, gT=gT, **tables))
-    (fp, rs), (fp1, cl) = out[0], out[L.F_NO_ROWSPLIT]
-    assert fp in (5, 6) and fp1 == 1 and rs.path == 2 and cl.path == 1
+    (fp, rs), (fp1, cl) = out[xf], out[L.F_NO_ROWSPLIT]
+    assert fp in (5, 6) and fp1 == 1 and rs.path == fp - 3 and cl.path == 1
     assert torch.equal(rs.gW, cl.gW)
     if variant == "v1":
         for a, b in zip(rs.g_beta1 + rs.g_beta2, cl.g_beta1 + cl.g_beta2):
@@ -276,4 +288,4 @@ def test_rowsplit_reverse_sweep_cotangents(variant, kind, B, cot, dl):
     else:
         gs_r, gs_c = rs.g_scalar.cpu().numpy(), cl.g_scalar.cpu().numpy()
         for k in range(K):
-            assert nrel(gs_r[k], gs_c[k]) <= 2e-6, (k, gs_r[k], gs_c[k])
+            assert nrel(gs_r[k], gs_c[k]) <= PSLOT_TOL, (k, gs_r[k], gs_c[k])

@@ -38,6 +38,9 @@ def main():
                          "backward runs the 64-column reverse sweep instead of its row-split form")
     ap.add_argument("--per-layer", action="store_true",
                     help="plan flag bwd_per_layer: the per-layer backward kernels")
+    ap.add_argument("--flag-set", default="",
+                    help="comma-separated forward plan flags to compare with the in-tree library "
+                         "(e.g. 0,128,64: bwd paths 3 / 2 / 1 at small batches); overrides --libs")
     a = ap.parse_args()
     dl = importlib.import_module("d-ladmm_amd")
     ops = importlib.import_module("d-ladmm_amd.ops")
@@ -52,37 +55,44 @@ def main():
         tables = net._tables(dev)
     W = [w.detach() for w in net._weights()]
     args = (net.VARIANT, X, net.A, W, net.Z0, net.E0, net.L0)
+    fls = [int(f) for f in a.flag_set.split(",")] if a.flag_set else \
+        [L.F_NO_ROWSPLIT if a.no_rowsplit else 0]
+    fwd = {}
     with torch.no_grad():
-        r = ops.dladmm_forward(*args, keep_all=True, want_T=True, want_P=True,
-                               loss_kind=L.LOSS_L1L1, flags=L.F_NO_ROWSPLIT if a.no_rowsplit else 0,
-                               **tables)
+        for fl in fls:
+            fwd[fl] = ops.dladmm_forward(*args, keep_all=True, want_T=True, want_P=True,
+                                         loss_kind=L.LOSS_L1L1, flags=fl, **tables)
     coef = torch.tensor([[1e-3 / B, 1.0 / B]] * K, device=dev)
     kw = dict(loss_kind=L.LOSS_L1L1, loss_coef=coef, **tables)
     if a.gz:
         g = torch.Generator(device=dev).manual_seed(7)
         kw = dict(gZ=[torch.randn(n, B, generator=g, device=dev) / B for _ in range(K)], **tables)
     libs = {}
-    for spec in a.libs.split(","):
+    for spec in (["main"] if a.flag_set else a.libs.split(",")):
         L._LIB = None
         L.LIB_PATH = os.path.join(ROOT, "d-ladmm_amd", "lib", "libdladmm_hip.so") \
             if spec == "main" else os.path.join(ROOT, spec)
         libs[spec] = L.lib()
-    times = {s: [] for s in libs}
+    runs = [(s, fl) for s in libs for fl in fls]
+    name = (lambda s, fl: f"fwd_flags={fl}") if a.flag_set else (lambda s, fl: s)
+    times = {name(s, fl): [] for s, fl in runs}
+    paths = {}
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for rep in range(a.reps + 1):
-        for spec, h in libs.items():
-            L._LIB = h
+        for spec, fl in runs:
+            L._LIB = libs[spec]
             torch.cuda.synchronize()
             ev0.record()
             with ops.plan_flags(bwd_per_layer=a.per_layer):
-                res = ops.dladmm_backward(*args, r, **kw)
+                res = ops.dladmm_backward(*args, fwd[fl], **kw)
             bwd_path = res.path
+            paths[name(spec, fl)] = res.path
             ev1.record()
             torch.cuda.synchronize()
             if rep:  # the first round warms every library's kernels and workspace
-                times[spec].append(ev0.elapsed_time(ev1))
+                times[name(spec, fl)].append(ev0.elapsed_time(ev1))
             del res
-    out = {s: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))}
+    out = {s: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)), "bwd_path": paths[s]}
            for s, t in times.items()}
     out["config"] = dict(m=m, n=n, K=K, B=B, reps=a.reps, rev=not a.per_layer, gz=a.gz,
                          no_rowsplit=a.no_rowsplit, bwd_path=bwd_path)
