@@ -248,7 +248,8 @@ class BackwardResult:
     g_beta1: List[torch.Tensor]       # V1: K tensors (m, B)
     g_beta2: List[torch.Tensor]
     path: int = 0                     # dladmm_bwd_path: 1 = one reverse-sweep kernel (2: its
-                                      # small-batch row-split form), 0 = per layer
+                                      # small-batch row-split form, 3: that over four
+                                      # workgroups per 16 columns), 0 = per layer
 
 
 def dladmm_backward(variant: int, X: torch.Tensor, A: torch.Tensor, W: Sequence[torch.Tensor],

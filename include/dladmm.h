@@ -277,7 +277,8 @@ size_t dladmm_bwd_workspace_bytes(const dladmm_bwd_desc* d);
    product's rows over its waves; after an fp32 path-5 / 6 forward of V1 / V4 / V5 / V6, any
    cotangents, at most one 16-column workgroup per CU: gU_k, Var_k, the weight gradients and
    V1's beta gradients bit-equal to path 1's, the scalar-parameter gradients to rounding),
-   0 = per-layer kernels,
+   3 = that form over four workgroups per 16 columns after a path-6 forward (the same
+   guarantees), 0 = per-layer kernels,
    <0 = DLADMM_E_* error.  The reverse sweep
    runs when ALL of these hold:
      - any variant V1-V6 (and the newS models built on V4 / V5);
