@@ -484,7 +484,10 @@ hipError_t launch_lena(int shape, const LenaArgs& a, int grid, hipStream_t s) {
 // ---------------------------------------------------------------------------------------------
 // Small batches (dladmm_lena_f32 at most one 16-column workgroup per CU, the 256 x 512 shape):
 // the same objective with one workgroup per 16 columns and the ROWS of each product split over
-// its 4 waves (the scheme of dladmm_fused_rs.hip).  Per layer k, wave w loads rows 4w.. of L_k
+// its 4 waves (the scheme of dladmm_fused_rs.hip).  The layers' terms are independent (each reads
+// only L_k, E_k and X), so every (16-column group, layer) pair is its own workgroup (grid
+// ceil(B / 16) x K): at the reference loop's B = 20, 30 workgroups instead of 2.  In layer k, wave
+// w loads rows 4w.. of L_k
 // into LDS (G1's B operand is all of L_k), computes G1 = A^T L_k for n blocks 8w .. 8w+7 (their
 // dual_gap sums and S = dual_gap'), hands S over through LDS, and computes G2 = A S for m blocks
 // 4w .. 4w+3 with the gL / gE epilogue and the E / L / X sums of those rows.  Same packed
@@ -552,11 +555,9 @@ __global__ __launch_bounds__(256, 1) void lena_rs_kernel(const LenaArgs a) {
     }
   };
 
-  for (int k = 0; k < K; ++k) {
-    // mode 0 has no barrier between G1 and the next layer: every wave must be done reading
-    // L_{k-1} before L_k overwrites it (the gradient modes' S barrier covers that)
-    if constexpr (!GRAD)
-      if (k > 0) __syncthreads();
+  {
+    const int k = blockIdx.y;  // this workgroup's layer
+    (void)K;
     const rsrc_t rl = mkrsrc(a.L + (int64_t)k * a.ls, mbytes);
     const rsrc_t re = mkrsrc(a.E + (int64_t)k * a.ls, mbytes);
     float Lw[MB4][4], Ew[MB4][4];
@@ -571,8 +572,7 @@ __global__ __launch_bounds__(256, 1) void lena_rs_kernel(const LenaArgs a) {
       }
       lx[(b2o + b) * 64 + lane] = lv;
     }
-    __syncthreads();  // L_k complete (and every wave is past layer k-1's reads of S)
-    if (SUMS && k > 0) flush(k - 1);
+    __syncthreads();  // L_k complete
     float se = 0.f, sdy = 0.f, sdl = 0.f, slx = 0.f;
     // ---- G1: Y = A^T L_k for this wave's n blocks
     f32x4 fa[4], fb[4];
@@ -697,18 +697,20 @@ __global__ __launch_bounds__(256, 1) void lena_rs_kernel(const LenaArgs a) {
   }
   if constexpr (SUMS) {
     __syncthreads();
-    flush(K - 1);
+    flush(blockIdx.y);
   }
 }
 
 template <int MODE>
 hipError_t launch_lena_rs_m(const LenaArgs& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((lena_rs_kernel<kShapeMP[2], kShapeNP[2], MODE>), dim3(grid), dim3(256), 0,
-                     s, a);
+  hipLaunchKernelGGL((lena_rs_kernel<kShapeMP[2], kShapeNP[2], MODE>), dim3(grid, a.K), dim3(256),
+                     0, s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_lena_rs(const LenaArgs& a, int grid, hipStream_t s) {
+  if (a.K <= 0) return hipSuccess;           // no layer, no term
+  if (a.K > 65535) return hipErrorInvalidValue;  // grid.y
   if (a.mode == 0) return launch_lena_rs_m<0>(a, grid, s);
   if (a.mode == 1) return launch_lena_rs_m<1>(a, grid, s);
   return launch_lena_rs_m<2>(a, grid, s);
