@@ -53,6 +53,10 @@ def parser():
     ap.add_argument("--lena-fused", action="store_true",
                     help="main_lena.py:221-228's loss as net.training_loss(kind='lena') (fused: "
                          "dladmm_lena_f32 + the reverse sweep with E / L cotangents), alpha 0.45")
+    ap.add_argument("--graph", action="store_true",
+                    help="also time the whole step (zero_grad, forward, loss, backward, Adam with "
+                         "capturable=True) captured once as a HIP graph and replayed (torch's "
+                         "whole-network recipe): the step without the Python / launch overhead")
     ap.add_argument("--fused-loss", action="store_true",
                     help="net.training_loss (objective fused into the kernels) instead of the "
                          "reference's torch-op loss over the returned Z_k")
@@ -79,11 +83,13 @@ def run(a) -> dict:
 
     def dual_gap(x, al):  # main_lena.py:145-147
         return torch.nn.functional.softplus(x - al) + torch.nn.functional.softplus(-x - al)
-    opt = torch.optim.Adam(net.parameters(), lr=0.005, **({"fused": True} if a.adam_fused else {}))
+    opt = torch.optim.Adam(net.parameters(), lr=0.005,
+                           **({"fused": True} if a.adam_fused else {}),
+                           **({"capturable": True} if a.graph else {}))
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
 
     def step(timed):
-        opt.zero_grad()
+        opt.zero_grad(set_to_none=not a.graph)
         if timed:
             ev[0].record()
         coeffs = [0.6 if k < K - 1 else 1.0 for k in range(K)]
@@ -162,6 +168,31 @@ def run(a) -> dict:
         "backward_frac_fp32_mfma_reference_equiv": flop_r / (med(bw) * 1e-3) / PEAK,
         "loss": float(loss.detach()),
     }
+    if a.graph:
+        # torch's whole-network recipe: warm up on a side stream, capture one step (zero_grad
+        # keeps the .grad buffers the graph writes), replay.  The eager loop's last loss keeps its
+        # autograd graph (and AccumulateGrad nodes bound to the default stream) alive: drop it
+        del loss
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                step(False)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            gl = step(False)
+        g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            g.replay()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / a.steps
+        res.update({"graph_step_ms": dt * 1e3, "graph_samples_per_s": B / dt,
+                    "graph_loss": float(gl.detach()),
+                    "graph_note": "the whole step replayed from one HIP graph (Adam "
+                                  "capturable=True; eager numbers above use the same optimizer)"})
     del opt, net
     return res
 
